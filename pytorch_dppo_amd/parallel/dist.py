@@ -1,0 +1,166 @@
+"""Process groups and the collectives that replace the reference's shared-memory IPC.
+
+Reference → here:
+
+* R1 grad sum into ``Shared_grad_buffers`` (``model.py:53-55``) + chief ``Adam.step``
+  (``chief.py:13-20``)  →  ONE all-reduce of the flat fp32 gradient
+  (:meth:`DistContext.allreduce_grads`, async so it can overlap other work), then every
+  rank applies the same fused Adam step (replicated optimizer: no parameter broadcast).
+* R2 racy shared obs-stat RMW (``model.py:71-74``) → one all-reduce of batch moments about a
+  common shift (:meth:`DistContext.allreduce_obs_moments`).
+* R3 weight reads from shared memory (``train.py:62,135``) → one broadcast at start / resume.
+* R4 Counter + TrafficLight barrier (``utils.py:4-39``) → implicit in the collective.
+* R5 ``test_n`` counter → metrics all-reduce (:meth:`DistContext.allreduce_scalars`).
+
+On GPU the backend is ``nccl`` (= RCCL on ROCm, xGMI inside a node); on CPU it is ``gloo``.
+There is no custom transport and no multi-backend dispatch on the hot path.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def enabled(self) -> bool:
+        # a world-size-1 group still runs the real collective (bench at N=1 exercises RCCL)
+        return dist.is_available() and dist.is_initialized()
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    # -- collectives -----------------------------------------------------------------------
+    def allreduce_grads(self, flat_grad: torch.Tensor, mean: bool = False, async_op: bool = False):
+        """Sum (or mean) of the flat gradient over ranks, in place.
+
+        With ``async_op`` the returned work handle's ``wait()`` orders the consumer after
+        the collective on the device stream (RCCL runs on its own stream)."""
+        if not self.enabled:
+            return None
+        work = dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, async_op=async_op)
+        if mean:
+            if async_op:
+                work.wait()
+                work = None
+            flat_grad.mul_(1.0 / self.world_size)
+        return work
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> None:
+        if self.enabled:
+            dist.broadcast(t, src=src)
+
+    def allreduce_obs_moments(self, count: float, s1: torch.Tensor, s2: torch.Tensor):
+        """global (count, S1, S2) about a shift every rank shares — exact merge (R2)."""
+        if not self.enabled:
+            return count, s1, s2
+        O = s1.numel()
+        buf = torch.empty(1 + 2 * O, dtype=torch.float64, device=self.device)
+        buf[0] = count
+        buf[1:1 + O] = s1.reshape(-1).to(self.device, torch.float64)
+        buf[1 + O:] = s2.reshape(-1).to(self.device, torch.float64)
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+        return float(buf[0].item()), buf[1:1 + O].clone(), buf[1 + O:].clone()
+
+    def allreduce_scalars(self, vals: Dict[str, float], op: str = "sum") -> Dict[str, float]:
+        if not self.enabled:
+            return dict(vals)
+        keys = sorted(vals)
+        t = torch.tensor([float(vals[k]) for k in keys], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
+        return {k: float(x) for k, x in zip(keys, t.tolist())}
+
+    def allreduce_tensor_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.enabled:
+            dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+                                   "min": dist.ReduceOp.MIN}[op])
+        return t
+
+    def verify_replicas(self, flat: torch.Tensor) -> bool:
+        """debug checksum all-reduce: True iff every rank holds bit-identical params."""
+        if not self.enabled:
+            return True
+        h = flat.detach().view(torch.int32).to(torch.int64).sum().reshape(1)
+        h = h.to(self.device)
+        lo, hi = h.clone(), h.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        return bool((lo == hi).item())
+
+    def barrier(self) -> None:
+        if self.enabled:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def destroy(self) -> None:
+        if dist.is_available() and dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def init_distributed(device: str = "cpu", rank: Optional[int] = None, world_size: Optional[int] = None,
+                     master_addr: str = "127.0.0.1", master_port: Optional[int] = None,
+                     timeout_s: float = 300.0) -> DistContext:
+    """Initialise from torchrun env vars or explicit args; one process per GPU.
+
+    GPU → backend 'nccl' (RCCL over xGMI), CPU → 'gloo'.  world_size 1 → no process group
+    unless ``force`` is wanted by a caller (RCCL at world size 1 is exercised by bench.py).
+    """
+    rank = _env_int("RANK", 0) if rank is None else rank
+    world_size = _env_int("WORLD_SIZE", 1) if world_size is None else world_size
+    local_rank = _env_int("LOCAL_RANK", rank)
+    if device == "gpu":
+        ndev = torch.cuda.device_count()
+        if ndev == 0:
+            raise RuntimeError("device=gpu but no HIP device visible")
+        torch.cuda.set_device(local_rank % ndev)
+        dev = torch.device("cuda", local_rank % ndev)
+        backend = "nccl"
+    else:
+        dev = torch.device("cpu")
+        backend = "gloo"
+    ctx = DistContext(rank=rank, world_size=world_size, local_rank=local_rank, backend=backend,
+                      device=dev)
+    if world_size > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", master_addr)
+        if master_port is not None:
+            os.environ["MASTER_PORT"] = str(master_port)
+        os.environ.setdefault("MASTER_PORT", "29531")
+        kw = dict(backend=backend, rank=rank, world_size=world_size,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    return ctx
+
+
+def init_single_rank_collective(device: torch.device, port: int = 29541) -> DistContext:
+    """A world-size-1 RCCL group so the real collective path runs on a 1-GPU box."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(port))
+    if not dist.is_initialized():
+        dist.init_process_group(backend="nccl", rank=0, world_size=1, device_id=device)
+    return DistContext(rank=0, world_size=1, local_rank=device.index or 0, backend="nccl",
+                       device=device)

@@ -1,0 +1,180 @@
+"""The DPPO worker loop (one per process / GPU): the reference's worker + chief fused.
+
+Reference roles:
+
+* ``train.py:46-178`` worker: sync weights → collect ≥1000 steps → GAE → 10 epochs of
+  {minibatch loss, backward, push grads, increment counter, spin on the traffic light},
+* ``chief.py:7-21``: poll every 1 s, when all N grads are in → Adam step → release.
+
+Here every rank runs the SAME loop: rollout → (obs-stat all-reduce) → values → GAE →
+for each epoch/minibatch {grad → all-reduce(sum) → clip → Adam}.  Because the all-reduce
+delivers the identical summed gradient to every rank and every rank applies the identical
+fused Adam step, parameters stay bit-identical without a chief process or a broadcast
+(replicated optimizer; checked by ``verify_sync_every``).  The 1 s chief poll (Q13) and the
+busy-spin (Q14) disappear: a step costs compute + one collective.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from typing import Dict, Optional
+
+import torch
+
+from ..config import Params
+from ..envs import get_spec, make_vec_env
+from ..models.actor_critic import ActorCritic
+from ..parallel.dist import DistContext
+from ..utils import rng
+from ..utils.metrics import MetricsLogger, PhaseTimer
+from ..utils.obs_stats import RunningObsStats
+
+
+def build_engine(params: Params, model, env, stats, device, action_rank):
+    if params.device == "gpu":
+        from .engine_hip import HipEngine
+        return HipEngine(params, model, env, stats, device, action_rank)
+    from .engine_torch import TorchEngine
+    return TorchEngine(params, model, env, stats, device, action_rank)
+
+
+class DPPOWorker:
+    def __init__(self, params: Params, ctx: DistContext, log: Optional[MetricsLogger] = None):
+        self.p = params
+        self.ctx = ctx
+        self.device = ctx.device
+        self.spec = get_spec(params.env_name)
+        torch.manual_seed(params.seed)          # main.py:44 — identical init on every rank
+        self.model = ActorCritic(self.spec.obs_dim, self.spec.act_dim, params.hidden,
+                                 params.value_mult).to(self.device)
+        self.ctx.broadcast_(self.model.flat.data, src=0)   # R3 once at start
+        action_rank = 0 if params.compat else ctx.rank     # Q6: reference workers share the seed
+        self.env = make_vec_env(self.spec, params.num_envs, seed=params.seed, rank=ctx.rank,
+                                device=self.device, max_episode_length=params.max_episode_length)
+        self.stats = RunningObsStats(self.spec.obs_dim, self.device)
+        self.engine = build_engine(params, self.model, self.env, self.stats, self.device, action_rank)
+        self.iteration = 0
+        self.env_steps = 0            # global (all ranks)
+        self.updates = 0
+        self.log = log
+        self.timer = PhaseTimer(self.device)
+        self._stats_initialised = False
+        self.last_metrics: Dict = {}
+        self._perm_gen = torch.Generator(device="cpu")
+
+    # ---------------------------------------------------------------------------------------
+    def _merge_stats(self, count, s1, s2, shift) -> None:
+        count, s1, s2 = self.ctx.allreduce_obs_moments(count, s1, s2)
+        self.stats.merge_moments(count, s1, s2, shift)
+
+    def init_stats(self) -> None:
+        """Seed the normaliser with the reset observations of every rank (rollout mode),
+        so the first rollout is not normalised by empty statistics."""
+        if self._stats_initialised:
+            return
+        obs = self.engine.current_obs()
+        shift = self.stats.shift().clone()
+        c, s1, s2 = RunningObsStats.moments(obs, shift)
+        self._merge_stats(c, s1, s2, shift)
+        self._stats_initialised = True
+
+    def _minibatch_plan(self):
+        N = self.engine.T * self.engine.E
+        mb = self.p.minibatch_rows()
+        nmb = self.p.num_minibatches()
+        return N, mb, nmb
+
+    def iteration_step(self) -> Dict:
+        """One DPPO iteration; returns the rank-0-relevant metrics dict."""
+        p, eng, tm = self.p, self.engine, self.timer
+        self.init_stats()
+        t0 = time.perf_counter()
+        tm.start("rollout")
+        ro = eng.rollout()
+        tm.stop("rollout")
+        tm.start("obs_stats")
+        self._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"])
+        if p.obs_norm_update == "step" and hasattr(eng, "after_stats_merge"):
+            eng.after_stats_merge()
+        tm.stop("obs_stats")
+        tm.start("values_gae")
+        eng.values()
+        eng.gae()
+        tm.stop("values_gae")
+        tm.start("update")
+        eng.begin_update()
+        N, mb, nmb = self._minibatch_plan()
+        losses = {}
+        gnorm = 0.0
+        mean = p.grad_reduce == "mean"
+        self._perm_gen.manual_seed((p.seed * 1000003 + self.ctx.rank * 7919 + self.iteration) & 0x7FFFFFFF)
+        for epoch in range(p.num_epoch):
+            if mb >= N and nmb == 1:
+                perm = None
+            else:
+                perm = torch.randperm(N, generator=self._perm_gen)
+            for b in range(nmb):
+                if perm is None:
+                    idx = None
+                else:
+                    lo = (b * mb) % N
+                    idx = perm[lo:lo + mb]
+                    if idx.numel() < mb:
+                        idx = torch.cat([idx, perm[:mb - idx.numel()]])
+                losses = eng.grad(idx)
+                self.ctx.allreduce_grads(eng.grad_flat, mean=mean)
+                extra = 0.0
+                if p.compat and self.updates == 0:
+                    extra = 1.0  # Q1: Shared_grad_buffers start at ones (model.py:51)
+                gnorm = eng.apply(extra)
+                self.updates += 1
+        tm.stop("update")
+        eng.sync()
+        dt = time.perf_counter() - t0
+        steps_local = eng.T * eng.E
+        self.env_steps += steps_local * self.ctx.world_size
+        self.iteration += 1
+        sc = self.ctx.allreduce_scalars({"ep_return_sum": ro["ep_return_sum"],
+                                         "ep_count": ro["ep_count"]})
+        m = {"iteration": self.iteration, "env_steps": self.env_steps, "updates": self.updates,
+             "iter_s": dt, "steps_per_s": steps_local * self.ctx.world_size / max(dt, 1e-9),
+             "ep_count": sc["ep_count"],
+             "mean_ep_return": (sc["ep_return_sum"] / sc["ep_count"]) if sc["ep_count"] > 0 else float("nan"),
+             "grad_norm": gnorm, **{k: v for k, v in losses.items()}, **tm.summary()}
+        if p.verify_sync_every and self.iteration % p.verify_sync_every == 0:
+            m["replicas_in_sync"] = self.ctx.verify_replicas(self.model.flat.data)
+        self.last_metrics = m
+        return m
+
+    def should_stop(self) -> bool:
+        p = self.p
+        if p.max_iters and self.iteration >= p.max_iters:
+            return True
+        if p.total_env_steps and self.env_steps >= p.total_env_steps:
+            return True
+        if self.iteration >= p.time_horizon:
+            return True
+        return False
+
+    # -- checkpoint ---------------------------------------------------------------------------
+    def trainer_state(self) -> Dict:
+        eng = self.engine
+        return {"adam_m": eng.adam_m.detach().cpu(), "adam_v": eng.adam_v.detach().cpu(),
+                "adam_step": eng.adam_step, "obs_stats": self.stats.state_dict(),
+                "iteration": self.iteration, "env_steps": self.env_steps, "updates": self.updates,
+                "config": self.p.to_dict(), "world_size": self.ctx.world_size}
+
+    def load_trainer_state(self, st: Dict) -> None:
+        eng = self.engine
+        eng.adam_m.copy_(st["adam_m"].to(eng.adam_m.device))
+        eng.adam_v.copy_(st["adam_v"].to(eng.adam_v.device))
+        eng.adam_step = int(st["adam_step"])
+        self.stats.load_state_dict(st["obs_stats"])
+        self.iteration = int(st["iteration"])
+        self.env_steps = int(st["env_steps"])
+        self.updates = int(st["updates"])
+        self._stats_initialised = True
+        if hasattr(eng, "params_changed"):
+            eng.params_changed()
