@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env steps/sec (whole node), Humanoid-v2 DPPO workers (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One DPPO worker per GPU (one process per GPU, RCCL over xGMI).  A *step* is one full DPPO
+iteration of the reference algorithm on every worker (train.py:60-178 + chief.py):
+rollout of T x E = 16 x 4096 = 65,536 env steps (Humanoid-v2 dims: obs 376, act 17, synthetic
+dynamics), value forward, GAE, then 10 epochs, each ONE synchronous global step on the full
+65,536-row batch (reference: batch_size == exploration_size, main.py:20,28), each with the
+RCCL all-reduce of the flat gradient and the fused Adam step.  Per-GPU work is fixed as N
+grows (weak scaling).  Model: the reference actor-critic (model.py), random init, bf16 MFMA
+operands with fp32 master weights/accumulation.
+
+Timing: W untimed warmup iterations; barrier + device sync; K timed iterations; barrier +
+device sync; the max over ranks of the elapsed time.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from pytorch_dppo_amd.config import dppo_preset  # noqa: E402
+from pytorch_dppo_amd.parallel.dist import init_distributed, init_single_rank_collective  # noqa: E402
+from pytorch_dppo_amd.runtime.worker import DPPOWorker  # noqa: E402
+
+METRIC = "env steps/sec (whole node), MuJoCo Humanoid-v2, 8 DPPO workers"
+# BASELINE.md derived estimate for the reference on this metric: 0.8-1.6e3 steps/s per node
+# (8 workers).  We divide by the UPPER end (conservative).
+BASELINE_VALUE = 1.6e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--env-name", default="Humanoid-v2")
+    ap.add_argument("--num-envs", type=int, default=4096)
+    ap.add_argument("--rollout-len", type=int, default=16)
+    ap.add_argument("--num-epoch", type=int, default=10)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--batch-size", type=int, default=0, help="0 = full buffer (reference DPPO)")
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        ctx = init_distributed("gpu")
+    else:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        ctx = init_single_rank_collective(dev, port=int(os.environ.get("MASTER_PORT", "29561")))
+    E, T = args.num_envs, args.rollout_len
+    rows = E * T
+    p = dppo_preset(device="gpu", env_name=args.env_name, num_envs=E, exploration_size=rows,
+                    batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=args.dtype,
+                    num_processes=ctx.world_size, seed=1)
+    w = DPPOWorker(p, ctx)
+    for i in range(args.warmup):
+        m = w.iteration_step()
+        if args.verbose and ctx.rank == 0:
+            print("warmup", i, json.dumps({k: round(v, 4) if isinstance(v, float) else v for k, v in m.items()}),
+                  file=sys.stderr, flush=True)
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        m = w.iteration_step()
+        if args.verbose and ctx.rank == 0:
+            print("step", i, json.dumps({k: round(v, 4) if isinstance(v, float) else v for k, v in m.items()}),
+                  file=sys.stderr, flush=True)
+    ctx.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], device=ctx.device, dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    total_steps = rows * ctx.world_size * args.steps
+    value = total_steps / elapsed
+    if ctx.rank == 0:
+        out = {"metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": ctx.world_size,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": value / BASELINE_VALUE,
+               "dtype": args.dtype, "data": "synthetic (Humanoid-v2 obs/act dims, random-init weights)",
+               "config": {"model": "reference actor-critic MLP (policy 376-100-100-17, value 376-500-100-1)",
+                          "global_batch": rows * ctx.world_size, "seq_len": T,
+                          "parallelism": f"dp{ctx.world_size}", "env": args.env_name, "num_envs_per_gpu": E,
+                          "rollout_len": T, "num_epoch": args.num_epoch,
+                          "minibatch_rows": p.minibatch_rows(),
+                          "last_iter": {k: m[k] for k in ("loss", "mean_ep_return", "ms_rollout", "ms_values_gae",
+                                                          "ms_update", "ms_obs_stats") if k in m}}}
+        print(json.dumps(out), flush=True)
+    ctx.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,344 @@
+// PyTorch bindings for the DPPO HIP kernels.  Every entry point validates device, dtype,
+// contiguity and the exact extents the kernel's grid/indexing assumes BEFORE launching, so
+// a shape bug raises a Python exception instead of faulting the GPU.  Launches go to the
+// current HIP stream (graph-capturable: no allocation, no sync in here).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <limits>
+#include <vector>
+
+#include "kernels.h"
+
+namespace {
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+at::ScalarType storage_type(int dt) {
+  return dt == 0 ? at::kFloat : (dt == 1 ? at::kBFloat16 : at::kByte);
+}
+
+void check(const torch::Tensor& t, const char* name, at::ScalarType st, int64_t min_numel) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a device tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
+  TORCH_CHECK(t.numel() >= min_numel, name, " has ", t.numel(), " elements, kernel needs >= ", min_numel);
+}
+
+struct Layout {
+  int off_w[6], off_wt[6], d_in[6], d_out[6], n_out[6];
+};
+
+Layout parse_layout(const std::vector<int64_t>& v) {
+  TORCH_CHECK(v.size() == 30, "layout must have 30 ints");
+  Layout L;
+  for (int i = 0; i < 6; ++i) {
+    L.off_w[i] = (int)v[i];
+    L.off_wt[i] = (int)v[6 + i];
+    L.d_in[i] = (int)v[12 + i];
+    L.d_out[i] = (int)v[18 + i];
+    L.n_out[i] = (int)v[24 + i];
+    TORCH_CHECK(L.d_in[i] % 32 == 0 && L.d_out[i] % 32 == 0, "padded dims must be multiples of 32");
+    TORCH_CHECK(L.n_out[i] < L.d_out[i], "n_out must leave a pad column");
+  }
+  return L;
+}
+
+int64_t wimg_extent(const Layout& L) {
+  int64_t mx = 0;
+  for (int i = 0; i < 6; ++i) {
+    mx = std::max<int64_t>(mx, (int64_t)L.off_w[i] + (int64_t)L.d_out[i] * L.d_in[i]);
+    mx = std::max<int64_t>(mx, (int64_t)L.off_wt[i] + (int64_t)L.d_in[i] * L.d_out[i]);
+  }
+  return mx;
+}
+
+// ------------------------------------------------------------------------------------------
+void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len, torch::Tensor ep_ret,
+             torch::Tensor wimg, std::vector<int64_t> layout, std::vector<double> scales, torch::Tensor flat,
+             torch::Tensor mean, torch::Tensor inv_std, torch::Tensor shift, torch::Tensor x_out,
+             torch::Tensor actions, torch::Tensor logp, torch::Tensor rewards, torch::Tensor dones,
+             torch::Tensor mom, torch::Tensor epstat, std::vector<int64_t> ints, std::vector<int64_t> keys,
+             double reward_clip) {
+  TORCH_CHECK(ints.size() == 11, "ints: kind,E,O,A,S,T,t_base,buf_E,t0,limit,std_var");
+  TORCH_CHECK(keys.size() == 4, "keys: env,term,reset,action");
+  TORCH_CHECK(rows == 16 || rows == 32, "rows must be 16 or 32");
+  Layout L = parse_layout(layout);
+  RolloutArgs a{};
+  a.kind = (int)ints[0]; a.E = (int)ints[1]; a.O = (int)ints[2]; a.A = (int)ints[3]; a.S = (int)ints[4];
+  a.T = (int)ints[5]; a.t_base = (int)ints[6]; a.buf_E = (int)ints[7]; a.t0 = (uint32_t)ints[8];
+  a.limit = (int)ints[9]; a.std_var = (int)ints[10];
+  TORCH_CHECK(a.E > 0 && a.T >= 1 && a.buf_E == a.E, "bad E/T");
+  TORCH_CHECK(a.kind == 0 || a.kind == 1, "kind");
+  TORCH_CHECK(a.kind == 0 ? a.S == a.O : (a.S == 2 && a.O == 3), "state dims");
+  TORCH_CHECK(L.n_out[2] == a.A && L.d_in[0] == ((a.O + 1 + 31) / 32) * 32, "layout/env mismatch");
+  const int nblk = (a.E + (int)rows - 1) / (int)rows;
+  check(state, "state", at::kFloat, (int64_t)a.E * a.S);
+  check(ep_len, "ep_len", at::kInt, a.E);
+  check(ep_ret, "ep_ret", at::kFloat, a.E);
+  check(wimg, "wimg", storage_type((int)dt), wimg_extent(L));
+  check(flat, "flat", at::kFloat, a.A);
+  check(mean, "mean", at::kFloat, a.O);
+  check(inv_std, "inv_std", at::kFloat, a.O);
+  check(shift, "shift", at::kFloat, a.O);
+  const int64_t rows_needed = (int64_t)(a.t_base + a.T + 1) * a.E;
+  check(x_out, "x_out", storage_type((int)dt), rows_needed * L.d_in[0]);
+  check(actions, "actions", at::kFloat, (int64_t)(a.t_base + a.T) * a.E * a.A);
+  check(logp, "logp", at::kFloat, (int64_t)(a.t_base + a.T) * a.E);
+  check(rewards, "rewards", at::kFloat, (int64_t)(a.t_base + a.T) * a.E);
+  check(dones, "dones", at::kFloat, (int64_t)(a.t_base + a.T) * a.E);
+  check(mom, "mom", at::kFloat, (int64_t)nblk * 2 * a.O);
+  check(epstat, "epstat", at::kFloat, (int64_t)nblk * 2);
+  a.key_env = (uint32_t)keys[0]; a.key_term = (uint32_t)keys[1]; a.key_reset = (uint32_t)keys[2];
+  a.key_action = (uint32_t)keys[3];
+  a.state = state.data_ptr<float>();
+  a.ep_len = ep_len.data_ptr<int>();
+  a.ep_ret = ep_ret.data_ptr<float>();
+  a.W = wimg.data_ptr();
+  a.off_w1 = L.off_w[0]; a.off_w2 = L.off_w[1]; a.off_w3 = L.off_w[2];
+  a.d1 = L.d_in[0]; a.d2 = L.d_in[1]; a.d3 = L.d_in[2];
+  a.n1 = L.n_out[0]; a.n2 = L.n_out[1]; a.n3 = L.n_out[2];
+  a.s1 = (float)scales.at(0); a.s2 = (float)scales.at(1); a.s3 = (float)scales.at(2);
+  a.log_std = flat.data_ptr<float>();
+  a.mean = mean.data_ptr<float>();
+  a.inv_std = inv_std.data_ptr<float>();
+  a.shift = shift.data_ptr<float>();
+  a.reward_clip = (float)reward_clip;
+  a.x_out = x_out.data_ptr();
+  a.actions = actions.data_ptr<float>();
+  a.logp = logp.data_ptr<float>();
+  a.rewards = rewards.data_ptr<float>();
+  a.dones = dones.data_ptr<float>();
+  a.mom = mom.data_ptr<float>();
+  a.epstat = epstat.data_ptr<float>();
+  launch_rollout((int)dt, a, (int)rows, cur_stream());
+}
+
+// idx_limit: exclusive upper bound every gathered row index must respect (rows of x_buf and of
+// every per-row array).  check_idx=true range-checks the index VALUES on the device (one
+// device->host read).  check_idx=false is only for callers that range-checked the indices on
+// the host before uploading them (the hipGraph-captured update path, which cannot sync).
+int64_t train_lds_bytes_impl(int dt, const Layout& L, int64_t A) {
+  MlpArgs a{};
+  for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
+  a.A = (int)A;
+  return (int64_t)mlp_train_lds_bytes(dt, a);
+}
+
+MlpArgs base_mlp(int dt, const Layout& L, const std::vector<double>& scales, torch::Tensor x_buf,
+                 torch::Tensor idx, int64_t row0, int64_t M, torch::Tensor wimg, torch::Tensor flat, int64_t A,
+                 bool check_idx, int64_t idx_limit) {
+  MlpArgs a{};
+  check(wimg, "wimg", storage_type(dt), wimg_extent(L));
+  check(flat, "flat", at::kFloat, A);
+  TORCH_CHECK(M > 0, "M must be > 0");
+  TORCH_CHECK(L.d_in[0] == L.d_in[3], "both heads share the input width");
+  const int64_t nrows_x = x_buf.numel() / L.d_in[0];
+  check(x_buf, "x_buf", storage_type(dt), 1);
+  TORCH_CHECK(x_buf.numel() % L.d_in[0] == 0, "x_buf rows must have d_in[0] elements");
+  const int64_t limit = std::min<int64_t>(idx_limit, nrows_x);
+  if (idx.defined() && idx.numel() > 0) {
+    check(idx, "idx", at::kInt, M);
+    if (check_idx) {
+      auto mm = torch::aminmax(idx.narrow(0, 0, M));
+      const int mn = std::get<0>(mm).item<int>();
+      const int mx = std::get<1>(mm).item<int>();
+      TORCH_CHECK(mn >= 0 && mx < limit, "idx values out of range [0, ", limit, "): min ", mn, " max ", mx);
+    }
+    a.idx = idx.data_ptr<int>();
+  } else {
+    a.idx = nullptr;
+    TORCH_CHECK(row0 >= 0 && row0 + M <= limit, "row range out of x_buf / per-row arrays");
+  }
+  a.x_buf = x_buf.data_ptr();
+  a.row0 = (int)row0;
+  a.M = (int)M;
+  a.W = wimg.data_ptr();
+  for (int i = 0; i < 6; ++i) {
+    a.off_w[i] = L.off_w[i]; a.off_wt[i] = L.off_wt[i]; a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i];
+    a.n_out[i] = L.n_out[i]; a.scale[i] = (float)scales.at(i);
+  }
+  a.A = (int)A;
+  a.log_std = flat.data_ptr<float>();
+  return a;
+}
+
+void mlp_value(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0, int64_t M, torch::Tensor wimg,
+               std::vector<int64_t> layout, std::vector<double> scales, torch::Tensor flat, int64_t A,
+               torch::Tensor v_out, bool check_idx) {
+  Layout L = parse_layout(layout);
+  MlpArgs a = base_mlp((int)dt, L, scales, x_buf, idx, row0, M, wimg, flat, A, check_idx,
+                       std::numeric_limits<int64_t>::max());
+  check(v_out, "v_out", at::kFloat, M);
+  a.v_out = v_out.data_ptr<float>();
+  launch_mlp_value((int)dt, a, cur_stream());
+}
+
+void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0, int64_t M, torch::Tensor wimg,
+               std::vector<int64_t> layout, std::vector<double> scales, torch::Tensor flat, torch::Tensor log_std_old,
+               int64_t A, torch::Tensor actions, torch::Tensor logp_old, torch::Tensor adv, torch::Tensor ret,
+               torch::Tensor v_old, torch::Tensor mu_prev, torch::Tensor v_prev, std::vector<int64_t> opts,
+               std::vector<double> fopts, std::vector<torch::Tensor> tbufs, int64_t ldT, torch::Tensor part,
+               bool check_idx) {
+  Layout L = parse_layout(layout);
+  TORCH_CHECK(A > 0, "A");
+  check(actions, "actions", at::kFloat, A);
+  const int64_t nrows = actions.numel() / A;
+  MlpArgs a = base_mlp((int)dt, L, scales, x_buf, idx, row0, M, wimg, flat, A, check_idx, nrows);
+  TORCH_CHECK(opts.size() == 5, "opts: loss_kind, value_loss, std_var, first_step, npart");
+  TORCH_CHECK(fopts.size() == 2, "fopts: clip, ent_coeff");
+  TORCH_CHECK(tbufs.size() == 11, "11 transposed buffers");
+  check(logp_old, "logp_old", at::kFloat, nrows);
+  check(adv, "adv", at::kFloat, nrows);
+  check(ret, "ret", at::kFloat, nrows);
+  check(v_old, "v_old", at::kFloat, nrows);
+  check(mu_prev, "mu_prev", at::kFloat, nrows * A);
+  check(v_prev, "v_prev", at::kFloat, nrows);
+  check(log_std_old, "log_std_old", at::kFloat, A);
+  const int ROWS = train_rows_for((int)dt);
+  TORCH_CHECK(train_lds_bytes_impl((int)dt, L, A) <= 160 * 1024, "mlp_train tile does not fit LDS");
+  const int64_t Mpad = ((M + ROWS - 1) / ROWS) * ROWS;
+  TORCH_CHECK(ldT >= Mpad && ldT % 32 == 0, "ldT must cover M padded to the row tile and be a multiple of 32");
+  // rows each transposed buffer must hold (writer side)
+  const int64_t need[11] = {L.d_in[0], L.d_in[1], L.d_in[2], L.d_in[4], L.d_in[5],
+                            L.n_out[0], L.n_out[1], L.n_out[2], L.n_out[3], L.n_out[4], L.n_out[5]};
+  for (int i = 0; i < 11; ++i) check(tbufs[i], "transposed buffer", storage_type((int)dt), need[i] * ldT);
+  const int npart = (int)opts[4];
+  TORCH_CHECK(npart >= 8 + A, "npart too small");
+  const int nblk = (int)(Mpad / ROWS);
+  check(part, "part", at::kFloat, (int64_t)nblk * npart);
+  a.log_std_old = log_std_old.data_ptr<float>();
+  a.actions = actions.data_ptr<float>();
+  a.logp_old = logp_old.data_ptr<float>();
+  a.adv = adv.data_ptr<float>();
+  a.ret = ret.data_ptr<float>();
+  a.v_old = v_old.data_ptr<float>();
+  a.mu_prev = mu_prev.data_ptr<float>();
+  a.v_prev = v_prev.data_ptr<float>();
+  a.loss_kind = (int)opts[0];
+  a.value_loss = (int)opts[1];
+  a.std_var = (int)opts[2];
+  a.first_step = (int)opts[3];
+  a.npart = npart;
+  a.clip = (float)fopts[0];
+  a.ent_coeff = (float)fopts[1];
+  void** dst[11] = {&a.xT, &a.h1pT, &a.h2pT, &a.h1vT, &a.h2vT, &a.g1pT, &a.g2pT, &a.g3pT, &a.g1vT, &a.g2vT, &a.g3vT};
+  for (int i = 0; i < 11; ++i) *dst[i] = tbufs[i].data_ptr();
+  a.ldT = (int)ldT;
+  a.part = part.data_ptr<float>();
+  launch_mlp_train((int)dt, a, cur_stream());
+}
+
+int64_t train_lds_bytes(int64_t dt, std::vector<int64_t> layout, int64_t A) {
+  return train_lds_bytes_impl((int)dt, parse_layout(layout), A);
+}
+
+int64_t train_rows(int64_t dt) { return train_rows_for((int)dt); }
+
+void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor> xT, std::vector<int64_t> g_rows,
+           std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab) {
+  TORCH_CHECK(gT.size() == 6 && xT.size() == 6 && g_rows.size() == 6 && x_rows.size() == 6, "6 layers");
+  check(tasks, "tasks", at::kInt, 6);
+  TORCH_CHECK(tasks.numel() % 6 == 0, "tasks are 6-int records");
+  TORCH_CHECK(!tasks_host.is_cuda() && tasks_host.numel() == tasks.numel(), "tasks_host must mirror tasks on CPU");
+  const int ntasks = (int)(tasks.numel() / 6);
+  auto th = tasks_host.contiguous();
+  const int* tp = th.data_ptr<int>();
+  int64_t slab_need = 0;
+  for (int i = 0; i < ntasks; ++i) {
+    const int* t = tp + 6 * i;
+    TORCH_CHECK(t[0] >= 0 && t[0] < 6, "task layer");
+    TORCH_CHECK(t[1] + 64 <= g_rows[t[0]] && t[2] + 64 <= x_rows[t[0]], "task tile beyond operand rows");
+    TORCH_CHECK(t[3] >= 0 && t[4] <= ld && (t[4] - t[3]) % 32 == 0 && t[3] % 32 == 0, "task batch range");
+    slab_need = std::max<int64_t>(slab_need, (int64_t)t[5] + 64 * 64);
+  }
+  check(slab, "slab", at::kFloat, slab_need);
+  WgradArgs a{};
+  for (int i = 0; i < 6; ++i) {
+    check(gT[i], "gT", storage_type((int)dt), g_rows[i] * ld);
+    check(xT[i], "xT", storage_type((int)dt), x_rows[i] * ld);
+    a.gT[i] = gT[i].data_ptr();
+    a.xT[i] = xT[i].data_ptr();
+  }
+  a.ld = (int)ld;
+  a.tasks = reinterpret_cast<const WgradTask*>(tasks.data_ptr<int>());
+  a.ntasks = ntasks;
+  a.slab = slab.data_ptr<float>();
+  launch_wgrad((int)dt, a, cur_stream());
+}
+
+void grad_gather(torch::Tensor slab, torch::Tensor src_off, int64_t nchunks, int64_t stride, torch::Tensor part,
+                 int64_t nblk, int64_t npart, int64_t A, double scale, torch::Tensor grad) {
+  const int64_t n = grad.numel();
+  check(grad, "grad", at::kFloat, n);
+  check(src_off, "src_off", at::kInt, n);
+  check(slab, "slab", at::kFloat, nchunks * stride);
+  check(part, "part", at::kFloat, nblk * npart);
+  TORCH_CHECK(npart >= 8 + A, "npart");
+  launch_grad_gather(slab.data_ptr<float>(), src_off.data_ptr<int>(), (int)nchunks, (int)stride,
+                     part.data_ptr<float>(), (int)nblk, (int)npart, (int)A, (float)scale, grad.data_ptr<float>(),
+                     (int)n, cur_stream());
+}
+
+void gae(torch::Tensor rewards, torch::Tensor values, torch::Tensor dones, torch::Tensor adv, torch::Tensor ret,
+         double gamma, double lam) {
+  TORCH_CHECK(rewards.dim() == 2, "rewards [T,E]");
+  const int64_t T = rewards.size(0), E = rewards.size(1);
+  check(rewards, "rewards", at::kFloat, T * E);
+  check(values, "values", at::kFloat, (T + 1) * E);
+  check(dones, "dones", at::kFloat, T * E);
+  check(adv, "adv", at::kFloat, T * E);
+  check(ret, "ret", at::kFloat, T * E);
+  launch_gae(rewards.data_ptr<float>(), values.data_ptr<float>(), dones.data_ptr<float>(), adv.data_ptr<float>(),
+             ret.data_ptr<float>(), (int)T, (int)E, (float)gamma, (float)lam, cur_stream());
+}
+
+void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, double lr, double b1, double b2,
+          double eps, double max_norm, torch::Tensor state, torch::Tensor norm_part, torch::Tensor wimg,
+          torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul) {
+  const int64_t n = p.numel();
+  check(p, "p", at::kFloat, n);
+  check(g, "g", at::kFloat, n);
+  check(m, "m", at::kFloat, n);
+  check(v, "v", at::kFloat, n);
+  check(state, "state", at::kFloat, 4);
+  check(w_map, "w_map", at::kInt, n);
+  check(wt_map, "wt_map", at::kInt, n);
+  check(wimg, "wimg", storage_type((int)dt), 1);
+  const int nblk = (int)norm_part.numel();
+  check(norm_part, "norm_part", at::kFloat, nblk);
+  TORCH_CHECK(nblk >= 1 && nblk <= 4096, "norm_part size");
+  const float* q = nullptr;
+  if (qmul.defined() && qmul.numel() > 0) { check(qmul, "qmul", at::kFloat, n); q = qmul.data_ptr<float>(); }
+  launch_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (int)n, (float)lr,
+              (float)b1, (float)b2, (float)eps, (float)max_norm, state.data_ptr<float>(), norm_part.data_ptr<float>(),
+              nblk, wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q, cur_stream());
+}
+
+void pack(torch::Tensor p, torch::Tensor wimg, torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul) {
+  const int64_t n = p.numel();
+  check(p, "p", at::kFloat, n);
+  check(w_map, "w_map", at::kInt, n);
+  check(wt_map, "wt_map", at::kInt, n);
+  check(wimg, "wimg", storage_type((int)dt), 1);
+  const float* q = nullptr;
+  if (qmul.defined() && qmul.numel() > 0) { check(qmul, "qmul", at::kFloat, n); q = qmul.data_ptr<float>(); }
+  launch_pack(p.data_ptr<float>(), (int)n, wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q,
+              cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X-native DPPO kernels (gfx950 HIP)";
+  m.def("rollout", &rollout);
+  m.def("mlp_value", &mlp_value);
+  m.def("mlp_train", &mlp_train);
+  m.def("train_lds_bytes", &train_lds_bytes);
+  m.def("train_rows", &train_rows);
+  m.def("wgrad", &wgrad);
+  m.def("grad_gather", &grad_gather);
+  m.def("gae", &gae);
+  m.def("adam", &adam);
+  m.def("pack", &pack);
+  m.attr("arch") = "gfx950";
+}

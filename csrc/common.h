@@ -1,0 +1,120 @@
+// Shared device helpers for the DPPO kernels (gfx950 / CDNA4, wave64).
+//
+// * Prec<DT>: one MFMA "fragment" abstraction for the three operand precisions.
+//   Every fragment holds 8 consecutive K-elements per lane: lane l owns rows/cols (l & 15)
+//   and k = 8*(l >> 4) + j, j = 0..7 — the native operand map of
+//   v_mfma_f32_16x16x32_{bf16,fp8} (cdna_hip_programming.md §3).  The fp32 path issues
+//   eight v_mfma_f32_16x16x4_f32 (exact f32) over the SAME fragment by permuting k inside
+//   the 32-deep step (both operands use the same permutation, so the sum is unchanged).
+//   C/D map (dtype independent on gfx950): col = lane & 15, row = 4*(lane >> 4) + i.
+// * counter-based RNG identical to pytorch_dppo_amd/utils/rng.py (lowbias32 + Box-Muller).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp8.h>
+#include <stdint.h>
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+
+#define DEV __device__ __forceinline__
+
+enum { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2 };
+
+template <int DT> struct Prec;
+
+template <> struct Prec<DT_F32> {
+  using T = float;
+  struct Frag { float4 lo, hi; };
+  static constexpr int BYTES = 4;
+  DEV static Frag load(const T* p) {
+    Frag f; f.lo = reinterpret_cast<const float4*>(p)[0]; f.hi = reinterpret_cast<const float4*>(p)[1];
+    return f;
+  }
+  DEV static f32x4 mma(f32x4 c, const Frag& a, const Frag& b) {
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo.x, b.lo.x, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo.y, b.lo.y, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo.z, b.lo.z, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo.w, b.lo.w, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi.x, b.hi.x, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi.y, b.hi.y, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi.z, b.hi.z, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi.w, b.hi.w, c, 0, 0, 0);
+    return c;
+  }
+  DEV static T cvt(float x) { return x; }
+  DEV static float tof(T x) { return x; }
+};
+
+template <> struct Prec<DT_BF16> {
+  using T = __bf16;
+  using Frag = bf16x8;
+  static constexpr int BYTES = 2;
+  DEV static Frag load(const T* p) { return *reinterpret_cast<const bf16x8*>(p); }
+  DEV static f32x4 mma(f32x4 c, const Frag& a, const Frag& b) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  DEV static T cvt(float x) { return (__bf16)x; }
+  DEV static float tof(T x) { return (float)x; }
+};
+
+// OCP e4m3fn (gfx950 native; NOT the MI300 fnuz encoding)
+template <> struct Prec<DT_FP8> {
+  using T = uint8_t;
+  using Frag = long;
+  static constexpr int BYTES = 1;
+  DEV static Frag load(const T* p) { return *reinterpret_cast<const long*>(p); }
+  DEV static f32x4 mma(f32x4 c, const Frag& a, const Frag& b) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
+  }
+  DEV static T cvt(float x) {
+    __hip_fp8_e4m3 q(x);
+    return *reinterpret_cast<uint8_t*>(&q);
+  }
+  DEV static float tof(T x) {
+    __hip_fp8_e4m3 q;
+    *reinterpret_cast<uint8_t*>(&q) = x;
+    return float(q);
+  }
+};
+
+// LDS row padding: one 16-byte slot per row breaks the power-of-two row stride so the 16
+// lanes of a ds_read_b128 lane group (16 rows, same k) hit distinct bank slots.
+template <int DT> struct Lds {
+  static constexpr int PAD = 16 / Prec<DT>::BYTES;
+  __host__ __device__ static constexpr int stride(int d) { return d + PAD; }
+};
+
+DEV float fast_tanh(float x) {
+  // tanh via exp: accurate to ~1 ulp of f32 for |x| < 9, saturates beyond
+  float ax = fabsf(x);
+  if (ax > 9.0f) return copysignf(1.0f, x);
+  float e = __expf(2.0f * ax);
+  float t = 1.0f - 2.0f / (e + 1.0f);
+  return copysignf(t, x);
+}
+
+// ---- counter RNG (must match utils/rng.py) -------------------------------------------------
+DEV uint32_t hash_u32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x;
+}
+DEV uint32_t keyed(uint32_t base, uint32_t env, uint32_t step, uint32_t dim) {
+  uint32_t h = hash_u32(env ^ base);
+  h = hash_u32(h ^ step);
+  return hash_u32(h ^ dim);
+}
+DEV float uniform01(uint32_t h) { return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f); }
+DEV float gauss(uint32_t base, uint32_t env, uint32_t step, uint32_t dim) {
+  float u1 = uniform01(keyed(base, env, step, 2u * dim));
+  float u2 = uniform01(keyed(base, env, step, 2u * dim + 1u));
+  return sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795864f * u2);
+}
+
+#define HIP_CHECK_LAUNCH()                                                       \
+  do {                                                                           \
+    hipError_t e__ = hipGetLastError();                                          \
+    if (e__ != hipSuccess) {                                                     \
+      fprintf(stderr, "HIP launch error %s at %s:%d\n", hipGetErrorString(e__), \
+              __FILE__, __LINE__);                                               \
+    }                                                                            \
+  } while (0)

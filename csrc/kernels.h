@@ -1,0 +1,120 @@
+// Host-visible launcher prototypes + argument structs (no torch headers: the .hip files
+// compile fast and only bindings.cpp pulls in torch).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct RolloutArgs {
+  // env (state lives in global memory between launches, in LDS during the launch)
+  int kind;            // 0 synthetic, 1 pendulum
+  int E, O, A, S;      // envs, obs dims, act dims, state dims
+  int T;               // steps in this launch
+  int t_base;          // buffer time index of the first step
+  int buf_E;           // env stride of the [T+1][E] buffers (== E)
+  uint32_t t0;         // global step counter of the first step (RNG key)
+  int limit;           // episode step limit
+  uint32_t key_env, key_term, key_reset, key_action;
+  float* state;        // [E][S]
+  int* ep_len;         // [E]
+  float* ep_ret;       // [E]
+  // policy (packed weight image, storage precision)
+  const void* W;
+  int off_w1, off_w2, off_w3;
+  int d1, d2, d3;      // padded input widths of the 3 layers (P32(K+1))
+  int n1, n2, n3;      // real output widths (H1, H2, A)
+  float s1, s2, s3;    // dequant scales (fp8; 1 otherwise)
+  const float* log_std;  // [A] fp32 master
+  int std_var;         // 1: exp(log_std) is the variance (reference DPPO), 0: it is sigma
+  // observation normalisation
+  const float* mean;
+  const float* inv_std;
+  const float* shift;
+  float reward_clip;   // <= 0: off
+  // outputs
+  void* x_out;         // [(T+1)*E][d1] storage precision (row-major, update input)
+  float* actions;      // [T][E][A]
+  float* logp;         // [T][E]
+  float* rewards;      // [T][E] (clipped)
+  float* dones;        // [T][E]
+  float* mom;          // [nblk][2][O]  sum(x-shift), sum((x-shift)^2)
+  float* epstat;       // [nblk][2]     finished-episode return sum, count
+};
+
+struct MlpArgs {
+  // input rows: x_buf row-major [*][d1]; row m of this call reads x_buf[idx ? idx[m] : row0 + m]
+  const void* x_buf;
+  const int* idx;
+  int row0;
+  int M;               // rows in this call (multiple of ROWS handled by masking)
+  // packed weights (storage precision) + offsets (elements) of Wp / Wpt per layer
+  const void* W;
+  int off_w[6];        // p1 p2 p3 v1 v2 v3 (forward images)
+  int off_wt[6];       // transposed images (dgrad)
+  int d_in[6];         // padded input width per layer
+  int d_out[6];        // padded output width per layer
+  int n_out[6];        // real output width per layer
+  float scale[6];      // fp8 dequant scale per layer
+  int A;
+  const float* log_std;  // [A]
+  const float* log_std_old;  // [A] dppo_ref: log_std of the previous step
+  // ---- training inputs (indexed by source row) ----
+  const float* actions;   // [N][A]
+  const float* logp_old;  // [N]
+  const float* adv;       // [N]
+  const float* ret;       // [N]
+  const float* v_old;     // [N]
+  float* mu_prev;         // [N][A] dppo_ref: params of the previous step (read, then overwritten)
+  float* v_prev;          // [N]
+  int loss_kind;          // 0 ppo, 1 dppo_ref
+  int value_loss;         // 0 mse, 1 clipped_half
+  int std_var;
+  float clip, ent_coeff;
+  int first_step;         // dppo_ref: 1 -> old == current
+  // ---- outputs ----
+  float* v_out;           // value-only mode: [M] (written at position m)
+  // transposed (feature-major) operands for the wgrad GEMM, [rows][ldT] storage precision
+  void* xT; void* h1pT; void* h2pT; void* h1vT; void* h2vT;
+  void* g1pT; void* g2pT; void* g3pT; void* g1vT; void* g2vT; void* g3vT;
+  int ldT;                // = M (row length of every transposed buffer)
+  float* part;            // [nblk][NPART] per-workgroup partial sums (loss terms, dlog_std)
+  int npart;
+};
+
+struct WgradTask {
+  int layer;      // 0..5
+  int n0, k0;     // output tile origin
+  int m0, m1;     // reduction (batch) range
+  int slab;       // slab offset (floats) of this task's 64x64 tile
+};
+
+struct WgradArgs {
+  const void* gT[6];   // dY^T per layer  [rows >= n tile][ld]
+  const void* xT[6];   // X^T per layer   [rows >= k tile][ld]
+  int ld;
+  const WgradTask* tasks;
+  int ntasks;
+  float* slab;
+};
+
+extern "C" {
+void launch_rollout(int dt, const RolloutArgs& a, int rows, hipStream_t s);
+void launch_mlp_value(int dt, const MlpArgs& a, hipStream_t s);
+void launch_mlp_train(int dt, const MlpArgs& a, hipStream_t s);
+size_t mlp_train_lds_bytes(int dt, const MlpArgs& a);
+void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
+void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int chunk_stride,
+                        const float* part, int nblk, int npart, int A, float scale, float* grad,
+                        int n, hipStream_t s);
+void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
+                int T, int E, float gamma, float lam, hipStream_t s);
+void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, float b1, float b2,
+                 float eps, float max_norm, float* state, float* norm_part, int nblk,
+                 void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale,
+                 hipStream_t s);
+void launch_pack(const float* p, int n, void* wimg, const int* w_map, const int* wt_map, int dt,
+                 const float* img_scale, hipStream_t s);
+}
+
+// rows per workgroup of mlp_train_kernel: the fp32 tile set does not fit 160 KiB of LDS at 32
+// rows for the Humanoid value head, so fp32 uses 16-row tiles (host side must agree).
+static inline constexpr int train_rows_for(int dt) { return dt == 0 ? 16 : 32; }

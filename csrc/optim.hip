@@ -1,0 +1,145 @@
+// GAE scan and fused Adam + global-norm clip + weight-image refresh (K12, K16).
+#include "kernels.h"
+#include "mlp_core.h"
+
+namespace {
+
+// One lane per env, reverse recurrence over T (train.py:117-122):
+//   delta_t = r_t + gamma*V_{t+1}*(1-d_t) - V_t ;  A_t = delta_t + gamma*lam*(1-d_t)*A_{t+1}
+// [T][E] layout: lanes of a wave read consecutive envs -> coalesced.
+__global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rew, const float* __restrict__ val,
+                                                  const float* __restrict__ done, float* __restrict__ adv,
+                                                  float* __restrict__ ret, int T, int E, float gamma, float lam) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= E) return;
+  float nxt = 0.f;
+  float vnext = val[(size_t)T * E + e];
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t o = (size_t)t * E + e;
+    const float nt = 1.f - done[o];
+    const float v = val[o];
+    const float delta = rew[o] + gamma * vnext * nt - v;
+    nxt = delta + gamma * lam * nt * nxt;
+    adv[o] = nxt;
+    ret[o] = nxt + v;
+    vnext = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, int n, float* __restrict__ part,
+                                                    float* __restrict__ state) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) s += g[i] * g[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = red[0];
+    if (blockIdx.x == 0) state[1] = state[0] + 1.f;  // staged step counter (graph-replay safe)
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, int n, float lr,
+                                                   float b1, float b2, float eps, float max_norm,
+                                                   float* __restrict__ state, const float* __restrict__ part,
+                                                   int nblk, typename Prec<DT>::T* __restrict__ wimg,
+                                                   const int* __restrict__ w_map, const int* __restrict__ wt_map,
+                                                   const float* __restrict__ qmul) {
+  using P = Prec<DT>;
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += 256) s += part[b];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const float norm = sqrtf(red[0]);
+  float coef = 1.f;
+  if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
+  const float step = state[1];
+  const float bc1 = 1.f - powf(b1, step);
+  const float bc2 = 1.f - powf(b2, step);
+  const float step_size = lr / bc1;
+  const float rbc2 = 1.f / sqrtf(bc2);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const float gi = g[i] * coef;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float pi = p[i] - step_size * mi / (sqrtf(vi) * rbc2 + eps);
+    p[i] = pi;
+    const int wi = w_map[i];
+    if (wi >= 0) {
+      const typename P::T q = P::cvt(qmul ? pi * qmul[i] : pi);
+      wimg[wi] = q;
+      wimg[wt_map[i]] = q;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    state[0] = step;
+    state[2] = norm;
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ p, int n,
+                                                   typename Prec<DT>::T* __restrict__ wimg,
+                                                   const int* __restrict__ w_map, const int* __restrict__ wt_map,
+                                                   const float* __restrict__ qmul) {
+  using P = Prec<DT>;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int wi = w_map[i];
+    if (wi >= 0) {
+      const typename P::T q = P::cvt(qmul ? p[i] * qmul[i] : p[i]);
+      wimg[wi] = q;
+      wimg[wt_map[i]] = q;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
+                           int T, int E, float gamma, float lam, hipStream_t s) {
+  hipLaunchKernelGGL(gae_kernel, dim3((E + 255) / 256), dim3(256), 0, s, rewards, values, dones, adv, ret, T, E,
+                     gamma, lam);
+  HIP_CHECK_LAUNCH();
+}
+
+extern "C" void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, float b1, float b2,
+                            float eps, float max_norm, float* state, float* norm_part, int nblk, void* wimg,
+                            const int* w_map, const int* wt_map, int dt, const float* img_scale, hipStream_t s) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, s, g, n, norm_part, state);
+  if (dt == DT_F32)
+    hipLaunchKernelGGL(adam_kernel<DT_F32>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
+                       state, norm_part, nblk, (float*)wimg, w_map, wt_map, img_scale);
+  else if (dt == DT_BF16)
+    hipLaunchKernelGGL(adam_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
+                       state, norm_part, nblk, (__bf16*)wimg, w_map, wt_map, img_scale);
+  else
+    hipLaunchKernelGGL(adam_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
+                       state, norm_part, nblk, (uint8_t*)wimg, w_map, wt_map, img_scale);
+  HIP_CHECK_LAUNCH();
+}
+
+extern "C" void launch_pack(const float* p, int n, void* wimg, const int* w_map, const int* wt_map, int dt,
+                            const float* img_scale, hipStream_t s) {
+  int grid = (n + 255) / 256;
+  if (grid > 1024) grid = 1024;
+  if (dt == DT_F32)
+    hipLaunchKernelGGL(pack_kernel<DT_F32>, dim3(grid), dim3(256), 0, s, p, n, (float*)wimg, w_map, wt_map, img_scale);
+  else if (dt == DT_BF16)
+    hipLaunchKernelGGL(pack_kernel<DT_BF16>, dim3(grid), dim3(256), 0, s, p, n, (__bf16*)wimg, w_map, wt_map, img_scale);
+  else
+    hipLaunchKernelGGL(pack_kernel<DT_FP8>, dim3(grid), dim3(256), 0, s, p, n, (uint8_t*)wimg, w_map, wt_map, img_scale);
+  HIP_CHECK_LAUNCH();
+}

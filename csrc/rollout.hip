@@ -1,0 +1,275 @@
+// Fused rollout kernel (SURVEY K1+K2/K3+K4+K6+K7+K8+K15): one launch collects T steps.
+//
+// Each workgroup owns ROWS envs for the whole launch.  Per step, entirely on-chip:
+//   obs (from the env state in LDS) -> running-stat moments (K2) -> normalise + clamp (K3)
+//   -> policy MLP on MFMA (K4; activations stay in LDS, weights stream from L2)
+//   -> Gaussian sample + log-prob with in-kernel counter RNG (K6-K8)
+//   -> env physics + reward clip + done/reset (K1, K15)
+// and writes the update inputs (normalised obs in the MFMA storage precision, action, logp,
+// clipped reward, done) to the HBM-resident [T][E] buffer.  The value head is NOT evaluated
+// here: V(s_t) for GAE is computed afterwards by one big batched forward over all (T+1)*E
+// rows (mlp.hip), which is far more MFMA-efficient than T small ones.
+//
+// Reference: train.py:82-106 (one env, batch 1, python loop) and model.py:68-80.
+#include "kernels.h"
+#include "mlp_core.h"
+
+namespace {
+
+constexpr float LOG_2PI_F = 1.8378770664093453f;
+constexpr float SYN_DECAY = 0.9f, SYN_DRIVE = 0.1f, SYN_NOISE = 0.05f, SYN_RESET = 0.1f;
+constexpr float SYN_TERM_P = 0.002f;
+
+DEV float env_obs(int kind, const float* st, int S, int r, int d) {
+  if (kind == 1) {  // pendulum: (cos th, sin th, thdot)
+    float th = st[r * S + 0];
+    return d == 0 ? cosf(th) : (d == 1 ? sinf(th) : st[r * S + 1]);
+  }
+  return st[r * S + d];
+}
+
+template <int DT, int ROWS>
+__global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
+  using P = Prec<DT>;
+  using T = typename P::T;
+  constexpr int NW = 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int e0 = blockIdx.x * ROWS;
+  const int nvalid = min(ROWS, a.E - e0);
+  const int O = a.O, A = a.A, S = a.S;
+  const int ld1 = Lds<DT>::stride(a.d1), ld2 = Lds<DT>::stride(a.d2), ld3 = Lds<DT>::stride(a.d3);
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  LdsCarve cv(smem);
+  float* st = cv.take<float>(ROWS * S);
+  T* xs = cv.take<T>(ROWS * ld1);
+  T* h1 = cv.take<T>(ROWS * ld2);
+  T* h2 = cv.take<T>(ROWS * ld3);
+  float* mu = cv.take<float>(ROWS * A);
+  float* act = cv.take<float>(ROWS * A);
+  float* epsb = cv.take<float>(ROWS * A);
+  float* s1 = cv.take<float>(O);
+  float* s2 = cv.take<float>(O);
+  float* done_s = cv.take<float>(ROWS);
+  int* eplen = cv.take<int>(ROWS);
+  float* epret = cv.take<float>(ROWS);
+  float* epacc = cv.take<float>(2 * ROWS);
+
+  const T* W = reinterpret_cast<const T*>(a.W);
+  const T* W1 = W + a.off_w1;
+  const T* W2 = W + a.off_w2;
+  const T* W3 = W + a.off_w3;
+  T* xo = reinterpret_cast<T*>(a.x_out);
+
+  // ---- load state, zero the padded activation tiles (pad columns stay constant) ----
+  for (int i = tid; i < ROWS * S; i += 256) {
+    int r = i / S, d = i - r * S;
+    st[i] = (r < nvalid) ? a.state[(size_t)(e0 + r) * S + d] : 0.f;
+  }
+  for (int i = tid; i < ROWS * ld2; i += 256) {
+    int c = i % ld2;
+    h1[i] = P::cvt(c == a.n1 ? 1.f : 0.f);
+  }
+  for (int i = tid; i < ROWS * ld3; i += 256) {
+    int c = i % ld3;
+    h2[i] = P::cvt(c == a.n2 ? 1.f : 0.f);
+  }
+  for (int d = tid; d < O; d += 256) { s1[d] = 0.f; s2[d] = 0.f; }
+  if (tid < ROWS) {
+    int e = e0 + tid;
+    eplen[tid] = (tid < nvalid) ? a.ep_len[e] : 0;
+    epret[tid] = (tid < nvalid) ? a.ep_ret[e] : 0.f;
+    epacc[2 * tid] = 0.f;
+    epacc[2 * tid + 1] = 0.f;
+  }
+  __syncthreads();
+
+  // sigma per action dim
+  for (int step = 0; step <= a.T; ++step) {
+    const int tb = a.t_base + step;
+    const bool last = (step == a.T);  // bootstrap observation only
+    // ---- (a) observe, moments, normalise -> LDS tile + global buffer row ----
+    for (int d = tid; d < a.d1; d += 256) {
+      float m = 0.f, is = 1.f, sh = 0.f;
+      if (d < O) { m = a.mean[d]; is = a.inv_std[d]; sh = a.shift[d]; }
+      float ls1 = 0.f, ls2 = 0.f;
+      for (int r = 0; r < ROWS; ++r) {
+        float xv;
+        if (d < O) {
+          float o = env_obs(a.kind, st, S, r, d);
+          if (!last && r < nvalid) { float dd = o - sh; ls1 += dd; ls2 += dd * dd; }
+          xv = fminf(fmaxf((o - m) * is, -5.f), 5.f);
+        } else {
+          xv = (d == O) ? 1.f : 0.f;
+        }
+        T q = P::cvt(xv);
+        xs[r * ld1 + d] = q;
+        if (r < nvalid) xo[((size_t)tb * a.buf_E + e0 + r) * a.d1 + d] = q;
+      }
+      if (d < O) { s1[d] += ls1; s2[d] += ls2; }
+    }
+    if (last) break;
+    __syncthreads();
+    // ---- (b) policy MLP ----
+    layer_gemm<DT, ROWS, NW, EPI_TANH>(xs, ld1, a.d1, W1, a.n1, h1, ld2, a.s1, wave, lane);
+    __syncthreads();
+    layer_gemm<DT, ROWS, NW, EPI_TANH>(h1, ld2, a.d2, W2, a.n2, h2, ld3, a.s2, wave, lane);
+    __syncthreads();
+    layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32>(h2, ld3, a.d3, W3, a.n3, mu, A, a.s3, wave, lane);
+    __syncthreads();
+    // ---- (c) sample a = mu + sigma * eps ----
+    const uint32_t kstep = a.t0 + (uint32_t)step;
+    for (int i = tid; i < ROWS * A; i += 256) {
+      int r = i / A, j = i - r * A;
+      float ls = a.log_std[j];
+      float lsig = a.std_var ? 0.5f * ls : ls;
+      float eps = gauss(a.key_action, (uint32_t)(e0 + r), kstep, (uint32_t)j);
+      float av = mu[i] + __expf(lsig) * eps;
+      act[i] = av;
+      epsb[i] = eps;
+      if (r < nvalid) a.actions[((size_t)tb * a.buf_E + e0 + r) * A + j] = av;
+    }
+    __syncthreads();
+    // ---- (d) per-env: logp, reward, termination, episode bookkeeping ----
+    if (tid < ROWS) {
+      const int r = tid;
+      const int e = e0 + r;
+      float lp = 0.f;
+      for (int j = 0; j < A; ++j) {
+        float ls = a.log_std[j];
+        float lsig = a.std_var ? 0.5f * ls : ls;
+        float ep = epsb[r * A + j];
+        lp += -0.5f * ep * ep - 0.5f * LOG_2PI_F - lsig;
+      }
+      float rew;
+      bool term = false;
+      if (a.kind == 1) {
+        float th = st[r * S], thd = st[r * S + 1];
+        float u = fminf(fmaxf(act[r * A], -2.f), 2.f);
+        float thn = fmodf(th + 3.14159265358979f, 6.28318530717959f);
+        if (thn < 0.f) thn += 6.28318530717959f;
+        thn -= 3.14159265358979f;
+        rew = -(thn * thn + 0.1f * thd * thd + 0.001f * u * u);
+      } else {
+        int na = min(A, O);
+        float acc = 0.f;
+        for (int j = 0; j < na; ++j) {
+          float ac = fminf(fmaxf(act[r * A + j], -1.f), 1.f);
+          float er = ac - tanhf(st[r * S + j]);
+          acc += er * er;
+        }
+        rew = 1.f - acc / (float)na;
+        term = uniform01(keyed(a.key_term, (uint32_t)e, kstep, 0u)) < SYN_TERM_P;
+      }
+      int el = eplen[r] + 1;
+      float er_ = epret[r] + rew;
+      bool done = term || (el >= a.limit);
+      if (done) {
+        if (r < nvalid) { epacc[2 * r] += er_; epacc[2 * r + 1] += 1.f; }
+        el = 0;
+        er_ = 0.f;
+      }
+      eplen[r] = el;
+      epret[r] = er_;
+      done_s[r] = done ? 1.f : 0.f;
+      if (r < nvalid) {
+        size_t o = (size_t)tb * a.buf_E + e;
+        float rc = rew;
+        if (a.reward_clip > 0.f) rc = fminf(fmaxf(rc, -a.reward_clip), a.reward_clip);
+        a.logp[o] = lp;
+        a.rewards[o] = rc;
+        a.dones[o] = done ? 1.f : 0.f;
+      }
+    }
+    __syncthreads();
+    // ---- (e) state transition (+ in-place reset on done) ----
+    if (a.kind == 1) {
+      if (tid < ROWS) {
+        const int r = tid, e = e0 + r;
+        if (done_s[r] > 0.5f) {
+          float u0 = uniform01(keyed(a.key_reset, (uint32_t)e, kstep, 0u));
+          float u1 = uniform01(keyed(a.key_reset, (uint32_t)e, kstep, 1u));
+          st[r * S] = (2.f * u0 - 1.f) * 3.14159265358979f;
+          st[r * S + 1] = 2.f * u1 - 1.f;
+        } else {
+          float th = st[r * S], thd = st[r * S + 1];
+          float u = fminf(fmaxf(act[r * A], -2.f), 2.f);
+          float nthd = thd + (-3.f * 10.f / 2.f * sinf(th + 3.14159265358979f) + 3.f * u) * 0.05f;
+          float nth = th + nthd * 0.05f;
+          nthd = fminf(fmaxf(nthd, -8.f), 8.f);
+          st[r * S] = nth;
+          st[r * S + 1] = nthd;
+        }
+      }
+    } else {
+      for (int i = tid; i < ROWS * S; i += 256) {
+        int r = i / S, d = i - r * S;
+        uint32_t e = (uint32_t)(e0 + r);
+        float ns;
+        if (done_s[r] > 0.5f) {
+          ns = SYN_RESET * gauss(a.key_reset, e, kstep, (uint32_t)d);
+        } else {
+          float w = 0.5f + (float)(d % 7) / 7.0f;
+          float ac = fminf(fmaxf(act[r * A + (d % A)], -1.f), 1.f);
+          ns = SYN_DECAY * st[i] + SYN_DRIVE * tanhf(w * ac) + SYN_NOISE * gauss(a.key_env, e, kstep, (uint32_t)d);
+        }
+        st[i] = ns;
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  // ---- write back env state, episode trackers, partial moments / episode stats ----
+  for (int i = tid; i < nvalid * S; i += 256) a.state[(size_t)e0 * S + i] = st[i];
+  if (tid < nvalid) {
+    a.ep_len[e0 + tid] = eplen[tid];
+    a.ep_ret[e0 + tid] = epret[tid];
+  }
+  float* mom = a.mom + (size_t)blockIdx.x * 2 * O;
+  for (int d = tid; d < O; d += 256) { mom[d] = s1[d]; mom[O + d] = s2[d]; }
+  if (tid == 0) {
+    float sr = 0.f, sc = 0.f;
+    for (int r = 0; r < ROWS; ++r) { sr += epacc[2 * r]; sc += epacc[2 * r + 1]; }
+    a.epstat[2 * blockIdx.x] = sr;
+    a.epstat[2 * blockIdx.x + 1] = sc;
+  }
+}
+
+template <int DT, int ROWS>
+size_t rollout_lds(const RolloutArgs& a) {
+  auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+  using T = typename Prec<DT>::T;
+  size_t b = 0;
+  b += al(sizeof(float) * ROWS * a.S);
+  b += al(sizeof(T) * ROWS * Lds<DT>::stride(a.d1));
+  b += al(sizeof(T) * ROWS * Lds<DT>::stride(a.d2));
+  b += al(sizeof(T) * ROWS * Lds<DT>::stride(a.d3));
+  b += 3 * al(sizeof(float) * ROWS * a.A);
+  b += 2 * al(sizeof(float) * a.O);
+  b += al(sizeof(float) * ROWS) + al(sizeof(int) * ROWS) + al(sizeof(float) * ROWS) + al(sizeof(float) * 2 * ROWS);
+  return b;
+}
+
+template <int DT, int ROWS>
+void launch_t(const RolloutArgs& a, hipStream_t s) {
+  size_t lds = rollout_lds<DT, ROWS>(a);
+  int nblk = (a.E + ROWS - 1) / ROWS;
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)rollout_kernel<DT, ROWS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((rollout_kernel<DT, ROWS>), dim3(nblk), dim3(256), lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+extern "C" void launch_rollout(int dt, const RolloutArgs& a, int rows, hipStream_t s) {
+  if (rows == 32) {
+    if (dt == DT_F32) launch_t<DT_F32, 32>(a, s);
+    else if (dt == DT_BF16) launch_t<DT_BF16, 32>(a, s);
+    else launch_t<DT_FP8, 32>(a, s);
+  } else {
+    if (dt == DT_F32) launch_t<DT_F32, 16>(a, s);
+    else if (dt == DT_BF16) launch_t<DT_BF16, 16>(a, s);
+    else launch_t<DT_FP8, 16>(a, s);
+  }
+}

@@ -1,0 +1,102 @@
+"""In-tree build of the HIP extension (``pytorch_dppo_amd/ops/_dppo_hip*.so``).
+
+No JIT cache, no hipify, no setuptools: each ``csrc/*.hip`` is compiled by ``hipcc
+--offload-arch=gfx950`` to an object (cached by content hash under ``build/``), the torch
+binding ``csrc/bindings.cpp`` is compiled once with the torch include paths, and everything
+is linked into one shared object next to this file, so it travels to the GPU box with the
+repo snapshot and is what ``import`` loads there.
+
+    python -m pytorch_dppo_amd.ops._build        # or: __graft_entry__.build()
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build")
+OUT_DIR = os.path.dirname(os.path.abspath(__file__))
+EXT_NAME = "_dppo_hip"
+ARCH = os.environ.get("DPPO_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+DEVICE_SRCS = ["rollout.hip", "mlp.hip", "wgrad.hip", "optim.hip"]
+HEADERS = ["common.h", "mlp_core.h", "kernels.h"]
+
+
+def ext_path() -> str:
+    return os.path.join(OUT_DIR, EXT_NAME + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _torch_flags():
+    import torch
+    from torch.utils import cpp_extension as ce
+    inc = ce.include_paths(device_type="cuda")
+    libdirs = ce.library_paths(device_type="cuda")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cflags = [f"-I{p}" for p in inc] + [f"-I{sysconfig.get_paths()['include']}",
+                                         f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+                                         f"-DTORCH_EXTENSION_NAME={EXT_NAME}",
+                                         "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1"]
+    ldflags = [f"-L{p}" for p in libdirs] + [f"-Wl,-rpath,{p}" for p in libdirs] + [
+        "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip"]
+    return cflags, ldflags
+
+
+def _digest(paths, extra: str) -> str:
+    h = hashlib.sha256(extra.encode())
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _compile(src: str, cflags, verbose: bool) -> str:
+    srcp = os.path.join(CSRC, src)
+    deps = [srcp] + [os.path.join(CSRC, h) for h in HEADERS]
+    base = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+    flags = base + cflags
+    key = _digest(deps, " ".join(flags))
+    obj = os.path.join(BUILD, f"{os.path.splitext(src)[0]}-{key}.o")
+    if os.path.exists(obj):
+        return obj
+    cmd = [HIPCC] + flags + ["-c", srcp, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+    return obj
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    tcflags, ldflags = _torch_flags()
+    jobs = [(s, []) for s in DEVICE_SRCS] + [("bindings.cpp", tcflags)]
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(lambda j: _compile(j[0], j[1], verbose), jobs))
+    out = ext_path()
+    key = _digest(objs, " ".join(ldflags))
+    stamp = out + ".stamp"
+    if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
+        return out
+    tmp = out + ".tmp.so"
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + ldflags + ["-o", tmp]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    os.replace(tmp, out)
+    with open(stamp, "w") as f:
+        f.write(key)
+    return out
+
+
+if __name__ == "__main__":
+    p = build(verbose="-v" in sys.argv, force="--force" in sys.argv)
+    print(p)

@@ -1,0 +1,305 @@
+"""HIP engine: the MI355X execution path of one DPPO worker (one process per GPU).
+
+Per iteration (all device work on the current HIP stream, no host sync until the end):
+
+  rollout   1 launch  csrc/rollout.hip   T env steps of E envs fused (norm, policy MFMA, sample,
+                                         log-prob, env physics) -> [T][E] buffer in HBM
+  values    1 launch  csrc/mlp.hip       V(s) for all (T+1)*E rows (value head on MFMA)
+  gae       1 launch  csrc/optim.hip     one lane per env reverse scan
+  per minibatch (= one synchronous global step, train.py:133-175 / chief.py:13-20):
+    grad    3 launches  mlp_train (fwd+loss+dgrad) -> wgrad (grouped split-K) -> grad_gather
+    [RCCL all-reduce of the flat fp32 gradient — done by the worker between grad and apply]
+    apply   2 launches  sumsq + fused Adam/clip that also refreshes the packed weight images
+
+The packed weight images (PackedLayout) hold every layer as [d_out][d_in] and its transpose
+in the MFMA operand precision (fp32 / bf16), the bias folded into column K.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+
+from ..config import Params
+from ..models.actor_critic import ActorCritic, PackedLayout
+from ..ops import native
+from ..utils import rng
+from ..utils.obs_stats import RunningObsStats
+
+STORAGE = {0: torch.float32, 1: torch.bfloat16, 2: torch.uint8}
+NPART_FIXED = 8
+ROLL_ROWS = 16
+
+
+def _r(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class HipEngine:
+    name = "hip"
+
+    def __init__(self, params: Params, model: ActorCritic, env, stats: RunningObsStats,
+                 device: torch.device, action_rank: int):
+        if device.type != "cuda":
+            raise RuntimeError("HipEngine needs a HIP device")
+        if params.dtype == "fp8":
+            raise NotImplementedError("fp8 GEMM path is not wired yet; use --dtype bf16|fp32")
+        self.ext = native.load()
+        self.p = params
+        self.model = model
+        self.env = env
+        self.stats = stats
+        self.device = device
+        self.dt = native.DT_CODE[params.dtype]
+        self.sdtype = STORAGE[self.dt]
+        T, E, O, A = params.rollout_len, env.E, env.O, env.A
+        self.T, self.E, self.O, self.A = T, E, O, A
+        self.N = T * E
+        L = model.packed_layout()
+        self.L = L
+        ls = L.layers
+        self.layout = ([L.w_off[l.name] for l in ls] + [L.wt_off[l.name] for l in ls] +
+                       [l.d_in for l in ls] + [l.d_out for l in ls] + [l.fan_out for l in ls])
+        self.scales = [1.0] * 6
+        dev = dict(device=device)
+        f32 = dict(device=device, dtype=torch.float32)
+        self.w_map = L.flat_to_w.to(device)
+        self.wt_map = L.flat_to_wt.to(device)
+        self.wimg = torch.zeros(L.total, dtype=self.sdtype, **dev)
+        self.d0 = ls[0].d_in
+        self.x_buf = torch.zeros((T + 1) * E, self.d0, dtype=self.sdtype, **dev)
+        self.actions = torch.zeros(self.N, A, **f32)
+        self.logp = torch.zeros(self.N, **f32)
+        self.rewards = torch.zeros(self.N, **f32)
+        self.dones = torch.zeros(self.N, **f32)
+        self.values_buf = torch.zeros((T + 1) * E, **f32)
+        self.adv = torch.zeros(self.N, **f32)
+        self.ret = torch.zeros(self.N, **f32)
+        self.mu_prev = torch.zeros(self.N, A, **f32)
+        self.v_prev = torch.zeros(self.N, **f32)
+        self.log_std_old = torch.zeros(A, **f32)
+        nroll = (E + ROLL_ROWS - 1) // ROLL_ROWS
+        self.mom = torch.zeros(nroll, 2, O, **f32)
+        self.epstat = torch.zeros(nroll, 2, **f32)
+        # ---- update geometry ----
+        self.mb = params.minibatch_rows()
+        self.ldT = _r(self.mb, 32)
+        self.train_rows = int(self.ext.train_rows(self.dt))
+        self.ntrain_blk = self.ldT // self.train_rows
+        self.npart = NPART_FIXED + A
+        self.part = torch.zeros(self.ntrain_blk, self.npart, **f32)
+        # transposed operand buffers (feature-major), heights padded to the 64-row wgrad tile
+        lp1, lp2, lmu, lv1, lv2, lv = ls
+        x_rows = [lp1.d_in, lp2.d_in, lmu.d_in, lv1.d_in, lv2.d_in, lv.d_in]
+        g_rows = [lp1.fan_out, lp2.fan_out, lmu.fan_out, lv1.fan_out, lv2.fan_out, lv.fan_out]
+        self.x_rows = [_r(r, 64) for r in x_rows]
+        self.g_rows = [_r(r, 64) for r in g_rows]
+        mk = lambda rows: torch.zeros(rows, self.ldT, dtype=self.sdtype, **dev)
+        self.xT = mk(self.x_rows[0])                       # shared by p_fc1 and v_fc1
+        self.h1pT, self.h2pT = mk(self.x_rows[1]), mk(self.x_rows[2])
+        self.h1vT, self.h2vT = mk(self.x_rows[4]), mk(self.x_rows[5])
+        self.g1pT, self.g2pT, self.g3pT = mk(self.g_rows[0]), mk(self.g_rows[1]), mk(self.g_rows[2])
+        self.g1vT, self.g2vT, self.g3vT = mk(self.g_rows[3]), mk(self.g_rows[4]), mk(self.g_rows[5])
+        self.tbufs = [self.xT, self.h1pT, self.h2pT, self.h1vT, self.h2vT,
+                      self.g1pT, self.g2pT, self.g3pT, self.g1vT, self.g2vT, self.g3vT]
+        self.wg_g = [self.g1pT, self.g2pT, self.g3pT, self.g1vT, self.g2vT, self.g3vT]
+        self.wg_x = [self.xT, self.h1pT, self.h2pT, self.xT, self.h1vT, self.h2vT]
+        self._build_wgrad_plan(model)
+        # ---- optimizer state ----
+        n = model.num_params
+        self.grad_flat = torch.zeros(n, **f32)
+        self.adam_m = torch.zeros(n, **f32)
+        self.adam_v = torch.zeros(n, **f32)
+        self.adam_state = torch.zeros(4, **f32)
+        self.adam_step = 0
+        self.norm_part = torch.zeros(min(1024, (n + 255) // 256), **f32)
+        self.idx_dev = torch.zeros(self.ldT, dtype=torch.int32, **dev)
+        self.key_action = rng.base_key(params.seed, rng.STREAM_ACTION, action_rank)
+        self.empty = torch.empty(0, dtype=torch.int32, **dev)
+        self.no_q = torch.empty(0, **f32)
+        self._first_step = True
+        self._loss_dev: Optional[torch.Tensor] = None
+        self.local_stats: Optional[RunningObsStats] = None
+        env.reset()
+        self.params_changed()
+
+    # ------------------------------------------------------------------------------------------
+    def _build_wgrad_plan(self, model: ActorCritic) -> None:
+        ls = self.L.layers
+        tiles = []  # (layer, n0, k0)
+        for li, l in enumerate(ls):
+            for n0 in range(0, l.fan_out, 64):
+                for k0 in range(0, l.fan_in + 1, 64):
+                    tiles.append((li, n0, k0))
+        ntiles = len(tiles)
+        max_chunks = max(1, self.ldT // 256)
+        nchunks = max(1, min(max_chunks, -(-1024 // ntiles)))
+        mc = _r(-(-self.ldT // nchunks), 32)
+        chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
+        self.nchunks = len(chunks)
+        self.chunk_stride = ntiles * 4096
+        tile_off = {t: i * 4096 for i, t in enumerate(tiles)}
+        tasks = []
+        for ci, (m0, m1) in enumerate(chunks):
+            for t in tiles:
+                tasks.append([t[0], t[1], t[2], m0, m1, ci * self.chunk_stride + tile_off[t]])
+        self.tasks_host = torch.tensor(tasks, dtype=torch.int32).reshape(-1).contiguous()
+        self.tasks = self.tasks_host.to(self.device)
+        self.slab = torch.zeros(self.nchunks * self.chunk_stride, device=self.device, dtype=torch.float32)
+        # flat index -> offset of its element in the chunk-0 slab
+        src = torch.full((model.num_params,), -1, dtype=torch.int64)
+        for li, l in enumerate(ls):
+            woff, wn = model.offsets[f"{l.name}.weight"]
+            nn_ = torch.arange(l.fan_out).repeat_interleave(l.fan_in)
+            kk = torch.arange(l.fan_in).repeat(l.fan_out)
+            src[woff:woff + wn] = self._slab_index(tile_off, li, nn_, kk)
+            boff, bn = model.offsets[f"{l.name}.bias"]
+            nb = torch.arange(l.fan_out)
+            src[boff:boff + bn] = self._slab_index(tile_off, li, nb, torch.full_like(nb, l.fan_in))
+        src[src < 0] = 0  # log_std entries (handled from the partials)
+        self.src_off = src.to(torch.int32).to(self.device)
+
+    @staticmethod
+    def _slab_index(tile_off, li, n, k):
+        nt, kt = int(n.max()) // 64 + 1, int(k.max()) // 64 + 1
+        lut = torch.zeros(nt, kt, dtype=torch.int64)
+        for a in range(nt):
+            for b in range(kt):
+                lut[a, b] = tile_off.get((li, a * 64, b * 64), -1)
+        base = lut[n // 64, k // 64]
+        return base + (n % 64) * 64 + (k % 64)
+
+    # ------------------------------------------------------------------------------------------
+    def params_changed(self) -> None:
+        """re-pack the weight images from the fp32 master (after init / load / broadcast)."""
+        self.ext.pack(self.model.flat.data, self.wimg, self.w_map, self.wt_map, self.dt, self.no_q)
+        self.adam_state[0] = float(self.adam_step)
+
+    def current_obs(self) -> torch.Tensor:
+        return self.env.observe()
+
+    def env_state(self) -> Dict:
+        return self.env.state_dict()
+
+    def load_env_state(self, d: Dict) -> None:
+        self.env.load_state_dict(d)
+
+    # ------------------------------------------------------------------------------------------
+    def _launch_rollout(self, T: int, t_base: int, t0: int, norm: RunningObsStats, shift: torch.Tensor):
+        e = self.env
+        kp = e.kernel_params()
+        ints = [kp["kind"], self.E, self.O, self.A, e.state_dim, T, t_base, self.E, t0 & 0xFFFFFFFF,
+                kp["limit"], 1 if self.p.std_convention == "var" else 0]
+        keys = [kp["key_env"], kp["key_term"], kp["key_reset"], self.key_action]
+        self.ext.rollout(self.dt, ROLL_ROWS, e.state, e.ep_len, e.ep_ret, self.wimg, self.layout, self.scales,
+                         self.model.flat.data, norm.mean_f32, norm.inv_std_f32, shift, self.x_buf, self.actions,
+                         self.logp, self.rewards, self.dones, self.mom, self.epstat, ints, keys,
+                         float(self.p.reward_clip))
+
+    @torch.no_grad()
+    def rollout(self) -> Dict:
+        p = self.p
+        shift = self.stats.shift().clone()
+        if p.obs_norm_update == "rollout":
+            self._launch_rollout(self.T, 0, self.env.t, self.stats, shift)
+            self.env.t += self.T
+            s1 = self.mom[:, 0].double().sum(0)
+            s2 = self.mom[:, 1].double().sum(0)
+            ep = self.epstat.double().sum(0)
+        else:
+            self.local_stats = RunningObsStats(self.O, self.device)
+            self.local_stats.copy_from(self.stats)
+            s1 = torch.zeros(self.O, dtype=torch.float64, device=self.device)
+            s2 = torch.zeros_like(s1)
+            ep = torch.zeros(2, dtype=torch.float64, device=self.device)
+            for t in range(self.T):
+                self.local_stats.observes(self.current_obs())
+                self._launch_rollout(1, t, self.env.t, self.local_stats, shift)
+                self.env.t += 1
+                s1 += self.mom[:, 0].double().sum(0)
+                s2 += self.mom[:, 1].double().sum(0)
+                ep += self.epstat.double().sum(0)
+        ep = ep.tolist()
+        return {"count": float(self.N), "s1": s1, "s2": s2, "shift": shift,
+                "ep_return_sum": float(ep[0]), "ep_count": float(ep[1])}
+
+    @torch.no_grad()
+    def values(self) -> None:
+        M = (self.T + 1) * self.E
+        self.ext.mlp_value(self.dt, self.x_buf, self.empty, 0, M, self.wimg, self.layout, self.scales,
+                           self.model.flat.data, self.A, self.values_buf, False)
+
+    @torch.no_grad()
+    def gae(self) -> None:
+        T, E = self.T, self.E
+        self.ext.gae(self.rewards.view(T, E), self.values_buf.view(T + 1, E), self.dones.view(T, E),
+                     self.adv.view(T, E), self.ret.view(T, E), float(self.p.gamma), float(self.p.gae_param))
+        if self.p.normalize_adv:
+            m, s = self.adv.mean(), self.adv.std()
+            self.adv.sub_(m).div_(s + 1e-8)
+
+    def begin_update(self) -> None:
+        self.log_std_old.copy_(self.model.flat.data[:self.A])
+        self._first_step = True
+
+    # ------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def grad(self, idx: Optional[torch.Tensor]) -> None:
+        p = self.p
+        M = self.mb
+        if idx is None:
+            idx_t, row0 = self.empty, 0
+            assert M == self.N, "full-batch call needs minibatch == buffer"
+        else:
+            idx = idx.reshape(-1)
+            if idx.numel() != M:
+                raise ValueError(f"minibatch has {idx.numel()} rows, engine was planned for {M}")
+            lo, hi = int(idx.min()), int(idx.max())
+            if lo < 0 or hi >= self.N:   # host-side range check (the launch skips the device check)
+                raise IndexError(f"minibatch indices out of range [0, {self.N}): {lo}..{hi}")
+            self.idx_dev[:M].copy_(idx.to(torch.int32), non_blocking=True)
+            idx_t, row0 = self.idx_dev, 0
+        opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
+                1 if p.std_convention == "var" else 0, 1 if self._first_step else 0, self.npart]
+        fopts = [float(p.clip), float(p.ent_coeff)]
+        self.ext.mlp_train(self.dt, self.x_buf, idx_t, row0, M, self.wimg, self.layout, self.scales,
+                           self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
+                           self.ret, self.values_buf, self.mu_prev, self.v_prev, opts, fopts, self.tbufs,
+                           self.ldT, self.part, False)
+        self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, self.tasks,
+                       self.tasks_host, self.slab)
+        self.ext.grad_gather(self.slab, self.src_off, self.nchunks, self.chunk_stride, self.part,
+                             self.ntrain_blk, self.npart, self.A, 1.0 / M, self.grad_flat)
+        if p.loss == "dppo_ref":
+            self.log_std_old.copy_(self.model.flat.data[:self.A])  # train.py:164
+        self._first_step = False
+        self._loss_dev = self.part[:, :NPART_FIXED].sum(0)
+        return None
+
+    @torch.no_grad()
+    def apply(self, extra_grad: float = 0.0) -> None:
+        p = self.p
+        if extra_grad:
+            self.grad_flat.add_(extra_grad)
+        mx = float(p.max_grad_norm) if (p.max_grad_norm is not None and p.max_grad_norm > 0) else 0.0
+        b1, b2 = p.adam_betas
+        self.ext.adam(self.model.flat.data, self.grad_flat, self.adam_m, self.adam_v, float(p.lr), float(b1),
+                      float(b2), float(p.adam_eps), mx, self.adam_state, self.norm_part, self.wimg, self.w_map,
+                      self.wt_map, self.dt, self.no_q)
+        self.adam_step += 1
+        return None
+
+    def last_losses(self) -> Dict[str, float]:
+        if self._loss_dev is None:
+            return {}
+        v = self._loss_dev.tolist()
+        n = max(v[5], 1.0)
+        out = {"loss_clip": v[0] / n, "loss_value": v[1] / n, "loss_ent": v[2] / n,
+               "approx_kl": v[3] / n, "clipfrac": v[4] / n}
+        out["loss"] = out["loss_clip"] + out["loss_value"] + out["loss_ent"]
+        out["grad_norm"] = float(self.adam_state[2])
+        return out
+
+    def sync(self) -> None:
+        torch.cuda.synchronize(self.device)

@@ -157,7 +157,8 @@ class TorchEngine:
             self.flat_old.copy_(self.model.flat.detach())
         out["loss"].backward()
         self.grad_flat.copy_(self.model.flat.grad)
-        return {k: float(v.detach()) for k, v in out.items()}
+        self._last = {k: float(v.detach()) for k, v in out.items()}
+        return self._last
 
     @torch.no_grad()
     def apply(self, extra_grad: float = 0.0) -> float:
@@ -171,7 +172,13 @@ class TorchEngine:
         self.adam_step += 1
         oracle.adam_step_(self.model.flat.data, g, self.adam_m, self.adam_v, self.adam_step,
                           self.p.lr, self.p.adam_betas, self.p.adam_eps)
+        self._norm = norm
         return norm
+
+    def last_losses(self) -> Dict[str, float]:
+        out = dict(getattr(self, "_last", {}))
+        out["grad_norm"] = getattr(self, "_norm", 0.0)
+        return out
 
     def sync(self) -> None:
         pass

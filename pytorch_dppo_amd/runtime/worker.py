@@ -123,15 +123,17 @@ class DPPOWorker:
                     idx = perm[lo:lo + mb]
                     if idx.numel() < mb:
                         idx = torch.cat([idx, perm[:mb - idx.numel()]])
-                losses = eng.grad(idx)
+                eng.grad(idx)
                 self.ctx.allreduce_grads(eng.grad_flat, mean=mean)
                 extra = 0.0
                 if p.compat and self.updates == 0:
                     extra = 1.0  # Q1: Shared_grad_buffers start at ones (model.py:51)
-                gnorm = eng.apply(extra)
+                eng.apply(extra)
                 self.updates += 1
         tm.stop("update")
         eng.sync()
+        losses = eng.last_losses()
+        gnorm = losses.pop("grad_norm", 0.0)
         dt = time.perf_counter() - t0
         steps_local = eng.T * eng.E
         self.env_steps += steps_local * self.ctx.world_size

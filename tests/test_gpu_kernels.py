@@ -1,0 +1,285 @@
+"""HIP kernel numerics vs the plain-PyTorch fp32 oracle (SURVEY §4 'Unit: HIP kernels').
+
+fp32 operands run the exact-f32 MFMA path (v_mfma_f32_16x16x4_f32) -> tight tolerances;
+bf16 operands -> loose, relative budgets.  Shapes cover Pendulum (3/1), HalfCheetah (17/6)
+and Humanoid (376/17) dims with odd E and padded tails.
+"""
+import math
+
+import pytest
+import torch
+
+from pytorch_dppo_amd.config import Params, dppo_preset, ppo_preset
+from pytorch_dppo_amd.envs import get_spec, make_vec_env
+from pytorch_dppo_amd.models.actor_critic import ActorCritic
+from pytorch_dppo_amd.ops import oracle
+from pytorch_dppo_amd.utils.obs_stats import RunningObsStats
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0) if torch.cuda.is_available() else None
+
+
+def _ext():
+    from pytorch_dppo_amd.ops import native
+    return native.load()
+
+
+def _model(O, A, hidden=(100, 100), seed=0):
+    torch.manual_seed(seed)
+    m = ActorCritic(O, A, hidden).to(DEV)
+    with torch.no_grad():
+        m.flat.data[:A] = torch.linspace(-0.5, 0.3, A, device=DEV)  # non-trivial log_std
+    return m
+
+
+def _engine(params, seed=0):
+    from pytorch_dppo_amd.runtime.engine_hip import HipEngine
+    spec = get_spec(params.env_name)
+    torch.manual_seed(seed)
+    model = ActorCritic(spec.obs_dim, spec.act_dim, params.hidden).to(DEV)
+    env = make_vec_env(spec, params.num_envs, seed=params.seed, device=DEV)
+    stats = RunningObsStats(spec.obs_dim, DEV)
+    return HipEngine(params, model, env, stats, DEV, 0), model, env, stats
+
+
+def test_extension_loads_for_gfx950():
+    ext = _ext()
+    assert ext.arch == "gfx950"
+    assert ext.__file__.endswith(".so")
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_pack_matches_reference_layout(dtype):
+    p = dppo_preset(device="gpu", env_name="HalfCheetah-v2", num_envs=64, exploration_size=256,
+                    batch_size=256, dtype=dtype)
+    eng, model, _, _ = _engine(p)
+    ref = model.packed_layout().pack(model.flat.data, eng.sdtype)
+    assert torch.equal(eng.wimg.float(), ref.float())
+
+
+@pytest.mark.parametrize("env_name,dtype,tol", [("Pendulum-v0", "fp32", 2e-5), ("HalfCheetah-v2", "fp32", 2e-5),
+                                                ("Humanoid-v2", "fp32", 5e-5), ("Humanoid-v2", "bf16", 3e-2)])
+def test_value_forward(env_name, dtype, tol):
+    p = dppo_preset(device="gpu", env_name=env_name, num_envs=37, exploration_size=37 * 5,
+                    batch_size=37 * 5, dtype=dtype)
+    eng, model, _, _ = _engine(p)
+    O = model.num_inputs
+    M = (eng.T + 1) * eng.E
+    x = torch.randn(M, O, device=DEV).clamp(-5, 5)
+    xb = torch.zeros(M, eng.d0, device=DEV)
+    xb[:, :O] = x
+    xb[:, O] = 1.0
+    eng.x_buf.copy_(xb.to(eng.sdtype))
+    eng.values()
+    with torch.no_grad():
+        _, _, v = model(eng.x_buf[:, :O].float())
+    err = (eng.values_buf - v.reshape(-1)).abs().max().item()
+    scale = v.abs().max().item() + 1e-3
+    assert err / scale < tol, (err, scale)
+
+
+def _torch_rollout(params, model, seed_state_from):
+    from pytorch_dppo_amd.runtime.engine_torch import TorchEngine
+    spec = get_spec(params.env_name)
+    env = make_vec_env(spec, params.num_envs, seed=params.seed, device=DEV)
+    stats = RunningObsStats(spec.obs_dim, DEV)
+    stats.copy_from(seed_state_from)
+    eng = TorchEngine(params, model, env, stats, DEV, 0)
+    return eng
+
+
+@pytest.mark.parametrize("env_name", ["Pendulum-v0", "HalfCheetah-v2", "Humanoid-v2"])
+def test_rollout_matches_torch_engine(env_name):
+    p = dppo_preset(device="gpu", env_name=env_name, num_envs=45, exploration_size=45 * 8,
+                    batch_size=45 * 8, dtype="fp32")
+    eng, model, env, stats = _engine(p)
+    stats.observes(env.observe())
+    with torch.no_grad():
+        model.flat.data[:model.num_outputs] = -0.3
+    eng.params_changed()
+    p_cpu = Params.from_dict({**p.to_dict(), "device": "cpu"})
+    ref = _torch_rollout(p_cpu, model, stats)
+    ro_h = eng.rollout()
+    ro_t = ref.rollout()
+    T, E = eng.T, eng.E
+    O = model.num_inputs
+    assert torch.allclose(eng.actions.view(T, E, -1), ref.actions, atol=2e-4, rtol=1e-4)
+    assert torch.allclose(eng.logp.view(T, E), ref.logp, atol=1e-4, rtol=1e-5)
+    assert torch.allclose(eng.rewards.view(T, E), ref.rewards, atol=2e-4, rtol=1e-4)
+    assert torch.equal(eng.dones.view(T, E), ref.dones)
+    xk = eng.x_buf.float().view(T + 1, E, -1)[..., :O]
+    assert torch.allclose(xk, ref.x, atol=2e-4, rtol=1e-4)
+    assert torch.allclose(env.state, ref.env.state, atol=2e-4, rtol=1e-4)
+    assert torch.allclose(ro_h["s1"], ro_t["s1"], rtol=1e-4, atol=1e-2)
+    assert abs(ro_h["ep_count"] - ro_t["ep_count"]) < 0.5
+
+
+def test_gae_kernel_matches_oracle():
+    ext = _ext()
+    T, E = 33, 1031
+    r = torch.randn(T, E, device=DEV)
+    v = torch.randn(T + 1, E, device=DEV)
+    d = (torch.rand(T, E, device=DEV) < 0.05).float()
+    adv = torch.empty(T, E, device=DEV)
+    ret = torch.empty(T, E, device=DEV)
+    ext.gae(r, v, d, adv, ret, 0.99, 0.95)
+    a_ref, r_ref = oracle.gae(r, v, d, 0.99, 0.95)
+    assert torch.allclose(adv, a_ref, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(ret, r_ref, atol=1e-5, rtol=1e-5)
+
+
+def _fill_buffer(eng, model, gen_seed=3):
+    g = torch.Generator(device="cpu").manual_seed(gen_seed)
+    N, O, A = eng.N, model.num_inputs, model.num_outputs
+    x = torch.randn(N + eng.E, O, generator=g).clamp(-5, 5).to(DEV)
+    xb = torch.zeros(N + eng.E, eng.d0, device=DEV)
+    xb[:, :O] = x
+    xb[:, O] = 1.0
+    eng.x_buf.copy_(xb.to(eng.sdtype))
+    xq = eng.x_buf.float()[:N, :O]
+    with torch.no_grad():
+        mu, ls, v = model(xq)
+    a = (mu + 0.6 * torch.randn(N, A, generator=g).to(DEV))
+    eng.actions.copy_(a)
+    sig = torch.exp(ls if eng.p.std_convention == "std" else 0.5 * ls)
+    logp_old = oracle.gaussian_logp(a, mu + 0.05 * torch.randn(N, A, generator=g).to(DEV), ls, eng.p.std_convention)
+    eng.logp.copy_(logp_old.reshape(-1))
+    eng.adv.copy_(torch.randn(N, generator=g).to(DEV))
+    eng.ret.copy_((v.reshape(-1) + 0.5 * torch.randn(N, generator=g).to(DEV)))
+    eng.values_buf[:N].copy_(v.reshape(-1) + 0.3 * torch.randn(N, generator=g).to(DEV))
+    return xq
+
+
+def _torch_grad(model, p, xq, eng, idx):
+    x = xq[idx]
+    model.flat.grad = None
+    mu, ls, v = model(x)
+    out = oracle.ppo_loss(mu, ls, v, eng.actions[idx], eng.logp[idx], eng.adv[idx], eng.ret[idx],
+                          eng.values_buf[:eng.N][idx], clip=p.clip, ent_coeff=p.ent_coeff,
+                          value_loss=p.value_loss, convention=p.std_convention)
+    out["loss"].backward()
+    return model.flat.grad.detach().clone(), out
+
+
+@pytest.mark.parametrize("env_name,dtype,value_loss,conv,mb,tol", [
+    ("HalfCheetah-v2", "fp32", "mse", "std", 256, 1e-4),
+    ("HalfCheetah-v2", "fp32", "clipped_half", "var", 200, 1e-4),
+    ("Humanoid-v2", "fp32", "clipped_half", "std", 512, 2e-4),
+    ("Humanoid-v2", "bf16", "mse", "std", 512, 6e-2),
+    ("Pendulum-v0", "fp32", "mse", "std", 64, 1e-4),
+])
+def test_fused_loss_backward_matches_autograd(env_name, dtype, value_loss, conv, mb, tol):
+    p = ppo_preset(device="gpu", env_name=env_name, num_envs=64, exploration_size=64 * 8,
+                   batch_size=mb, dtype=dtype, value_loss=value_loss, std_convention=conv, ent_coeff=0.01)
+    eng, model, _, _ = _engine(p)
+    with torch.no_grad():
+        model.flat.data[:model.num_outputs] = torch.linspace(-0.4, 0.2, model.num_outputs, device=DEV)
+    eng.params_changed()
+    xq = _fill_buffer(eng, model)
+    idx = torch.randperm(eng.N, generator=torch.Generator().manual_seed(5))[:mb]
+    eng.begin_update()
+    eng.grad(idx)
+    g_ref, out = _torch_grad(model, p, xq, eng, idx.to(DEV))
+    g = eng.grad_flat
+    rel = (g - g_ref).norm().item() / (g_ref.norm().item() + 1e-12)
+    assert rel < tol, rel
+    ll = eng.last_losses()
+    assert abs(ll["loss_clip"] - out["loss_clip"].item()) < max(5e-3, 50 * tol) * (1 + abs(out["loss_clip"].item()))
+    assert abs(ll["loss_value"] - out["loss_value"].item()) < max(5e-3, 50 * tol) * (1 + abs(out["loss_value"].item()))
+
+
+def test_dppo_ref_loss_two_steps_matches_autograd():
+    p = dppo_preset(device="gpu", env_name="HalfCheetah-v2", num_envs=32, exploration_size=256,
+                    batch_size=256, dtype="fp32", loss="dppo_ref", ent_coeff=0.01)
+    eng, model, _, _ = _engine(p)
+    xq = _fill_buffer(eng, model)
+    eng.begin_update()
+    old_flat = model.flat.data.clone()
+    eng.grad(None)
+    # step 1: old == current
+    x = xq
+    model.flat.grad = None
+    mu, ls, v = model(x)
+    out = oracle.dppo_ref_loss(mu, ls, v, mu.detach(), ls.detach(), v.detach(), eng.actions, eng.adv, eng.ret,
+                               clip=p.clip, ent_coeff=p.ent_coeff)
+    out["loss"].backward()
+    rel = (eng.grad_flat - model.flat.grad).norm() / model.flat.grad.norm()
+    assert rel < 1e-4
+    eng.apply()
+    # step 2: old = params of step 1
+    eng.grad(None)
+    model.flat.grad = None
+    mu, ls, v = model(x)
+    from pytorch_dppo_amd.runtime.engine_torch import _forward_with
+    with torch.no_grad():
+        mu_o, ls_o, v_o = _forward_with(model, old_flat, x)
+    out = oracle.dppo_ref_loss(mu, ls, v, mu_o, ls_o, v_o, eng.actions, eng.adv, eng.ret,
+                               clip=p.clip, ent_coeff=p.ent_coeff)
+    out["loss"].backward()
+    rel = (eng.grad_flat - model.flat.grad).norm() / model.flat.grad.norm()
+    assert rel < 2e-4
+
+
+@pytest.mark.parametrize("max_norm", [0.0, 0.5])
+def test_adam_kernel_matches_oracle(max_norm):
+    p = ppo_preset(device="gpu", env_name="HalfCheetah-v2", num_envs=16, exploration_size=128,
+                   batch_size=128, dtype="fp32", max_grad_norm=max_norm or None)
+    eng, model, _, _ = _engine(p)
+    n = model.num_params
+    p_ref = model.flat.data.clone()
+    m_ref = torch.zeros(n, device=DEV)
+    v_ref = torch.zeros(n, device=DEV)
+    for step in range(1, 4):
+        g = torch.randn(n, device=DEV) * 0.3
+        eng.grad_flat.copy_(g)
+        eng.apply()
+        gr = g.clone()
+        if max_norm:
+            oracle.clip_grad_norm_(gr, max_norm)
+        oracle.adam_step_(p_ref, gr, m_ref, v_ref, step, p.lr, p.adam_betas, p.adam_eps)
+    assert torch.allclose(model.flat.data, p_ref, atol=1e-6, rtol=1e-5)
+    ref_img = model.packed_layout().pack(model.flat.data, eng.sdtype)
+    assert torch.equal(eng.wimg, ref_img)
+
+
+def test_engine_iteration_matches_torch_engine_fp32():
+    """Full iteration (rollout -> values -> GAE -> 2 full-batch steps) HIP vs torch oracle."""
+    from pytorch_dppo_amd.parallel.dist import DistContext
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    common = dict(env_name="HalfCheetah-v2", num_envs=48, exploration_size=48 * 6, batch_size=48 * 6,
+                  num_epoch=2, dtype="fp32", max_iters=1)
+    pg = dppo_preset(device="gpu", **common)
+    pc = dppo_preset(device="cpu", **common)
+    wg = DPPOWorker(pg, DistContext(device=DEV))
+    wc = DPPOWorker(pc, DistContext(device=torch.device("cpu")))
+    assert torch.equal(wg.model.flat.data.cpu(), wc.model.flat.data)
+    mg = wg.iteration_step()
+    mc = wc.iteration_step()
+    d = (wg.model.flat.data.cpu() - wc.model.flat.data).abs()
+    # Adam moves every element by ~lr per step whatever the gradient magnitude, so elements
+    # whose true gradient is ~0 may legitimately differ by up to 2*lr*steps; the bulk must agree.
+    assert d.max().item() <= 2 * pg.lr * pg.num_epoch + 1e-6
+    assert (d > 1e-5).float().mean().item() < 0.01
+    assert abs(mg["loss_value"] - mc["loss_value"]) < 1e-3 * (1 + abs(mc["loss_value"]))
+
+
+def test_rccl_world1_allreduce_and_training_step():
+    """The real RCCL collective path at world size 1 (the 1-GPU box): grads, obs moments."""
+    import torch.distributed as dist
+    from pytorch_dppo_amd.parallel.dist import init_single_rank_collective
+    from pytorch_dppo_amd.runtime.launcher import free_port
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    ctx = init_single_rank_collective(DEV, port=free_port())
+    try:
+        g = torch.arange(1000, device=DEV, dtype=torch.float32)
+        ctx.allreduce_grads(g)
+        assert torch.equal(g, torch.arange(1000, device=DEV, dtype=torch.float32))
+        p = dppo_preset(device="gpu", env_name="Walker2d-v2", num_envs=64, exploration_size=64 * 4,
+                        batch_size=128, num_epoch=2, dtype="bf16", verify_sync_every=1)
+        w = DPPOWorker(p, ctx)
+        m = w.iteration_step()
+        assert m["replicas_in_sync"] is True
+        assert math.isfinite(m["loss"]) and m["updates"] == 4
+    finally:
+        dist.destroy_process_group()
