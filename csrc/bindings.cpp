@@ -247,9 +247,9 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
   for (int i = 0; i < ntasks; ++i) {
     const int* t = tp + 6 * i;
     TORCH_CHECK(t[0] >= 0 && t[0] < 6, "task layer");
-    TORCH_CHECK(t[1] + 64 <= g_rows[t[0]] && t[2] + 64 <= x_rows[t[0]], "task tile beyond operand rows");
+    TORCH_CHECK(t[1] + WGRAD_TILE <= g_rows[t[0]] && t[2] + WGRAD_TILE <= x_rows[t[0]], "task tile beyond operand rows");
     TORCH_CHECK(t[3] >= 0 && t[4] <= ld && (t[4] - t[3]) % 32 == 0 && t[3] % 32 == 0, "task batch range");
-    slab_need = std::max<int64_t>(slab_need, (int64_t)t[5] + 64 * 64);
+    slab_need = std::max<int64_t>(slab_need, (int64_t)t[5] + WGRAD_TILE * WGRAD_TILE);
   }
   check(slab, "slab", at::kFloat, slab_need);
   WgradArgs a{};

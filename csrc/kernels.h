@@ -118,3 +118,6 @@ void launch_pack(const float* p, int n, void* wimg, const int* w_map, const int*
 // rows per workgroup of mlp_train_kernel: the fp32 tile set does not fit 160 KiB of LDS at 32
 // rows for the Humanoid value head, so fp32 uses 16-row tiles (host side must agree).
 static inline constexpr int train_rows_for(int dt) { return dt == 0 ? 16 : 32; }
+
+// output tile (square) of one wgrad task; operand buffers are padded to multiples of it
+#define WGRAD_TILE 128

@@ -69,6 +69,18 @@ DEV void write_transposed(const typename Prec<DT>::T* tile, int ld, int nfeat, v
   }
 }
 
+// bytes of the shared region that first holds X, then H2p | H2v | DMU | DV
+template <int DT, int ROWS>
+__host__ __device__ size_t train_region_bytes(const MlpArgs& a) {
+  using T = typename Prec<DT>::T;
+  const size_t x = al16(sizeof(T) * ROWS * Lds<DT>::stride(a.d_in[0]));
+  const size_t rest = al16(sizeof(T) * ROWS * Lds<DT>::stride(a.d_in[2])) +
+                      al16(sizeof(T) * ROWS * Lds<DT>::stride(a.d_in[5])) +
+                      al16(sizeof(T) * ROWS * Lds<DT>::stride(a.d_out[2])) +
+                      al16(sizeof(T) * ROWS * Lds<DT>::stride(a.d_out[5]));
+  return x > rest ? x : rest;
+}
+
 template <int DT, int ROWS>
 __global__ __launch_bounds__(256) void mlp_value_kernel(MlpArgs a) {
   using P = Prec<DT>;
@@ -117,15 +129,20 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(MlpArgs a) {
   const int ldmu = Lds<DT>::stride(a.d_out[2]);
   const int ldv = Lds<DT>::stride(a.d_out[5]);
 
+  // LDS plan: X is dead after the two first layers, so H2p/H2v/DMU/DV live inside X's region
+  // (train_lds sizes the region as the max of the two uses) -> 2 workgroups per CU at bf16.
   extern __shared__ __attribute__((aligned(16))) char smem[];
   LdsCarve cv(smem);
-  T* X = cv.take<T>(ROWS * ldx);
+  char* region = cv.base;
+  cv.off = train_region_bytes<DT, ROWS>(a);
+  T* X = reinterpret_cast<T*>(region);
+  LdsCarve rc(region);
+  T* H2p = rc.take<T>(ROWS * ld2p);
+  T* H2v = rc.take<T>(ROWS * ld2v);
+  T* DMU = rc.take<T>(ROWS * ldmu);
+  T* DV = rc.take<T>(ROWS * ldv);
   T* H1p = cv.take<T>(ROWS * ld1p);
-  T* H2p = cv.take<T>(ROWS * ld2p);
   T* H1v = cv.take<T>(ROWS * ld1v);
-  T* H2v = cv.take<T>(ROWS * ld2v);
-  T* DMU = cv.take<T>(ROWS * ldmu);
-  T* DV = cv.take<T>(ROWS * ldv);
   float* MU = cv.take<float>(ROWS * A);
   float* V = cv.take<float>(ROWS);
   float* DLS = cv.take<float>(ROWS * A);
@@ -134,16 +151,18 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(MlpArgs a) {
   const T* W = reinterpret_cast<const T*>(a.W);
   load_rows<DT>(reinterpret_cast<const T*>(a.x_buf), a.idx, a.row0, m0, nvalid, a.d_in[0], X, ldx, ROWS, tid);
   preset_tile<DT>(H1p, ld1p, ROWS, a.n_out[0], tid);
-  preset_tile<DT>(H2p, ld2p, ROWS, a.n_out[1], tid);
   preset_tile<DT>(H1v, ld1v, ROWS, a.n_out[3], tid);
-  preset_tile<DT>(H2v, ld2v, ROWS, a.n_out[4], tid);
-  preset_tile<DT>(DMU, ldmu, ROWS, -1, tid);
-  preset_tile<DT>(DV, ldv, ROWS, -1, tid);
   __syncthreads();
   // ---------------- forward ----------------
   write_transposed<DT, ROWS>(X, ldx, a.d_in[0], a.xT, a.ldT, m0, tid);
   layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[0], W + a.off_w[0], a.n_out[0], H1p, ld1p, a.scale[0], wave, lane);
   layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1v, ld1v, a.scale[3], wave, lane);
+  __syncthreads();
+  // X is dead: preset the tiles that alias its region
+  preset_tile<DT>(H2p, ld2p, ROWS, a.n_out[1], tid);
+  preset_tile<DT>(H2v, ld2v, ROWS, a.n_out[4], tid);
+  preset_tile<DT>(DMU, ldmu, ROWS, -1, tid);
+  preset_tile<DT>(DV, ldv, ROWS, -1, tid);
   __syncthreads();
   layer_gemm<DT, ROWS, NW, EPI_TANH>(H1p, ld1p, a.d_in[1], W + a.off_w[1], a.n_out[1], H2p, ld2p, a.scale[1], wave, lane);
   layer_gemm<DT, ROWS, NW, EPI_TANH>(H1v, ld1v, a.d_in[4], W + a.off_w[4], a.n_out[4], H2v, ld2v, a.scale[4], wave, lane);
@@ -274,14 +293,9 @@ size_t train_lds(const MlpArgs& a) {
   using T = typename Prec<DT>::T;
   auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
   auto ld = [](int d) { return (size_t)Lds<DT>::stride(d); };
-  size_t b = 0;
-  b += al(sizeof(T) * ROWS * ld(a.d_in[0]));
+  size_t b = train_region_bytes<DT, ROWS>(a);
   b += al(sizeof(T) * ROWS * ld(a.d_in[1]));
-  b += al(sizeof(T) * ROWS * ld(a.d_in[2]));
   b += al(sizeof(T) * ROWS * ld(a.d_in[4]));
-  b += al(sizeof(T) * ROWS * ld(a.d_in[5]));
-  b += al(sizeof(T) * ROWS * ld(a.d_out[2]));
-  b += al(sizeof(T) * ROWS * ld(a.d_out[5]));
   b += al(sizeof(float) * ROWS * a.A) * 2 + al(sizeof(float) * ROWS) + al(sizeof(float) * ROWS * NPART_FIXED);
   return b;
 }

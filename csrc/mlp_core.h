@@ -27,45 +27,63 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
   const int ntiles = (n_real + 15) >> 4;
   const int lr = lane & 15;
   const int lk = (lane >> 4) * 8;
-  for (int nt = wave; nt < ntiles; nt += NW) {
-    f32x4 acc[RB];
+  // each pass of a wave covers NT2 = 2 adjacent column tiles: 2 B fragments + RB A fragments
+  // per k-step feed 2*RB MFMAs, and the next k-step's B fragments are already in flight.
+  constexpr int NT2 = 2;
+  for (int nt0 = wave * NT2; nt0 < ntiles; nt0 += NW * NT2) {
+    const bool two = (nt0 + 1) < ntiles;
+    f32x4 acc[NT2][RB];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const typename P::T* bp = B + (size_t)(nt * 16 + lr) * kdim + lk;
+    for (int t = 0; t < NT2; ++t)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[t][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const typename P::T* bp0 = B + (size_t)(nt0 * 16 + lr) * kdim + lk;
+    // the second tile's pointer is clamped to the first when it does not exist (loads stay in
+    // bounds; its results are discarded)
+    const typename P::T* bp1 = two ? bp0 + (size_t)16 * kdim : bp0;
     const typename P::T* ap = A + lr * lda + lk;
-    Frag bn = P::load(bp);
+    Frag bn0 = P::load(bp0), bn1 = P::load(bp1);
     for (int ks = 0; ks < ksteps; ++ks) {
-      Frag b = bn;
-      if (ks + 1 < ksteps) bn = P::load(bp + (ks + 1) * 32);
+      Frag b0 = bn0, b1 = bn1;
+      if (ks + 1 < ksteps) {
+        bn0 = P::load(bp0 + (ks + 1) * 32);
+        bn1 = P::load(bp1 + (ks + 1) * 32);
+      }
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
         Frag a = P::load(ap + rb * 16 * lda + ks * 32);
-        acc[rb] = P::mma(acc[rb], a, b);
+        acc[0][rb] = P::mma(acc[0][rb], a, b0);
+        acc[1][rb] = P::mma(acc[1][rb], a, b1);
       }
     }
-    const int c = nt * 16 + lr;
-    if (c < n_real) {
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
+    for (int t = 0; t < NT2; ++t) {
+      const int c = (nt0 + t) * 16 + lr;
+      if (c < n_real && (t == 0 || two)) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = rb * 16 + (lane >> 4) * 4 + i;
-          float v = acc[rb][i] * scale;
-          if constexpr (EPI == EPI_TANH) {
-            out[r * ldo + c] = P::cvt(tanhf(v));
-          } else if constexpr (EPI == EPI_LINEAR_F32) {
-            out[r * ldo + c] = v;
-          } else if constexpr (EPI == EPI_LINEAR_T) {
-            out[r * ldo + c] = P::cvt(v);
-          } else {  // EPI_DTANH_INPLACE: out holds h = tanh(pre); write dpre = v * (1 - h^2)
-            float h = P::tof(out[r * ldo + c]);
-            out[r * ldo + c] = P::cvt(v * (1.0f - h * h));
+        for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = rb * 16 + (lane >> 4) * 4 + i;
+            float v = acc[t][rb][i] * scale;
+            if constexpr (EPI == EPI_TANH) {
+              out[r * ldo + c] = P::cvt(tanhf(v));
+            } else if constexpr (EPI == EPI_LINEAR_F32) {
+              out[r * ldo + c] = v;
+            } else if constexpr (EPI == EPI_LINEAR_T) {
+              out[r * ldo + c] = P::cvt(v);
+            } else {  // EPI_DTANH_INPLACE: out holds h = tanh(pre); write dpre = v * (1 - h^2)
+              float h = P::tof(out[r * ldo + c]);
+              out[r * ldo + c] = P::cvt(v * (1.0f - h * h));
+            }
           }
         }
       }
     }
   }
 }
+
+__host__ __device__ inline size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
 
 // 16-byte aligned carve of the dynamic LDS region (Guideline 17: keep the base 16-B aligned).
 struct LdsCarve {

@@ -3,9 +3,10 @@
 //   dW_aug[n][k] = sum_m dY[m][n] * X[m][k]      (k == K is the bias column: X^T row K == 1)
 //
 // Both operands are feature-major (written transposed by mlp_train_kernel), so every MFMA
-// fragment is one 16-byte load along m, the reduction axis.  A task = (layer, 64x64 output
-// tile, batch chunk); each of the 4 waves owns a 32x32 quadrant (2x2 16x16 MFMA tiles, f32
-// accumulate).  Results go to per-chunk fp32 slabs that grad_gather sums in a fixed order —
+// fragment is one 16-byte load along m, the reduction axis.  A task = (layer, 128x128 output
+// tile, batch chunk); each of the 4 waves owns a 64x64 quadrant = 4x4 tiles of 16x16 MFMA
+// (64 f32 accumulator registers), so one k-step issues 8 fragment loads for 16 MFMAs.
+// Results go to per-chunk fp32 slabs that grad_gather sums in a fixed order —
 // deterministic, no float atomics (SURVEY §7.4 hard part 2).
 #include "kernels.h"
 #include "mlp_core.h"
@@ -23,62 +24,75 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   const T* g = reinterpret_cast<const T*>(a.gT[tk.layer]);
   const T* x = reinterpret_cast<const T*>(a.xT[tk.layer]);
   const int lr = lane & 15, lk = (lane >> 4) * 8;
-  const T* ga0 = g + (size_t)(tk.n0 + wn * 32 + lr) * a.ld + lk;
-  const T* ga1 = ga0 + (size_t)16 * a.ld;
-  const T* xb0 = x + (size_t)(tk.k0 + wk * 32 + lr) * a.ld + lk;
-  const T* xb1 = xb0 + (size_t)16 * a.ld;
-  f32x4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
-  int m = tk.m0;
-  // two 32-deep k-steps per iteration: 8 independent 16-byte loads in flight per lane
-  for (; m + 64 <= tk.m1; m += 64) {
-    Frag a0 = P::load(ga0 + m), a1 = P::load(ga1 + m);
-    Frag b0 = P::load(xb0 + m), b1 = P::load(xb1 + m);
-    Frag c0 = P::load(ga0 + m + 32), c1 = P::load(ga1 + m + 32);
-    Frag d0 = P::load(xb0 + m + 32), d1 = P::load(xb1 + m + 32);
-    acc00 = P::mma(acc00, a0, b0);
-    acc01 = P::mma(acc01, a0, b1);
-    acc10 = P::mma(acc10, a1, b0);
-    acc11 = P::mma(acc11, a1, b1);
-    acc00 = P::mma(acc00, c0, d0);
-    acc01 = P::mma(acc01, c0, d1);
-    acc10 = P::mma(acc10, c1, d0);
-    acc11 = P::mma(acc11, c1, d1);
+  const size_t ld = (size_t)a.ld;
+  const T* gp = g + (size_t)(tk.n0 + wn * 64 + lr) * ld + lk;
+  const T* xp = x + (size_t)(tk.k0 + wk * 64 + lr) * ld + lk;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag an[4], bn[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    an[i] = P::load(gp + 16 * i * ld + tk.m0);
+    bn[i] = P::load(xp + 16 * i * ld + tk.m0);
   }
-  for (; m < tk.m1; m += 32) {
-    Frag a0 = P::load(ga0 + m), a1 = P::load(ga1 + m);
-    Frag b0 = P::load(xb0 + m), b1 = P::load(xb1 + m);
-    acc00 = P::mma(acc00, a0, b0);
-    acc01 = P::mma(acc01, a0, b1);
-    acc10 = P::mma(acc10, a1, b0);
-    acc11 = P::mma(acc11, a1, b1);
+  for (int m = tk.m0; m < tk.m1; m += 32) {
+    Frag af[4], bf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { af[i] = an[i]; bf[i] = bn[i]; }
+    if (m + 32 < tk.m1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        an[i] = P::load(gp + 16 * i * ld + m + 32);
+        bn[i] = P::load(xp + 16 * i * ld + m + 32);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(acc[i][j], af[i], bf[j]);
   }
   float* out = a.slab + tk.slab;
-  const int col = wk * 32 + lr;
-  const int rbase = wn * 32 + (lane >> 4) * 4;
+  const int col = wk * 64 + lr;
+  const int rbase = wn * 64 + (lane >> 4) * 4;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    out[(rbase + q) * 64 + col] = acc00[q];
-    out[(rbase + q) * 64 + col + 16] = acc01[q];
-    out[(rbase + 16 + q) * 64 + col] = acc10[q];
-    out[(rbase + 16 + q) * 64 + col + 16] = acc11[q];
-  }
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * WGRAD_TILE + col + 16 * j] = acc[i][j][q];
 }
 
-// grad[i] = scale * sum_c slab[c*stride + src_off[i]]   (fixed chunk order: deterministic)
-// i < A (log_std): grad[i] = scale * sum_b part[b*npart + 8 + i]
+// Workgroups [0, A): grad[j] = scale * sum_b part[b*npart + 8 + j]  (log_std, one WG per dim,
+//                    strided partial sums + LDS tree: fixed order, deterministic)
+// Workgroups [A, grid): grad[i] = scale * sum_c slab[c*stride + src_off[i]], i in [A, n)
+//                    (fixed chunk order: deterministic; no float atomics anywhere)
 __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restrict__ slab,
                                                           const int* __restrict__ src_off, int nchunks,
                                                           int stride, const float* __restrict__ part,
                                                           int nblk, int npart, int A, float scale,
                                                           float* __restrict__ grad, int n) {
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+  if ((int)blockIdx.x < A) {
+    __shared__ float red[256];
+    const int j = blockIdx.x;
     float s = 0.f;
-    if (i < A) {
-      for (int b = 0; b < nblk; ++b) s += part[(size_t)b * npart + 8 + i];
-    } else {
-      const int o = src_off[i];
-      for (int c = 0; c < nchunks; ++c) s += slab[(size_t)c * stride + o];
+    for (int b = threadIdx.x; b < nblk; b += 256) s += part[(size_t)b * npart + 8 + j];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
     }
+    if (threadIdx.x == 0) grad[j] = red[0] * scale;
+    return;
+  }
+  const int nb = gridDim.x - A;
+  for (int i = A + (blockIdx.x - A) * 256 + threadIdx.x; i < n; i += nb * 256) {
+    const int o = src_off[i];
+    float s = 0.f;
+    for (int c = 0; c < nchunks; ++c) s += slab[(size_t)c * stride + o];
     grad[i] = s * scale;
   }
 }
@@ -96,8 +110,10 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
 extern "C" void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int chunk_stride,
                                    const float* part, int nblk, int npart, int A, float scale, float* grad,
                                    int n, hipStream_t s) {
-  int grid = (n + 255) / 256;
+  int grid = (n - A + 255) / 256;
   if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;
+  grid += A;
   hipLaunchKernelGGL(grad_gather_kernel, dim3(grid), dim3(256), 0, s, slab, src_off, nchunks, chunk_stride,
                      part, nblk, npart, A, scale, grad, n);
   HIP_CHECK_LAUNCH();

@@ -29,6 +29,7 @@ from ..utils.obs_stats import RunningObsStats
 
 STORAGE = {0: torch.float32, 1: torch.bfloat16, 2: torch.uint8}
 NPART_FIXED = 8
+WT = 128            # wgrad output tile (csrc/kernels.h WGRAD_TILE)
 ROLL_ROWS = 16
 
 
@@ -89,12 +90,12 @@ class HipEngine:
         self.ntrain_blk = self.ldT // self.train_rows
         self.npart = NPART_FIXED + A
         self.part = torch.zeros(self.ntrain_blk, self.npart, **f32)
-        # transposed operand buffers (feature-major), heights padded to the 64-row wgrad tile
+        # transposed operand buffers (feature-major), heights padded to the wgrad tile
         lp1, lp2, lmu, lv1, lv2, lv = ls
         x_rows = [lp1.d_in, lp2.d_in, lmu.d_in, lv1.d_in, lv2.d_in, lv.d_in]
         g_rows = [lp1.fan_out, lp2.fan_out, lmu.fan_out, lv1.fan_out, lv2.fan_out, lv.fan_out]
-        self.x_rows = [_r(r, 64) for r in x_rows]
-        self.g_rows = [_r(r, 64) for r in g_rows]
+        self.x_rows = [_r(r, WT) for r in x_rows]
+        self.g_rows = [_r(r, WT) for r in g_rows]
         mk = lambda rows: torch.zeros(rows, self.ldT, dtype=self.sdtype, **dev)
         self.xT = mk(self.x_rows[0])                       # shared by p_fc1 and v_fc1
         self.h1pT, self.h2pT = mk(self.x_rows[1]), mk(self.x_rows[2])
@@ -129,8 +130,8 @@ class HipEngine:
         ls = self.L.layers
         tiles = []  # (layer, n0, k0)
         for li, l in enumerate(ls):
-            for n0 in range(0, l.fan_out, 64):
-                for k0 in range(0, l.fan_in + 1, 64):
+            for n0 in range(0, l.fan_out, WT):
+                for k0 in range(0, l.fan_in + 1, WT):
                     tiles.append((li, n0, k0))
         ntiles = len(tiles)
         max_chunks = max(1, self.ldT // 256)
@@ -138,8 +139,8 @@ class HipEngine:
         mc = _r(-(-self.ldT // nchunks), 32)
         chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
         self.nchunks = len(chunks)
-        self.chunk_stride = ntiles * 4096
-        tile_off = {t: i * 4096 for i, t in enumerate(tiles)}
+        self.chunk_stride = ntiles * WT * WT
+        tile_off = {t: i * WT * WT for i, t in enumerate(tiles)}
         tasks = []
         for ci, (m0, m1) in enumerate(chunks):
             for t in tiles:
@@ -162,13 +163,13 @@ class HipEngine:
 
     @staticmethod
     def _slab_index(tile_off, li, n, k):
-        nt, kt = int(n.max()) // 64 + 1, int(k.max()) // 64 + 1
+        nt, kt = int(n.max()) // WT + 1, int(k.max()) // WT + 1
         lut = torch.zeros(nt, kt, dtype=torch.int64)
         for a in range(nt):
             for b in range(kt):
-                lut[a, b] = tile_off.get((li, a * 64, b * 64), -1)
-        base = lut[n // 64, k // 64]
-        return base + (n % 64) * 64 + (k % 64)
+                lut[a, b] = tile_off.get((li, a * WT, b * WT), -1)
+        base = lut[n // WT, k // WT]
+        return base + (n % WT) * WT + (k % WT)
 
     # ------------------------------------------------------------------------------------------
     def params_changed(self) -> None:
