@@ -126,6 +126,13 @@ class TorchEngine:
     def current_obs(self) -> torch.Tensor:
         return self.obs
 
+    def env_state(self) -> Dict:
+        return self.env.state_dict()
+
+    def load_env_state(self, d: Dict) -> None:
+        self.env.load_state_dict(d)
+        self.obs = self.env.observe().to(self.device)
+
     def begin_update(self) -> None:
         self.flat_old.copy_(self.model.flat.detach())
 

@@ -1,0 +1,167 @@
+"""Multi-process tests on the gloo backend (SURVEY §4 'Distributed (fake backend)').
+
+Every test spawns fresh python processes (spawn start method) rendezvousing on 127.0.0.1.
+"""
+import os
+import time
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from pytorch_dppo_amd.config import Params, dppo_preset
+from pytorch_dppo_amd.runtime.launcher import free_port
+
+pytestmark = pytest.mark.slow
+
+
+def _init(rank, world, port, timeout=60.0):
+    from pytorch_dppo_amd.parallel.dist import init_distributed
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    return init_distributed("cpu", rank=rank, world_size=world, timeout_s=timeout)
+
+
+def _worker_grad_sum(rank, world, port, out_dir):
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    ctx = _init(rank, world, port)
+    p = dppo_preset(env_name="HalfCheetah-v2", num_envs=8, exploration_size=64, batch_size=64, num_epoch=2,
+                    verify_sync_every=1, num_processes=world)
+    w = DPPOWorker(p, ctx)
+    eng = w.engine
+    w.init_stats()
+    ro = eng.rollout()
+    w._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"])
+    eng.values()
+    eng.gae()
+    eng.begin_update()
+    eng.grad(None)
+    local = eng.grad_flat.clone()
+    ctx.allreduce_grads(eng.grad_flat)
+    reduced = eng.grad_flat.clone()
+    eng.apply()
+    m = w.iteration_step()
+    torch.save({"local": local, "reduced": reduced, "flat": w.model.flat.data.clone(),
+                "stats_mean": w.stats.mean.clone(), "stats_n": w.stats.n, "in_sync": m["replicas_in_sync"]},
+               os.path.join(out_dir, f"r{rank}.pt"))
+    ctx.destroy()
+
+
+def _spawn(fn, world, *args):
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=fn, args=(r, world, port) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    return procs
+
+
+def _join(procs, timeout):
+    t0 = time.time()
+    for p in procs:
+        p.join(max(1.0, timeout - (time.time() - t0)))
+    for p in procs:
+        if p.is_alive():
+            p.terminate()
+    return [p.exitcode for p in procs]
+
+
+def test_grad_allreduce_is_sum_and_replicas_stay_identical(tmp_path):
+    codes = _join(_spawn(_worker_grad_sum, 2, str(tmp_path)), 240)
+    assert codes == [0, 0]
+    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
+    assert not torch.equal(r0["local"], r1["local"])          # different data per rank
+    assert torch.allclose(r0["reduced"], r0["local"] + r1["local"], atol=1e-6)   # R1 = sum (model.py:55)
+    assert torch.equal(r0["reduced"], r1["reduced"])
+    assert torch.equal(r0["flat"], r1["flat"])                 # replicated Adam: bit-identical
+    assert r0["in_sync"] and r1["in_sync"]
+    assert torch.equal(r0["stats_mean"], r1["stats_mean"]) and r0["stats_n"] == r1["stats_n"]
+
+
+def _worker_obs_merge(rank, world, port, out_dir):
+    from pytorch_dppo_amd.utils.obs_stats import RunningObsStats
+    ctx = _init(rank, world, port)
+    g = torch.Generator().manual_seed(100 + rank)
+    st = RunningObsStats(4)
+    for _ in range(3):
+        x = torch.randn(50, 4, generator=g) * (rank + 1) + rank
+        shift = st.shift().clone()
+        c, s1, s2 = RunningObsStats.moments(x, shift)
+        c, s1, s2 = ctx.allreduce_obs_moments(c, s1, s2)
+        st.merge_moments(c, s1, s2, shift)
+    torch.save({"mean": st.mean, "md": st.mean_diff, "n": st.n}, os.path.join(out_dir, f"s{rank}.pt"))
+    ctx.destroy()
+
+
+def test_obs_stats_merge_equals_single_process_on_concatenated_stream(tmp_path):
+    from pytorch_dppo_amd.utils.obs_stats import RunningObsStats
+    assert _join(_spawn(_worker_obs_merge, 3, str(tmp_path)), 120) == [0, 0, 0]
+    ref = RunningObsStats(4)
+    gens = [torch.Generator().manual_seed(100 + r) for r in range(3)]
+    for _ in range(3):
+        xs = [torch.randn(50, 4, generator=gens[r]) * (r + 1) + r for r in range(3)]
+        ref.observes(torch.cat(xs))
+    for r in range(3):
+        s = torch.load(tmp_path / f"s{r}.pt", weights_only=True)
+        assert s["n"] == ref.n == 450
+        assert torch.allclose(s["mean"], ref.mean, atol=1e-10)
+        assert torch.allclose(s["md"], ref.mean_diff, rtol=1e-9)
+
+
+def _worker_fault(rank, world, port, out_dir):
+    ctx = _init(rank, world, port, timeout=20.0)
+    if rank == 1:
+        os._exit(3)  # injected fault: a worker dies (reference Q21 would deadlock the chief)
+    t0 = time.time()
+    try:
+        for _ in range(100):
+            ctx.allreduce_grads(torch.ones(1000))
+            time.sleep(0.05)
+        msg = "no error"
+    except Exception as e:  # noqa: BLE001
+        msg = f"error after {time.time() - t0:.1f}s: {type(e).__name__}"
+    with open(os.path.join(out_dir, "fault.txt"), "w") as f:
+        f.write(msg)
+
+
+def test_dead_rank_makes_survivor_fail_fast_instead_of_deadlock(tmp_path):
+    t0 = time.time()
+    codes = _join(_spawn(_worker_fault, 2, str(tmp_path)), 120)
+    assert codes[1] == 3
+    msg = (tmp_path / "fault.txt").read_text()
+    assert msg.startswith("error"), msg
+    assert time.time() - t0 < 110
+
+
+def test_launcher_two_workers_checkpoint_and_resume(tmp_path):
+    from pytorch_dppo_amd.runtime.launcher import launch
+    ck = str(tmp_path / "ck")
+    p = dppo_preset(env_name="Pendulum-v0", num_processes=2, num_envs=4, exploration_size=64, batch_size=64,
+                    num_epoch=2, hidden=(16, 16), max_iters=2, checkpoint_dir=ck, log_jsonl=str(tmp_path / "log.jsonl"))
+    launch(p)
+    assert os.path.exists(os.path.join(ck, "model.pt"))
+    assert os.path.exists(os.path.join(ck, "env_rank1.pt"))
+    lines = open(tmp_path / "log.jsonl").read().strip().splitlines()
+    assert len(lines) == 2
+    st = torch.load(os.path.join(ck, "trainer_state.pt"), weights_only=True)
+    assert st["iteration"] == 2 and st["updates"] == 4 and st["world_size"] == 2
+    p2 = Params.from_dict({**p.to_dict(), "resume": ck, "max_iters": 3, "checkpoint_dir": str(tmp_path / "ck2"),
+                           "log_jsonl": ""})
+    launch(p2)
+    st2 = torch.load(os.path.join(str(tmp_path / "ck2"), "trainer_state.pt"), weights_only=True)
+    assert st2["iteration"] == 3 and st2["updates"] == 6
+
+
+def test_resume_continues_bit_identically_single_process(tmp_path):
+    from pytorch_dppo_amd.parallel.dist import DistContext
+    from pytorch_dppo_amd.runtime.launcher import run_worker
+    base = dict(env_name="HalfCheetah-v2", num_processes=1, num_envs=8, exploration_size=64, batch_size=32,
+                num_epoch=2, hidden=(32, 32))
+    w_full, _ = run_worker(dppo_preset(max_iters=3, **base), DistContext(), evaluator=False, quiet=True)
+    ck = str(tmp_path / "ck")
+    run_worker(dppo_preset(max_iters=2, checkpoint_dir=ck, **base), DistContext(), evaluator=False, quiet=True)
+    w_res, _ = run_worker(dppo_preset(max_iters=3, resume=ck, **base), DistContext(), evaluator=False, quiet=True)
+    assert w_res.iteration == 3
+    assert torch.equal(w_full.model.flat.data, w_res.model.flat.data)
