@@ -77,6 +77,21 @@ template <> struct Prec<DT_FP8> {
   }
 };
 
+// Fragment-major ("FM") layout of a [rows][cols] matrix (rows % 16 == 0, cols % 32 == 0):
+// 16x32 blocks stored block-row-major, and inside a block lane l = (r & 15) + 16*((c & 31) >> 3)
+// holds elements c & 7 = 0..7 contiguously — exactly the MFMA operand map.  A fragment load
+// of block (rt, ks) is then ONE contiguous 512-element read (1 KiB at bf16) per wave:
+// base + 8*lane, instead of 16 rows x 64 B (TA-bound, cdna_hip_programming.md §5 table).
+// Used for the packed weight images and the feature-major wgrad operands.
+__host__ __device__ inline size_t fm_index(int r, int c, int cols) {
+  return ((size_t)(r >> 4) * (size_t)(cols >> 5) + (size_t)(c >> 5)) * 512u +
+         (size_t)((((r & 15) + (((c & 31) >> 3) << 4)) << 3) + (c & 7));
+}
+// element offset of lane `lane`'s fragment of block (rt, ks) in an FM matrix with `cols` columns
+__host__ __device__ inline size_t fm_frag(int rt, int ks, int cols, int lane) {
+  return ((size_t)rt * (size_t)(cols >> 5) + (size_t)ks) * 512u + (size_t)lane * 8u;
+}
+
 // LDS row padding: one 16-byte slot per row breaks the power-of-two row stride so the 16
 // lanes of a ds_read_b128 lane group (16 rows, same k) hit distinct bank slots.
 template <int DT> struct Lds {

@@ -24,47 +24,43 @@ DEV void load_rows(const typename Prec<DT>::T* xb, const int* idx, int row0, int
   using T = typename Prec<DT>::T;
   constexpr int E16 = 16 / Prec<DT>::BYTES;
   const int chunks = d / E16;
-  for (int i = tid; i < ROWS * chunks; i += 256) {
-    int r = i / chunks, c = i - r * chunks;
+  // (row, chunk) walk with one division per thread instead of one per element
+  int r = tid / chunks, c = tid - r * chunks;
+  const int step_r = 256 / chunks, step_c = 256 - step_r * chunks;
+  while (r < ROWS) {
     uint4 v = make_uint4(0, 0, 0, 0);
     if (r < nvalid) {
       int src = idx ? idx[m0 + r] : row0 + m0 + r;
       v = *reinterpret_cast<const uint4*>(xb + (size_t)src * d + c * E16);
     }
     *reinterpret_cast<uint4*>(X + r * ldx + c * E16) = v;
+    r += step_r;
+    c += step_c;
+    if (c >= chunks) { c -= chunks; ++r; }
   }
 }
 
-// preset a padded activation tile: column `one_col` = 1, everything else 0
-template <int DT>
-DEV void preset_tile(typename Prec<DT>::T* H, int ld, int rows, int one_col, int tid) {
-  using P = Prec<DT>;
-  for (int i = tid; i < rows * ld; i += 256) {
-    int c = i % ld;
-    H[i] = P::cvt(c == one_col ? 1.f : 0.f);
-  }
-}
-
-// dst[f][m0 + r] = tile[r][f]  for f < nfeat, r < ROWS   (16-byte stores along m)
+// dst^T (fragment-major, [rows][ldT]) row f, columns m0 + r  <-  tile[r][f],  f < nfeat, r < ROWS.
+// One item = 8 consecutive m of one feature = one contiguous 8-element group of the FM layout.
 template <int DT, int ROWS>
 DEV void write_transposed(const typename Prec<DT>::T* tile, int ld, int nfeat, void* dstv, int ldT,
                           int m0, int tid) {
   using T = typename Prec<DT>::T;
-  constexpr int E16 = 16 / Prec<DT>::BYTES;
-  constexpr int CH = ROWS / E16 > 0 ? ROWS / E16 : 1;
-  constexpr int EL = ROWS < E16 ? ROWS : E16;
+  constexpr int CH = ROWS / 8;
   T* dst = reinterpret_cast<T*>(dstv);
   for (int i = tid; i < nfeat * CH; i += 256) {
-    int f = i / CH, c = i - f * CH;
-    T buf[E16];
+    const int f = i / CH, c = i - f * CH;
+    T buf[8];
 #pragma unroll
-    for (int j = 0; j < E16; ++j) buf[j] = (j < EL) ? tile[(c * E16 + j) * ld + f] : Prec<DT>::cvt(0.f);
-    T* o = dst + (size_t)f * ldT + m0 + c * E16;
-    if constexpr (ROWS >= E16) {
+    for (int j = 0; j < 8; ++j) buf[j] = tile[(c * 8 + j) * ld + f];
+    T* o = dst + fm_index(f, m0 + c * 8, ldT);
+    if constexpr (DT == DT_F32) {
+      reinterpret_cast<uint4*>(o)[0] = reinterpret_cast<const uint4*>(buf)[0];
+      reinterpret_cast<uint4*>(o)[1] = reinterpret_cast<const uint4*>(buf)[1];
+    } else if constexpr (DT == DT_BF16) {
       *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(buf);
     } else {
-#pragma unroll
-      for (int j = 0; j < EL; ++j) o[j] = buf[j];
+      *reinterpret_cast<uint2*>(o) = *reinterpret_cast<const uint2*>(buf);
     }
   }
 }
@@ -100,8 +96,8 @@ __global__ __launch_bounds__(256) void mlp_value_kernel(MlpArgs a) {
   float* V = cv.take<float>(ROWS);
   const T* W = reinterpret_cast<const T*>(a.W);
   load_rows<DT>(reinterpret_cast<const T*>(a.x_buf), a.idx, a.row0, m0, nvalid, a.d_in[3], X, ldx, ROWS, tid);
-  preset_tile<DT>(H1, ld1, ROWS, a.n_out[3], tid);
-  preset_tile<DT>(H2, ld2, ROWS, a.n_out[4], tid);
+  preset_tile<DT>(H1, ld1, ROWS, a.n_out[3], tid, 256);
+  preset_tile<DT>(H2, ld2, ROWS, a.n_out[4], tid, 256);
   __syncthreads();
   layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1, ld1, a.scale[3], wave, lane);
   __syncthreads();
@@ -150,27 +146,35 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(MlpArgs a) {
 
   const T* W = reinterpret_cast<const T*>(a.W);
   load_rows<DT>(reinterpret_cast<const T*>(a.x_buf), a.idx, a.row0, m0, nvalid, a.d_in[0], X, ldx, ROWS, tid);
-  preset_tile<DT>(H1p, ld1p, ROWS, a.n_out[0], tid);
-  preset_tile<DT>(H1v, ld1v, ROWS, a.n_out[3], tid);
+  preset_tile<DT>(H1p, ld1p, ROWS, a.n_out[0], tid, 256);
+  preset_tile<DT>(H1v, ld1v, ROWS, a.n_out[3], tid, 256);
   __syncthreads();
   // ---------------- forward ----------------
+  // Activations go to the feature-major wgrad operands straight from the MFMA accumulators
+  // (rows < n_real; the constant-1 bias row of each buffer is preset once by the host).
+  T* h1pT = reinterpret_cast<T*>(a.h1pT);
+  T* h2pT = reinterpret_cast<T*>(a.h2pT);
+  T* h1vT = reinterpret_cast<T*>(a.h1vT);
+  T* h2vT = reinterpret_cast<T*>(a.h2vT);
   write_transposed<DT, ROWS>(X, ldx, a.d_in[0], a.xT, a.ldT, m0, tid);
-  layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[0], W + a.off_w[0], a.n_out[0], H1p, ld1p, a.scale[0], wave, lane);
-  layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1v, ld1v, a.scale[3], wave, lane);
+  layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[0], W + a.off_w[0], a.n_out[0], H1p, ld1p, a.scale[0], wave, lane,
+                                     h1pT, a.ldT, m0);
+  layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1v, ld1v, a.scale[3], wave, lane,
+                                     h1vT, a.ldT, m0);
   __syncthreads();
   // X is dead: preset the tiles that alias its region
-  preset_tile<DT>(H2p, ld2p, ROWS, a.n_out[1], tid);
-  preset_tile<DT>(H2v, ld2v, ROWS, a.n_out[4], tid);
-  preset_tile<DT>(DMU, ldmu, ROWS, -1, tid);
-  preset_tile<DT>(DV, ldv, ROWS, -1, tid);
+  preset_tile<DT>(H2p, ld2p, ROWS, a.n_out[1], tid, 256);
+  preset_tile<DT>(H2v, ld2v, ROWS, a.n_out[4], tid, 256);
+  preset_tile<DT>(DMU, ldmu, ROWS, -1, tid, 256);
+  preset_tile<DT>(DV, ldv, ROWS, -1, tid, 256);
   __syncthreads();
-  layer_gemm<DT, ROWS, NW, EPI_TANH>(H1p, ld1p, a.d_in[1], W + a.off_w[1], a.n_out[1], H2p, ld2p, a.scale[1], wave, lane);
-  layer_gemm<DT, ROWS, NW, EPI_TANH>(H1v, ld1v, a.d_in[4], W + a.off_w[4], a.n_out[4], H2v, ld2v, a.scale[4], wave, lane);
+  layer_gemm<DT, ROWS, NW, EPI_TANH>(H1p, ld1p, a.d_in[1], W + a.off_w[1], a.n_out[1], H2p, ld2p, a.scale[1], wave, lane,
+                                     h2pT, a.ldT, m0);
+  layer_gemm<DT, ROWS, NW, EPI_TANH>(H1v, ld1v, a.d_in[4], W + a.off_w[4], a.n_out[4], H2v, ld2v, a.scale[4], wave, lane,
+                                     h2vT, a.ldT, m0);
   __syncthreads();
   layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32>(H2p, ld2p, a.d_in[2], W + a.off_w[2], A, MU, A, a.scale[2], wave, lane);
   layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32>(H2v, ld2v, a.d_in[5], W + a.off_w[5], 1, V, 1, a.scale[5], wave, lane);
-  write_transposed<DT, ROWS>(H1p, ld1p, a.d_in[1], a.h1pT, a.ldT, m0, tid);
-  write_transposed<DT, ROWS>(H1v, ld1v, a.d_in[4], a.h1vT, a.ldT, m0, tid);
   __syncthreads();
   // ---------------- loss + dL/d(mu, log_std, v) per row ----------------
   if (tid < ROWS) {
@@ -263,8 +267,6 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(MlpArgs a) {
       for (int j = 0; j < A; ++j) DLS[r * A + j] = 0.f;
     }
   }
-  write_transposed<DT, ROWS>(H2p, ld2p, a.d_in[2], a.h2pT, a.ldT, m0, tid);
-  write_transposed<DT, ROWS>(H2v, ld2v, a.d_in[5], a.h2vT, a.ldT, m0, tid);
   __syncthreads();
   // ---------------- per-workgroup partials + dY^T of the output layers ----------------
   if (tid < NPART_FIXED + A) {
@@ -275,17 +277,16 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(MlpArgs a) {
   }
   write_transposed<DT, ROWS>(DMU, ldmu, A, a.g3pT, a.ldT, m0, tid);
   write_transposed<DT, ROWS>(DV, ldv, 1, a.g3vT, a.ldT, m0, tid);
-  // ---------------- dgrad chain ----------------
-  layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(DMU, ldmu, a.d_out[2], W + a.off_wt[2], a.n_out[1], H2p, ld2p, a.scale[2], wave, lane);
-  layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(DV, ldv, a.d_out[5], W + a.off_wt[5], a.n_out[4], H2v, ld2v, a.scale[5], wave, lane);
+  // ---------------- dgrad chain (dY^T of every layer stored from the accumulators) --------
+  layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(DMU, ldmu, a.d_out[2], W + a.off_wt[2], a.n_out[1], H2p, ld2p, a.scale[2],
+                                              wave, lane, reinterpret_cast<T*>(a.g2pT), a.ldT, m0);
+  layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(DV, ldv, a.d_out[5], W + a.off_wt[5], a.n_out[4], H2v, ld2v, a.scale[5],
+                                              wave, lane, reinterpret_cast<T*>(a.g2vT), a.ldT, m0);
   __syncthreads();
-  write_transposed<DT, ROWS>(H2p, ld2p, a.n_out[1], a.g2pT, a.ldT, m0, tid);
-  write_transposed<DT, ROWS>(H2v, ld2v, a.n_out[4], a.g2vT, a.ldT, m0, tid);
-  layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(H2p, ld2p, a.d_out[1], W + a.off_wt[1], a.n_out[0], H1p, ld1p, a.scale[1], wave, lane);
-  layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(H2v, ld2v, a.d_out[4], W + a.off_wt[4], a.n_out[3], H1v, ld1v, a.scale[4], wave, lane);
-  __syncthreads();
-  write_transposed<DT, ROWS>(H1p, ld1p, a.n_out[0], a.g1pT, a.ldT, m0, tid);
-  write_transposed<DT, ROWS>(H1v, ld1v, a.n_out[3], a.g1vT, a.ldT, m0, tid);
+  layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(H2p, ld2p, a.d_out[1], W + a.off_wt[1], a.n_out[0], H1p, ld1p, a.scale[1],
+                                              wave, lane, reinterpret_cast<T*>(a.g1pT), a.ldT, m0);
+  layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(H2v, ld2v, a.d_out[4], W + a.off_wt[4], a.n_out[3], H1v, ld1v, a.scale[4],
+                                              wave, lane, reinterpret_cast<T*>(a.g1vT), a.ldT, m0);
 }
 
 template <int DT, int ROWS>

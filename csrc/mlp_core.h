@@ -7,29 +7,68 @@
 // for dgrad).  The bias is column K of Wp and the activation tiles carry a constant 1 in
 // column K, so no separate bias add exists anywhere (PackedLayout in models/actor_critic.py).
 //
-// Work split: the 4 (or NW) waves of the workgroup stride over 16-wide output column tiles;
-// each wave computes ALL ROWS/16 row blocks of its column tile, so one 16-byte B fragment
-// (weights, the operand that comes from L2) feeds ROWS/16 MFMAs.  The next k-step's B
-// fragment is requested before the current MFMAs issue (one tile of prefetch).
+// Work split: the NW waves of the workgroup stride over PAIRS of 16-wide output column tiles;
+// each wave computes ALL ROWS/16 row blocks of its tiles, so one 16-byte B fragment (weights,
+// the operand that streams from L2) feeds ROWS/16 MFMAs.  B fragments are register
+// double-buffered in chunks of KC k-steps: while the MFMAs of chunk j run, the 2*KC loads of
+// chunk j+1 are in flight (PMC showed the 1-step prefetch left waves parked on L2 latency
+// ~60% of their cycles).
+//
+// Optional transposed store: with outT != nullptr the epilogue ALSO writes the value to the
+// feature-major buffer outT[c][m0 + r] that feeds the wgrad GEMM.  In the MFMA C/D layout a
+// lane holds 4 consecutive rows of one column, i.e. 4 contiguous m of one feature: one
+// 4-element store per lane per row block, straight from registers (no LDS gather).
 #pragma once
 #include "common.h"
 
 enum { EPI_TANH = 0, EPI_LINEAR_F32 = 1, EPI_DTANH_INPLACE = 2, EPI_LINEAR_T = 3 };
 
+// tanh for the MFMA epilogues: exp + reciprocal on the transcendental unit (v_exp_f32,
+// v_rcp_f32) instead of the libm polynomial; |err| ~1e-7.  The fp32 path keeps tanhf (it is
+// the near-exact path the numerics tests compare against the torch oracle).
+template <int DT>
+DEV float act_tanh(float x) {
+  if constexpr (DT == DT_F32) {
+    return tanhf(x);
+  } else {
+    const float e = __expf(-2.0f * fabsf(x));
+    const float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
+    return copysignf(t, x);
+  }
+}
+
+template <int DT> struct KChunk { static constexpr int KC = (DT == DT_F32) ? 2 : 4; };
+
+template <int DT>
+DEV void store4_T(typename Prec<DT>::T* dst, float v0, float v1, float v2, float v3) {
+  using P = Prec<DT>;
+  if constexpr (DT == DT_F32) {
+    *reinterpret_cast<float4*>(dst) = make_float4(v0, v1, v2, v3);
+  } else if constexpr (DT == DT_BF16) {
+    typename P::T t[4] = {P::cvt(v0), P::cvt(v1), P::cvt(v2), P::cvt(v3)};
+    *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(t);
+  } else {
+    typename P::T t[4] = {P::cvt(v0), P::cvt(v1), P::cvt(v2), P::cvt(v3)};
+    *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(t);
+  }
+}
+
 template <int DT, int ROWS, int NW, int EPI, typename OutT>
 DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdim,
                     const typename Prec<DT>::T* __restrict__ B, int n_real,
-                    OutT* out, int ldo, float scale, int wave, int lane) {
+                    OutT* out, int ldo, float scale, int wave, int lane,
+                    typename Prec<DT>::T* __restrict__ outT = nullptr, int ldT = 0, int m0 = 0) {
   using P = Prec<DT>;
+  using T = typename P::T;
   using Frag = typename P::Frag;
   constexpr int RB = ROWS / 16;
+  constexpr int KC = KChunk<DT>::KC;
+  constexpr int NT2 = 2;
   const int ksteps = kdim >> 5;
+  const int nchunks = (ksteps + KC - 1) / KC;
   const int ntiles = (n_real + 15) >> 4;
   const int lr = lane & 15;
   const int lk = (lane >> 4) * 8;
-  // each pass of a wave covers NT2 = 2 adjacent column tiles: 2 B fragments + RB A fragments
-  // per k-step feed 2*RB MFMAs, and the next k-step's B fragments are already in flight.
-  constexpr int NT2 = 2;
   for (int nt0 = wave * NT2; nt0 < ntiles; nt0 += NW * NT2) {
     const bool two = (nt0 + 1) < ntiles;
     f32x4 acc[NT2][RB];
@@ -37,24 +76,43 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
     for (int t = 0; t < NT2; ++t)
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) acc[t][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const typename P::T* bp0 = B + (size_t)(nt0 * 16 + lr) * kdim + lk;
+    // B is fragment-major (FM): block (row tile, k-step) = 512 contiguous elements
+    const T* bp0 = B + fm_frag(nt0, 0, kdim, lane);
     // the second tile's pointer is clamped to the first when it does not exist (loads stay in
     // bounds; its results are discarded)
-    const typename P::T* bp1 = two ? bp0 + (size_t)16 * kdim : bp0;
-    const typename P::T* ap = A + lr * lda + lk;
-    Frag bn0 = P::load(bp0), bn1 = P::load(bp1);
-    for (int ks = 0; ks < ksteps; ++ks) {
-      Frag b0 = bn0, b1 = bn1;
-      if (ks + 1 < ksteps) {
-        bn0 = P::load(bp0 + (ks + 1) * 32);
-        bn1 = P::load(bp1 + (ks + 1) * 32);
+    const T* bp1 = two ? bp0 + (size_t)ksteps * 512 : bp0;
+    const T* ap = A + lr * lda + lk;
+    Frag bc0[KC], bc1[KC], bn0[KC], bn1[KC];
+    // k-steps past the end re-load the last valid step (in bounds; never consumed)
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const int ks = min(j, ksteps - 1);
+      bc0[j] = P::load(bp0 + ks * 512);
+      bc1[j] = P::load(bp1 + ks * 512);
+    }
+    for (int kc = 0; kc < nchunks; ++kc) {
+      if (kc + 1 < nchunks) {
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+          const int ks = min((kc + 1) * KC + j, ksteps - 1);
+          bn0[j] = P::load(bp0 + ks * 512);
+          bn1[j] = P::load(bp1 + ks * 512);
+        }
       }
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        Frag a = P::load(ap + rb * 16 * lda + ks * 32);
-        acc[0][rb] = P::mma(acc[0][rb], a, b0);
-        acc[1][rb] = P::mma(acc[1][rb], a, b1);
+      for (int j = 0; j < KC; ++j) {
+        const int ks = kc * KC + j;
+        if (ks < ksteps) {
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb) {
+            Frag a = P::load(ap + rb * 16 * lda + ks * 32);
+            acc[0][rb] = P::mma(acc[0][rb], a, bc0[j]);
+            acc[1][rb] = P::mma(acc[1][rb], a, bc1[j]);
+          }
+        }
       }
+#pragma unroll
+      for (int j = 0; j < KC; ++j) { bc0[j] = bn0[j]; bc1[j] = bn1[j]; }
     }
 #pragma unroll
     for (int t = 0; t < NT2; ++t) {
@@ -62,20 +120,28 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
       if (c < n_real && (t == 0 || two)) {
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
+          float vals[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int r = rb * 16 + (lane >> 4) * 4 + i;
             float v = acc[t][rb][i] * scale;
             if constexpr (EPI == EPI_TANH) {
-              out[r * ldo + c] = P::cvt(tanhf(v));
+              v = act_tanh<DT>(v);
+              out[r * ldo + c] = P::cvt(v);
             } else if constexpr (EPI == EPI_LINEAR_F32) {
               out[r * ldo + c] = v;
             } else if constexpr (EPI == EPI_LINEAR_T) {
               out[r * ldo + c] = P::cvt(v);
             } else {  // EPI_DTANH_INPLACE: out holds h = tanh(pre); write dpre = v * (1 - h^2)
-              float h = P::tof(out[r * ldo + c]);
-              out[r * ldo + c] = P::cvt(v * (1.0f - h * h));
+              const float h = P::tof(out[r * ldo + c]);
+              v = v * (1.0f - h * h);
+              out[r * ldo + c] = P::cvt(v);
             }
+            vals[i] = v;
+          }
+          if (outT != nullptr) {  // FM wgrad operand: 4 consecutive m of feature c are contiguous
+            store4_T<DT>(outT + fm_index(c, m0 + rb * 16 + (lane >> 4) * 4, ldT), vals[0], vals[1], vals[2],
+                         vals[3]);
           }
         }
       }
@@ -97,3 +163,15 @@ struct LdsCarve {
     return p;
   }
 };
+
+// Fill rows x ld of a padded activation tile: column `one_col` = 1, the rest 0.  Threads own
+// columns; rows are an outer loop (no per-element integer division).
+template <int DT>
+DEV void preset_tile(typename Prec<DT>::T* H, int ld, int rows, int one_col, int tid, int nthreads) {
+  using P = Prec<DT>;
+  const typename P::T zero = P::cvt(0.f), one = P::cvt(1.f);
+  for (int c = tid; c < ld; c += nthreads) {
+    const typename P::T v = (c == one_col) ? one : zero;
+    for (int r = 0; r < rows; ++r) H[r * ld + c] = v;
+  }
+}

@@ -23,10 +23,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   const int wn = wave >> 1, wk = wave & 1;
   const T* g = reinterpret_cast<const T*>(a.gT[tk.layer]);
   const T* x = reinterpret_cast<const T*>(a.xT[tk.layer]);
-  const int lr = lane & 15, lk = (lane >> 4) * 8;
-  const size_t ld = (size_t)a.ld;
-  const T* gp = g + (size_t)(tk.n0 + wn * 64 + lr) * ld + lk;
-  const T* xp = x + (size_t)(tk.k0 + wk * 64 + lr) * ld + lk;
+  // operands are fragment-major (FM): the fragment of (row tile, k-step) is 512 contiguous
+  // elements, so each of the 8 loads per k-step is one contiguous 1 KiB wave read
+  const size_t blk_row = (size_t)(a.ld >> 5) * 512;  // elements per 16-row block-row
+  const T* gp = g + fm_frag((tk.n0 + wn * 64) >> 4, tk.m0 >> 5, a.ld, lane);
+  const T* xp = x + fm_frag((tk.k0 + wk * 64) >> 4, tk.m0 >> 5, a.ld, lane);
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -35,18 +36,20 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   Frag an[4], bn[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    an[i] = P::load(gp + 16 * i * ld + tk.m0);
-    bn[i] = P::load(xp + 16 * i * ld + tk.m0);
+    an[i] = P::load(gp + i * blk_row);
+    bn[i] = P::load(xp + i * blk_row);
   }
+  const int lr = lane & 15;
   for (int m = tk.m0; m < tk.m1; m += 32) {
     Frag af[4], bf[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) { af[i] = an[i]; bf[i] = bn[i]; }
     if (m + 32 < tk.m1) {
+      const size_t ko = (size_t)((m + 32 - tk.m0) >> 5) * 512;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        an[i] = P::load(gp + 16 * i * ld + m + 32);
-        bn[i] = P::load(xp + 16 * i * ld + m + 32);
+        an[i] = P::load(gp + i * blk_row + ko);
+        bn[i] = P::load(xp + i * blk_row + ko);
       }
     }
 #pragma unroll

@@ -152,15 +152,26 @@ class ActorCritic(nn.Module):
         return PackedLayout(self)
 
 
+def fm_index(r: torch.Tensor, c: torch.Tensor, cols: int) -> torch.Tensor:
+    """Fragment-major element index of (r, c) in a [rows][cols] matrix — csrc/common.h fm_index.
+
+    16x32 blocks, block-row-major; inside a block lane = (r % 16) + 16 * ((c % 32) // 8) holds
+    the 8 elements c % 8 contiguously, so one MFMA operand fragment is one contiguous read."""
+    r = r.to(torch.int64)
+    c = c.to(torch.int64)
+    return (((r // 16) * (cols // 32) + c // 32) * 512 + (((r % 16) + ((c % 32) // 8) * 16) * 8) + (c % 8))
+
+
 class PackedLayout:
     """Padded weight images consumed by the MFMA kernels (csrc/mlp.hip, csrc/rollout.hip).
 
     For each layer (order p_fc1, p_fc2, mu, v_fc1, v_fc2, v) two images in one buffer:
       Wp  [d_out][d_in]: Wp[n][k] = W[n][k] (k < K), Wp[n][K] = b[n], zeros elsewhere
       Wpt [d_in][d_out]: transpose of Wp (dgrad operand)
-    The bias sits in column K because every activation tile carries a constant-1 column
-    at index K (SURVEY §7.4 hard part 1: padded math == unpadded math), which also makes
-    the wgrad GEMM emit the bias gradient as column K.
+    Both are stored FRAGMENT-MAJOR (:func:`fm_index`), so a kernel's B-operand fragment is a
+    contiguous 1 KiB read.  The bias sits in column K because every activation tile carries a
+    constant-1 column at index K (SURVEY §7.4 hard part 1: padded math == unpadded math),
+    which also makes the wgrad GEMM emit the bias gradient as column K.
     ``flat_to_w`` / ``flat_to_wt`` map every flat-buffer index to its element in the two
     images (-1 for log_std); the fused Adam kernel uses them to refresh the images.
     """
@@ -185,14 +196,29 @@ class PackedLayout:
             woff, wn = model.offsets[f"{ls.name}.weight"]
             nn_ = torch.arange(ls.fan_out).repeat_interleave(ls.fan_in)
             kk = torch.arange(ls.fan_in).repeat(ls.fan_out)
-            w_map[woff:woff + wn] = (self.w_off[ls.name] + nn_ * ls.d_in + kk).to(torch.int32)
-            wt_map[woff:woff + wn] = (self.wt_off[ls.name] + kk * ls.d_out + nn_).to(torch.int32)
+            w_map[woff:woff + wn] = (self.w_off[ls.name] + fm_index(nn_, kk, ls.d_in)).to(torch.int32)
+            wt_map[woff:woff + wn] = (self.wt_off[ls.name] + fm_index(kk, nn_, ls.d_out)).to(torch.int32)
             boff, bn = model.offsets[f"{ls.name}.bias"]
             nb = torch.arange(ls.fan_out)
-            w_map[boff:boff + bn] = (self.w_off[ls.name] + nb * ls.d_in + ls.fan_in).to(torch.int32)
-            wt_map[boff:boff + bn] = (self.wt_off[ls.name] + ls.fan_in * ls.d_out + nb).to(torch.int32)
+            kb = torch.full_like(nb, ls.fan_in)
+            w_map[boff:boff + bn] = (self.w_off[ls.name] + fm_index(nb, kb, ls.d_in)).to(torch.int32)
+            wt_map[boff:boff + bn] = (self.wt_off[ls.name] + fm_index(kb, nb, ls.d_out)).to(torch.int32)
         self.flat_to_w = w_map
         self.flat_to_wt = wt_map
+
+    def _rowmajor(self, img: torch.Tensor, off: int, rows: int, cols: int) -> torch.Tensor:
+        r = torch.arange(rows, device=img.device).repeat_interleave(cols)
+        c = torch.arange(cols, device=img.device).repeat(rows)
+        return img[off + fm_index(r, c, cols)].view(rows, cols)
+
+    def image_w(self, img: torch.Tensor, name: str) -> torch.Tensor:
+        """row-major view [d_out][d_in] of layer ``name``'s forward image (tests/debug)."""
+        ls = next(l for l in self.layers if l.name == name)
+        return self._rowmajor(img, self.w_off[name], ls.d_out, ls.d_in)
+
+    def image_wt(self, img: torch.Tensor, name: str) -> torch.Tensor:
+        ls = next(l for l in self.layers if l.name == name)
+        return self._rowmajor(img, self.wt_off[name], ls.d_in, ls.d_out)
 
     def pack(self, flat: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
         """Reference implementation of the image packing (torch; tests + CPU fallback)."""

@@ -22,7 +22,7 @@ from typing import Dict, Optional
 import torch
 
 from ..config import Params
-from ..models.actor_critic import ActorCritic, PackedLayout
+from ..models.actor_critic import ActorCritic, PackedLayout, fm_index
 from ..ops import native
 from ..utils import rng
 from ..utils.obs_stats import RunningObsStats
@@ -106,6 +106,13 @@ class HipEngine:
                       self.g1pT, self.g2pT, self.g3pT, self.g1vT, self.g2vT, self.g3vT]
         self.wg_g = [self.g1pT, self.g2pT, self.g3pT, self.g1vT, self.g2vT, self.g3vT]
         self.wg_x = [self.xT, self.h1pT, self.h2pT, self.xT, self.h1vT, self.h2vT]
+        # constant bias rows of the hidden-activation operands (the kernel writes rows < n_out;
+        # row n_out == 1 makes the wgrad GEMM emit the bias gradient as column K).  The operand
+        # buffers are fragment-major, so "row r" is a scattered index set.
+        cols = torch.arange(self.ldT, device=device)
+        for buf, r in ((self.h1pT, lp1.fan_out), (self.h2pT, lp2.fan_out), (self.h1vT, lv1.fan_out),
+                       (self.h2vT, lv2.fan_out)):
+            buf.view(-1)[fm_index(torch.full_like(cols, r), cols, self.ldT)] = 1.0
         self._build_wgrad_plan(model)
         # ---- optimizer state ----
         n = model.num_params
@@ -135,16 +142,28 @@ class HipEngine:
                     tiles.append((li, n0, k0))
         ntiles = len(tiles)
         max_chunks = max(1, self.ldT // 256)
-        nchunks = max(1, min(max_chunks, -(-1024 // ntiles)))
+        want = -(-1024 // ntiles)                 # >= ~1024 workgroups in flight
+        want = -(-want // 8) * 8                  # whole chunks per XCD (8 XCDs)
+        nchunks = max(1, min(max_chunks, want))
         mc = _r(-(-self.ldT // nchunks), 32)
         chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
         self.nchunks = len(chunks)
         self.chunk_stride = ntiles * WT * WT
         tile_off = {t: i * WT * WT for i, t in enumerate(tiles)}
-        tasks = []
+        # XCD-aware order: workgroups b, b+8, b+16, ... are dealt to the same XCD (observed
+        # round-robin placement; speed only), so all tiles of a batch chunk — which share the
+        # chunk's operand rows — are given consecutive slots of ONE XCD and hit its L2.
+        per_xcd = [[] for _ in range(8)]
         for ci, (m0, m1) in enumerate(chunks):
             for t in tiles:
-                tasks.append([t[0], t[1], t[2], m0, m1, ci * self.chunk_stride + tile_off[t]])
+                per_xcd[ci % 8].append([t[0], t[1], t[2], m0, m1, ci * self.chunk_stride + tile_off[t]])
+        tasks = []
+        j = 0
+        while any(j < len(q) for q in per_xcd):
+            for q in per_xcd:
+                if j < len(q):
+                    tasks.append(q[j])
+            j += 1
         self.tasks_host = torch.tensor(tasks, dtype=torch.int32).reshape(-1).contiguous()
         self.tasks = self.tasks_host.to(self.device)
         self.slab = torch.zeros(self.nchunks * self.chunk_stride, device=self.device, dtype=torch.float32)

@@ -86,8 +86,8 @@ def test_packed_layout_padded_math_equals_unpadded():
     def run(head):
         h = x
         for ls in head:
-            Wp = img[L.w_off[ls.name]:L.w_off[ls.name] + ls.d_out * ls.d_in].view(ls.d_out, ls.d_in)
-            Wpt = img[L.wt_off[ls.name]:L.wt_off[ls.name] + ls.d_in * ls.d_out].view(ls.d_in, ls.d_out)
+            Wp = L.image_w(img, ls.name)
+            Wpt = L.image_wt(img, ls.name)
             assert torch.equal(Wpt, Wp.t())
             xa = torch.zeros(h.shape[0], ls.d_in)
             xa[:, :ls.fan_in] = h
@@ -104,3 +104,18 @@ def test_packed_layout_padded_math_equals_unpadded():
     assert torch.allclose(run(m.value_layers), v_ref, atol=1e-6)
     assert all(ls.d_in % 32 == 0 and ls.d_in > ls.fan_in for ls in L.layers)
     assert pad32(377) == 384
+
+
+def test_fragment_major_index_is_a_bijection_with_contiguous_fragments():
+    from pytorch_dppo_amd.models.actor_critic import fm_index
+    rows, cols = 48, 96
+    r = torch.arange(rows).repeat_interleave(cols)
+    c = torch.arange(cols).repeat(rows)
+    idx = fm_index(r, c, cols)
+    assert torch.equal(torch.sort(idx).values, torch.arange(rows * cols))
+    # lane l of block (rt=1, ks=2) owns row 16 + l%16, cols 64 + 8*(l//16) .. +7 -> offsets base + 8l .. 8l+7
+    base = (1 * (cols // 32) + 2) * 512
+    for lane in (0, 5, 17, 63):
+        rr = torch.full((8,), 16 + lane % 16)
+        cc = 64 + 8 * (lane // 16) + torch.arange(8)
+        assert torch.equal(fm_index(rr, cc, cols), base + 8 * lane + torch.arange(8))
