@@ -24,6 +24,12 @@ void check(const torch::Tensor& t, const char* name, at::ScalarType st, int64_t 
   TORCH_CHECK(t.numel() >= min_numel, name, " has ", t.numel(), " elements, kernel needs >= ", min_numel);
 }
 
+const float* opt_scales(const torch::Tensor& q) {
+  if (!q.defined() || q.numel() == 0) return nullptr;
+  check(q, "qscale", at::kFloat, 6);
+  return q.data_ptr<float>();
+}
+
 struct Layout {
   int off_w[6], off_wt[6], d_in[6], d_out[6], n_out[6];
 };
@@ -58,7 +64,7 @@ void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len
              torch::Tensor mean, torch::Tensor inv_std, torch::Tensor shift, torch::Tensor x_out,
              torch::Tensor actions, torch::Tensor logp, torch::Tensor rewards, torch::Tensor dones,
              torch::Tensor mom, torch::Tensor epstat, std::vector<int64_t> ints, std::vector<int64_t> keys,
-             double reward_clip) {
+             double reward_clip, torch::Tensor qscale) {
   TORCH_CHECK(ints.size() == 11, "ints: kind,E,O,A,S,T,t_base,buf_E,t0,limit,std_var");
   TORCH_CHECK(keys.size() == 4, "keys: env,term,reset,action");
   TORCH_CHECK(rows == 16 || rows == 32, "rows must be 16 or 32");
@@ -81,7 +87,7 @@ void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len
   check(inv_std, "inv_std", at::kFloat, a.O);
   check(shift, "shift", at::kFloat, a.O);
   const int64_t rows_needed = (int64_t)(a.t_base + a.T + 1) * a.E;
-  check(x_out, "x_out", storage_type((int)dt), rows_needed * L.d_in[0]);
+  check(x_out, "x_out", storage_type(dt == 2 ? 1 : (int)dt), rows_needed * L.d_in[0]);
   check(actions, "actions", at::kFloat, (int64_t)(a.t_base + a.T) * a.E * a.A);
   check(logp, "logp", at::kFloat, (int64_t)(a.t_base + a.T) * a.E);
   check(rewards, "rewards", at::kFloat, (int64_t)(a.t_base + a.T) * a.E);
@@ -97,6 +103,7 @@ void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len
   a.off_w1 = L.off_w[0]; a.off_w2 = L.off_w[1]; a.off_w3 = L.off_w[2];
   a.d1 = L.d_in[0]; a.d2 = L.d_in[1]; a.d3 = L.d_in[2];
   a.n1 = L.n_out[0]; a.n2 = L.n_out[1]; a.n3 = L.n_out[2];
+  a.qscale = opt_scales(qscale);
   a.s1 = (float)scales.at(0); a.s2 = (float)scales.at(1); a.s3 = (float)scales.at(2);
   a.log_std = flat.data_ptr<float>();
   a.mean = mean.data_ptr<float>();
@@ -133,7 +140,7 @@ MlpArgs base_mlp(int dt, const Layout& L, const std::vector<double>& scales, tor
   TORCH_CHECK(M > 0, "M must be > 0");
   TORCH_CHECK(L.d_in[0] == L.d_in[3], "both heads share the input width");
   const int64_t nrows_x = x_buf.numel() / L.d_in[0];
-  check(x_buf, "x_buf", storage_type(dt), 1);
+  check(x_buf, "x_buf", storage_type(dt == 2 ? 1 : dt), 1);  // fp8 kernels read a bf16 buffer
   TORCH_CHECK(x_buf.numel() % L.d_in[0] == 0, "x_buf rows must have d_in[0] elements");
   const int64_t limit = std::min<int64_t>(idx_limit, nrows_x);
   if (idx.defined() && idx.numel() > 0) {
@@ -164,12 +171,13 @@ MlpArgs base_mlp(int dt, const Layout& L, const std::vector<double>& scales, tor
 
 void mlp_value(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0, int64_t M, torch::Tensor wimg,
                std::vector<int64_t> layout, std::vector<double> scales, torch::Tensor flat, int64_t A,
-               torch::Tensor v_out, bool check_idx) {
+               torch::Tensor v_out, bool check_idx, torch::Tensor qscale) {
   Layout L = parse_layout(layout);
   MlpArgs a = base_mlp((int)dt, L, scales, x_buf, idx, row0, M, wimg, flat, A, check_idx,
                        std::numeric_limits<int64_t>::max());
   check(v_out, "v_out", at::kFloat, M);
   a.v_out = v_out.data_ptr<float>();
+  a.qscale = opt_scales(qscale);
   launch_mlp_value((int)dt, a, cur_stream());
 }
 
@@ -179,6 +187,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
                torch::Tensor v_old, torch::Tensor mu_prev, torch::Tensor v_prev, std::vector<int64_t> opts,
                std::vector<double> fopts, std::vector<torch::Tensor> tbufs, int64_t ldT, torch::Tensor part,
                bool check_idx) {
+  TORCH_CHECK(dt != 2, "the update runs in bf16 when dtype=fp8 (fp8 gradients underflow e4m3)");
   Layout L = parse_layout(layout);
   TORCH_CHECK(A > 0, "A");
   check(actions, "actions", at::kFloat, A);

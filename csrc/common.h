@@ -67,7 +67,8 @@ template <> struct Prec<DT_FP8> {
     return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
   }
   DEV static T cvt(float x) {
-    __hip_fp8_e4m3 q(x);
+    // saturate to the largest finite e4m3 value instead of producing NaN
+    __hip_fp8_e4m3 q(fminf(fmaxf(x, -448.f), 448.f));
     return *reinterpret_cast<uint8_t*>(&q);
   }
   DEV static float tof(T x) {
@@ -91,6 +92,10 @@ __host__ __device__ inline size_t fm_index(int r, int c, int cols) {
 __host__ __device__ inline size_t fm_frag(int rt, int ks, int cols, int lane) {
   return ((size_t)rt * (size_t)(cols >> 5) + (size_t)ks) * 512u + (size_t)lane * 8u;
 }
+
+// storage precision of the normalised-observation buffer written by the rollout and read by
+// the value/update kernels: fp8 forward kernels keep it in bf16 (the update runs in bf16)
+template <int DT> struct XStore { static constexpr int DTX = (DT == DT_FP8) ? DT_BF16 : DT; };
 
 // LDS row padding: one 16-byte slot per row breaks the power-of-two row stride so the 16
 // lanes of a ds_read_b128 lane group (16 rows, same k) hit distinct bank slots.

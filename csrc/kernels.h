@@ -23,6 +23,7 @@ struct RolloutArgs {
   int d1, d2, d3;      // padded input widths of the 3 layers (P32(K+1))
   int n1, n2, n3;      // real output widths (H1, H2, A)
   float s1, s2, s3;    // dequant scales (fp8; 1 otherwise)
+  const float* qscale; // optional device array of the 6 per-layer dequant scales (overrides s*)
   const float* log_std;  // [A] fp32 master
   int std_var;         // 1: exp(log_std) is the variance (reference DPPO), 0: it is sigma
   // observation normalisation
@@ -54,6 +55,7 @@ struct MlpArgs {
   int d_out[6];        // padded output width per layer
   int n_out[6];        // real output width per layer
   float scale[6];      // fp8 dequant scale per layer
+  const float* qscale; // optional device array of the 6 per-layer scales (overrides scale[])
   int A;
   const float* log_std;  // [A]
   const float* log_std_old;  // [A] dppo_ref: log_std of the previous step

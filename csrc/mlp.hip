@@ -40,6 +40,24 @@ DEV void load_rows(const typename Prec<DT>::T* xb, const int* idx, int row0, int
   }
 }
 
+// fp8 value forward: the observation buffer is bf16 (shared with the bf16 update); convert
+// 8 elements (16 B) per item into the fp8 LDS tile.
+DEV void load_rows_bf16_to_fp8(const __bf16* xb, const int* idx, int row0, int m0, int nvalid, int d,
+                               uint8_t* X, int ldx, int ROWS, int tid) {
+  const int chunks = d / 8;
+  for (int i = tid; i < ROWS * chunks; i += 256) {
+    const int r = i / chunks, c = i - r * chunks;
+    uint8_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r < nvalid) {
+      const int src = idx ? idx[m0 + r] : row0 + m0 + r;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(xb + (size_t)src * d + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = Prec<DT_FP8>::cvt((float)v[j]);
+    }
+    *reinterpret_cast<uint2*>(X + r * ldx + c * 8) = *reinterpret_cast<const uint2*>(q);
+  }
+}
+
 // dst^T (fragment-major, [rows][ldT]) row f, columns m0 + r  <-  tile[r][f],  f < nfeat, r < ROWS.
 // One item = 8 consecutive m of one feature = one contiguous 8-element group of the FM layout.
 template <int DT, int ROWS>
@@ -95,15 +113,23 @@ __global__ __launch_bounds__(256) void mlp_value_kernel(MlpArgs a) {
   T* H2 = cv.take<T>(ROWS * ld2);
   float* V = cv.take<float>(ROWS);
   const T* W = reinterpret_cast<const T*>(a.W);
-  load_rows<DT>(reinterpret_cast<const T*>(a.x_buf), a.idx, a.row0, m0, nvalid, a.d_in[3], X, ldx, ROWS, tid);
+  if constexpr (DT == DT_FP8) {
+    load_rows_bf16_to_fp8(reinterpret_cast<const __bf16*>(a.x_buf), a.idx, a.row0, m0, nvalid, a.d_in[3], X, ldx,
+                          ROWS, tid);
+  } else {
+    load_rows<DT>(reinterpret_cast<const T*>(a.x_buf), a.idx, a.row0, m0, nvalid, a.d_in[3], X, ldx, ROWS, tid);
+  }
   preset_tile<DT>(H1, ld1, ROWS, a.n_out[3], tid, 256);
   preset_tile<DT>(H2, ld2, ROWS, a.n_out[4], tid, 256);
+  const float sc3 = a.qscale ? a.qscale[3] : a.scale[3];
+  const float sc4 = a.qscale ? a.qscale[4] : a.scale[4];
+  const float sc5 = a.qscale ? a.qscale[5] : a.scale[5];
   __syncthreads();
-  layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1, ld1, a.scale[3], wave, lane);
+  layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1, ld1, sc3, wave, lane);
   __syncthreads();
-  layer_gemm<DT, ROWS, NW, EPI_TANH>(H1, ld1, a.d_in[4], W + a.off_w[4], a.n_out[4], H2, ld2, a.scale[4], wave, lane);
+  layer_gemm<DT, ROWS, NW, EPI_TANH>(H1, ld1, a.d_in[4], W + a.off_w[4], a.n_out[4], H2, ld2, sc4, wave, lane);
   __syncthreads();
-  layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32>(H2, ld2, a.d_in[5], W + a.off_w[5], 1, V, 1, a.scale[5], wave, lane);
+  layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32>(H2, ld2, a.d_in[5], W + a.off_w[5], 1, V, 1, sc5, wave, lane);
   __syncthreads();
   if (tid < nvalid) a.v_out[m0 + tid] = V[tid];
 }

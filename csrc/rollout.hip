@@ -59,7 +59,12 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
   const T* W1 = W + a.off_w1;
   const T* W2 = W + a.off_w2;
   const T* W3 = W + a.off_w3;
-  T* xo = reinterpret_cast<T*>(a.x_out);
+  using PX = Prec<XStore<DT>::DTX>;              // buffer precision (bf16 when DT is fp8)
+  typename PX::T* xo = reinterpret_cast<typename PX::T*>(a.x_out);
+  // per-layer dequant scales: device array (fp8 images, refreshed on-device) or kernel args
+  const float sc1 = a.qscale ? a.qscale[0] : a.s1;
+  const float sc2 = a.qscale ? a.qscale[1] : a.s2;
+  const float sc3 = a.qscale ? a.qscale[2] : a.s3;
 
   // ---- load state, zero the padded activation tiles (pad columns stay constant) ----
   for (int i = tid; i < ROWS * S; i += 256) {
@@ -102,20 +107,19 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
         } else {
           xv = (d == O) ? 1.f : 0.f;
         }
-        T q = P::cvt(xv);
-        xs[r * ld1 + d] = q;
-        if (r < nvalid) xo[((size_t)tb * a.buf_E + e0 + r) * a.d1 + d] = q;
+        xs[r * ld1 + d] = P::cvt(xv);
+        if (r < nvalid) xo[((size_t)tb * a.buf_E + e0 + r) * a.d1 + d] = PX::cvt(xv);
       }
       if (d < O) { s1[d] += ls1; s2[d] += ls2; }
     }
     if (last) break;
     __syncthreads();
     // ---- (b) policy MLP ----
-    layer_gemm<DT, ROWS, NW, EPI_TANH>(xs, ld1, a.d1, W1, a.n1, h1, ld2, a.s1, wave, lane);
+    layer_gemm<DT, ROWS, NW, EPI_TANH>(xs, ld1, a.d1, W1, a.n1, h1, ld2, sc1, wave, lane);
     __syncthreads();
-    layer_gemm<DT, ROWS, NW, EPI_TANH>(h1, ld2, a.d2, W2, a.n2, h2, ld3, a.s2, wave, lane);
+    layer_gemm<DT, ROWS, NW, EPI_TANH>(h1, ld2, a.d2, W2, a.n2, h2, ld3, sc2, wave, lane);
     __syncthreads();
-    layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32>(h2, ld3, a.d3, W3, a.n3, mu, A, a.s3, wave, lane);
+    layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32>(h2, ld3, a.d3, W3, a.n3, mu, A, sc3, wave, lane);
     __syncthreads();
     // ---- (c) sample a = mu + sigma * eps ----
     const uint32_t kstep = a.t0 + (uint32_t)step;

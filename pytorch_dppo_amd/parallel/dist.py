@@ -63,11 +63,20 @@ class DistContext:
         if self.enabled:
             dist.broadcast(t, src=src)
 
-    def allreduce_obs_moments(self, count: float, s1: torch.Tensor, s2: torch.Tensor):
-        """global (count, S1, S2) about a shift every rank shares — exact merge (R2)."""
+    def allreduce_obs_moments(self, count: float, s1: torch.Tensor, s2: torch.Tensor,
+                              count_uniform: bool = False):
+        """global (count, S1, S2) about a shift every rank shares — exact merge (R2).
+
+        ``count_uniform``: every rank contributed the same (host-known) count, so the global
+        count is count * world_size and no device->host read is needed (the hot path)."""
         if not self.enabled:
             return count, s1, s2
         O = s1.numel()
+        if count_uniform:
+            buf = torch.cat([s1.reshape(-1).to(self.device, torch.float64),
+                             s2.reshape(-1).to(self.device, torch.float64)])
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+            return count * self.world_size, buf[:O], buf[O:]
         buf = torch.empty(1 + 2 * O, dtype=torch.float64, device=self.device)
         buf[0] = count
         buf[1:1 + O] = s1.reshape(-1).to(self.device, torch.float64)
@@ -76,11 +85,13 @@ class DistContext:
         return float(buf[0].item()), buf[1:1 + O].clone(), buf[1 + O:].clone()
 
     def allreduce_scalars(self, vals: Dict[str, float], op: str = "sum") -> Dict[str, float]:
-        if not self.enabled:
-            return dict(vals)
+        """values may be python numbers or 0-d device tensors (stacked without a host read)."""
         keys = sorted(vals)
-        t = torch.tensor([float(vals[k]) for k in keys], dtype=torch.float64, device=self.device)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
+        parts = [vals[k].reshape(1).to(self.device, torch.float64) if torch.is_tensor(vals[k])
+                 else torch.tensor([float(vals[k])], dtype=torch.float64, device=self.device) for k in keys]
+        t = torch.cat(parts)
+        if self.enabled:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
         return {k: float(x) for k, x in zip(keys, t.tolist())}
 
     def allreduce_tensor_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:

@@ -44,15 +44,19 @@ class HipEngine:
                  device: torch.device, action_rank: int):
         if device.type != "cuda":
             raise RuntimeError("HipEngine needs a HIP device")
-        if params.dtype == "fp8":
-            raise NotImplementedError("fp8 GEMM path is not wired yet; use --dtype bf16|fp32")
         self.ext = native.load()
         self.p = params
         self.model = model
         self.env = env
         self.stats = stats
         self.device = device
-        self.dt = native.DT_CODE[params.dtype]
+        # dtype fp8 (BASELINE config 5): the forward GEMMs of the rollout policy and of the value
+        # pass run on the OCP e4m3 MFMA (v_mfma_f32_16x16x32_fp8_fp8) with per-layer weight
+        # scales; the update (loss, dgrad, wgrad) runs in bf16 because per-row gradients of
+        # magnitude ~1/batch underflow e4m3.  fp32 / bf16 use one precision throughout.
+        self.fp8 = params.dtype == "fp8"
+        self.dt = native.DT_CODE["bf16"] if self.fp8 else native.DT_CODE[params.dtype]
+        self.dt_fwd = native.DT_CODE[params.dtype]
         self.sdtype = STORAGE[self.dt]
         T, E, O, A = params.rollout_len, env.E, env.O, env.A
         self.T, self.E, self.O, self.A = T, E, O, A
@@ -68,6 +72,20 @@ class HipEngine:
         self.w_map = L.flat_to_w.to(device)
         self.wt_map = L.flat_to_wt.to(device)
         self.wimg = torch.zeros(L.total, dtype=self.sdtype, **dev)
+        self.qscale = torch.empty(0, **f32)
+        if self.fp8:
+            self.wimg_fwd = torch.zeros(L.total, dtype=torch.uint8, **dev)
+            self.qscale = torch.ones(6, **f32)
+            # layer id of every flat parameter (-1: log_std) for the per-layer amax
+            lid = torch.full((model.num_params,), -1, dtype=torch.int64)
+            for li, l in enumerate(ls):
+                for suffix in ("weight", "bias"):
+                    o, n_ = model.offsets[f"{l.name}.{suffix}"]
+                    lid[o:o + n_] = li
+            self.layer_id = lid.to(device)
+            self.layer_slices = [[model.offsets[f"{l.name}.{s}"] for s in ("weight", "bias")] for l in ls]
+        else:
+            self.wimg_fwd = self.wimg
         self.d0 = ls[0].d_in
         self.x_buf = torch.zeros((T + 1) * E, self.d0, dtype=self.sdtype, **dev)
         self.actions = torch.zeros(self.N, A, **f32)
@@ -195,6 +213,22 @@ class HipEngine:
         """re-pack the weight images from the fp32 master (after init / load / broadcast)."""
         self.ext.pack(self.model.flat.data, self.wimg, self.w_map, self.wt_map, self.dt, self.no_q)
         self.adam_state[0] = float(self.adam_step)
+        self.refresh_fwd_image()
+
+    @torch.no_grad()
+    def refresh_fwd_image(self) -> None:
+        """fp8 only: per-layer amax scales + e4m3 image of the current weights, all on the
+        device (no host sync).  s_l = amax_l / 416 keeps every weight inside e4m3's finite range
+        (448) with headroom; the kernels multiply each layer's accumulator by s_l."""
+        if not self.fp8:
+            return
+        flat = self.model.flat.data
+        amax = torch.stack([torch.maximum(flat[wo:wo + wn].abs().amax(), flat[bo:bo + bn].abs().amax())
+                            for (wo, wn), (bo, bn) in self.layer_slices])
+        s = torch.clamp(amax / 416.0, min=1e-12)
+        self.qscale.copy_(s)
+        qmul = torch.where(self.layer_id >= 0, (1.0 / s)[self.layer_id.clamp(min=0)], torch.zeros_like(flat))
+        self.ext.pack(flat, self.wimg_fwd, self.w_map, self.wt_map, self.dt_fwd, qmul)
 
     def current_obs(self) -> torch.Tensor:
         return self.env.observe()
@@ -212,14 +246,15 @@ class HipEngine:
         ints = [kp["kind"], self.E, self.O, self.A, e.state_dim, T, t_base, self.E, t0 & 0xFFFFFFFF,
                 kp["limit"], 1 if self.p.std_convention == "var" else 0]
         keys = [kp["key_env"], kp["key_term"], kp["key_reset"], self.key_action]
-        self.ext.rollout(self.dt, ROLL_ROWS, e.state, e.ep_len, e.ep_ret, self.wimg, self.layout, self.scales,
-                         self.model.flat.data, norm.mean_f32, norm.inv_std_f32, shift, self.x_buf, self.actions,
-                         self.logp, self.rewards, self.dones, self.mom, self.epstat, ints, keys,
-                         float(self.p.reward_clip))
+        self.ext.rollout(self.dt_fwd, ROLL_ROWS, e.state, e.ep_len, e.ep_ret, self.wimg_fwd, self.layout,
+                         self.scales, self.model.flat.data, norm.mean_f32, norm.inv_std_f32, shift, self.x_buf,
+                         self.actions, self.logp, self.rewards, self.dones, self.mom, self.epstat, ints, keys,
+                         float(self.p.reward_clip), self.qscale)
 
     @torch.no_grad()
     def rollout(self) -> Dict:
         p = self.p
+        self.refresh_fwd_image()   # fp8: weights changed during the previous update
         shift = self.stats.shift().clone()
         if p.obs_norm_update == "rollout":
             self._launch_rollout(self.T, 0, self.env.t, self.stats, shift)
@@ -240,15 +275,15 @@ class HipEngine:
                 s1 += self.mom[:, 0].double().sum(0)
                 s2 += self.mom[:, 1].double().sum(0)
                 ep += self.epstat.double().sum(0)
-        ep = ep.tolist()
+        # everything stays on the device: no host sync inside the iteration
         return {"count": float(self.N), "s1": s1, "s2": s2, "shift": shift,
-                "ep_return_sum": float(ep[0]), "ep_count": float(ep[1])}
+                "ep_return_sum": ep[0], "ep_count": ep[1]}
 
     @torch.no_grad()
     def values(self) -> None:
         M = (self.T + 1) * self.E
-        self.ext.mlp_value(self.dt, self.x_buf, self.empty, 0, M, self.wimg, self.layout, self.scales,
-                           self.model.flat.data, self.A, self.values_buf, False)
+        self.ext.mlp_value(self.dt_fwd, self.x_buf, self.empty, 0, M, self.wimg_fwd, self.layout, self.scales,
+                           self.model.flat.data, self.A, self.values_buf, False, self.qscale)
 
     @torch.no_grad()
     def gae(self) -> None:

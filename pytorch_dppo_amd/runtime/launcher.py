@@ -69,6 +69,7 @@ def run_worker(params: Params, ctx: DistContext, max_iters: Optional[int] = None
                 save(w, ctx, params.checkpoint_dir)
             if max_iters is not None and n >= max_iters:
                 break
+        w.flush_pending()
         if params.checkpoint_dir:
             save(w, ctx, params.checkpoint_dir)
     finally:

@@ -63,10 +63,11 @@ class DPPOWorker:
         self._stats_initialised = False
         self.last_metrics: Dict = {}
         self._perm_gen = torch.Generator(device="cpu")
+        self._pending = None          # (async all-reduce work, extra) under --overlap-rollout
 
     # ---------------------------------------------------------------------------------------
-    def _merge_stats(self, count, s1, s2, shift) -> None:
-        count, s1, s2 = self.ctx.allreduce_obs_moments(count, s1, s2)
+    def _merge_stats(self, count, s1, s2, shift, count_uniform: bool = False) -> None:
+        count, s1, s2 = self.ctx.allreduce_obs_moments(count, s1, s2, count_uniform=count_uniform)
         self.stats.merge_moments(count, s1, s2, shift)
 
     def init_stats(self) -> None:
@@ -93,9 +94,15 @@ class DPPOWorker:
         t0 = time.perf_counter()
         tm.start("rollout")
         ro = eng.rollout()
+        # --overlap-rollout (SURVEY §5.8 option b): the previous iteration's final gradient
+        # all-reduce ran on RCCL's stream concurrently with the rollout kernel just enqueued
+        # (which acts with the pre-update weights: a 1-update policy lag, safe for PPO because
+        # logp_old is recorded at rollout).  Wait for it and apply that Adam step now.
+        self.flush_pending()
         tm.stop("rollout")
         tm.start("obs_stats")
-        self._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"])
+        # every rank collects exactly T*E steps -> the global count is host-known (no sync)
+        self._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"], count_uniform=True)
         if p.obs_norm_update == "step" and hasattr(eng, "after_stats_merge"):
             eng.after_stats_merge()
         tm.stop("obs_stats")
@@ -124,11 +131,16 @@ class DPPOWorker:
                     if idx.numel() < mb:
                         idx = torch.cat([idx, perm[:mb - idx.numel()]])
                 eng.grad(idx)
-                self.ctx.allreduce_grads(eng.grad_flat, mean=mean)
                 extra = 0.0
                 if p.compat and self.updates == 0:
                     extra = 1.0  # Q1: Shared_grad_buffers start at ones (model.py:51)
-                eng.apply(extra)
+                last = epoch == p.num_epoch - 1 and b == nmb - 1
+                if p.overlap_rollout and last and not mean and self.ctx.enabled:
+                    work = self.ctx.allreduce_grads(eng.grad_flat, async_op=True)
+                    self._pending = (work, extra)      # applied after the next rollout launch
+                else:
+                    self.ctx.allreduce_grads(eng.grad_flat, mean=mean)
+                    eng.apply(extra)
                 self.updates += 1
         tm.stop("update")
         eng.sync()
@@ -150,6 +162,17 @@ class DPPOWorker:
         self.last_metrics = m
         return m
 
+    def flush_pending(self) -> None:
+        """complete a deferred (overlapped) all-reduce + Adam step, if any."""
+        pend = getattr(self, "_pending", None)
+        if pend is None:
+            return
+        work, extra = pend
+        self._pending = None
+        if work is not None:
+            work.wait()            # orders the compute stream after RCCL's (no host block on GPU)
+        self.engine.apply(extra)
+
     def should_stop(self) -> bool:
         p = self.p
         if p.max_iters and self.iteration >= p.max_iters:
@@ -162,6 +185,7 @@ class DPPOWorker:
 
     # -- checkpoint ---------------------------------------------------------------------------
     def trainer_state(self) -> Dict:
+        self.flush_pending()
         eng = self.engine
         return {"adam_m": eng.adam_m.detach().cpu(), "adam_v": eng.adam_v.detach().cpu(),
                 "adam_step": eng.adam_step, "obs_stats": self.stats.state_dict(),

@@ -1,0 +1,13 @@
+#!/bin/bash
+# bench variants on one box: dtype x overlap; each run time-limited, stop on fault
+set -u
+OUT=${OUT:-gpurun_out}
+mkdir -p "$OUT"
+for v in "bf16" "bf16 --overlap-rollout" "fp8" "fp32"; do
+  set -- $v
+  name="bench_$(echo $v | tr ' -' '__')"
+  timeout -k 10 300 python bench.py --steps 5 --warmup 2 --dtype $v > "$OUT/$name.log" 2>&1
+  rc=$?
+  echo "== $name rc=$rc"; tail -1 "$OUT/$name.log" | cut -c1-260
+  [ $rc -eq 0 ] || exit $rc
+done

@@ -165,3 +165,31 @@ def test_resume_continues_bit_identically_single_process(tmp_path):
     w_res, _ = run_worker(dppo_preset(max_iters=3, resume=ck, **base), DistContext(), evaluator=False, quiet=True)
     assert w_res.iteration == 3
     assert torch.equal(w_full.model.flat.data, w_res.model.flat.data)
+
+
+def _worker_overlap(rank, world, port, out_dir):
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    ctx = _init(rank, world, port)
+    res = {}
+    for ov in (False, True):
+        p = dppo_preset(env_name="HalfCheetah-v2", num_envs=8, exploration_size=64, batch_size=64, num_epoch=2,
+                        overlap_rollout=ov, num_processes=world, verify_sync_every=1)
+        w = DPPOWorker(p, ctx)
+        for _ in range(3):
+            m = w.iteration_step()
+        w.flush_pending()
+        res[ov] = (w.model.flat.data.clone(), m["replicas_in_sync"], w.updates, w.engine.adam_step)
+    torch.save(res, os.path.join(out_dir, f"o{rank}.pt"))
+    ctx.destroy()
+
+
+def test_overlap_rollout_defers_last_step_but_applies_every_update(tmp_path):
+    assert _join(_spawn(_worker_overlap, 2, str(tmp_path)), 240) == [0, 0]
+    r0 = torch.load(tmp_path / "o0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "o1.pt", weights_only=True)
+    for ov in (False, True):
+        assert r0[ov][1] and r1[ov][1]                       # replicas identical in both modes
+        assert r0[ov][2] == r0[ov][3] == 6                    # every update applied exactly once
+        assert torch.equal(r0[ov][0], r1[ov][0])
+    # the lagged rollouts see different weights -> a (slightly) different trajectory
+    assert not torch.equal(r0[False][0], r0[True][0])

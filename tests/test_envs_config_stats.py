@@ -150,3 +150,34 @@ def test_obs_stats_state_dict_uses_reference_names():
     st2 = RunningObsStats(3)
     st2.load_state_dict(sd)
     assert torch.equal(st2.mean, st.mean) and st2.n == st.n
+
+
+# ---------------- API parity utilities ----------------
+def test_counter_and_traffic_light_over_store():
+    import torch.distributed as dist
+    from pytorch_dppo_amd.utils.sync import Counter, TrafficLight
+    store = dist.HashStore()
+    c, light = Counter(store), TrafficLight(store)
+    assert c.get() == 0 and light.get() is False
+    for _ in range(3):
+        c.increment()
+    assert c.get() == 3
+    c.reset()
+    assert c.get() == 0
+    before = light.get()
+    light.switch()
+    assert light.get() != before
+
+
+def test_replay_memory_reference_api():
+    from pytorch_dppo_amd.utils.sync import ReplayMemory
+    mem = ReplayMemory(5, seed=0)
+    states = [torch.full((1, 2), float(i)) for i in range(7)]
+    acts = [torch.full((1, 1), float(i)) for i in range(7)]
+    mem.push([states, acts])
+    assert len(mem) == 5                       # FIFO eviction kept the last 5
+    s, a = mem.sample(5)
+    assert s.shape == (5, 2) and a.shape == (5, 1)
+    assert sorted(a.view(-1).tolist()) == [2.0, 3.0, 4.0, 5.0, 6.0]
+    mem.clear()
+    assert len(mem) == 0

@@ -59,7 +59,8 @@ def test_pack_matches_reference_layout(dtype):
 
 
 @pytest.mark.parametrize("env_name,dtype,tol", [("Pendulum-v0", "fp32", 2e-5), ("HalfCheetah-v2", "fp32", 2e-5),
-                                                ("Humanoid-v2", "fp32", 5e-5), ("Humanoid-v2", "bf16", 3e-2)])
+                                                ("Humanoid-v2", "fp32", 5e-5), ("Humanoid-v2", "bf16", 3e-2),
+                                                ("Humanoid-v2", "fp8", 1.5e-1), ("HalfCheetah-v2", "fp8", 1.5e-1)])
 def test_value_forward(env_name, dtype, tol):
     p = dppo_preset(device="gpu", env_name=env_name, num_envs=37, exploration_size=37 * 5,
                     batch_size=37 * 5, dtype=dtype)
@@ -262,6 +263,30 @@ def test_engine_iteration_matches_torch_engine_fp32():
     assert d.max().item() <= 2 * pg.lr * pg.num_epoch + 1e-6
     assert (d > 1e-5).float().mean().item() < 0.01
     assert abs(mg["loss_value"] - mc["loss_value"]) < 1e-3 * (1 + abs(mc["loss_value"]))
+
+
+def test_fp8_rollout_tracks_fp32_and_engine_trains():
+    """fp8 e4m3 forward GEMMs (rollout policy + value): actions close to the fp32 path for the same
+    noise; a full fp8 iteration (bf16 update) stays finite and the fp8 scales follow amax."""
+    common = dict(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 4, batch_size=64 * 4,
+                  num_epoch=2)
+    e32, m32, env32, st32 = _engine(dppo_preset(dtype="fp32", **common))
+    e8, m8, env8, st8 = _engine(dppo_preset(dtype="fp8", **common))
+    assert torch.equal(m32.flat.data, m8.flat.data)
+    for st, env in ((st32, env32), (st8, env8)):
+        st.observes(env.observe())
+    e32.rollout()
+    e8.rollout()
+    mu_err = (e8.actions - e32.actions).abs()
+    assert mu_err.mean().item() < 0.05, mu_err.mean().item()
+    amax = torch.stack([m8.view(f"{n}.weight").abs().amax() for n in ("p_fc1", "p_fc2", "mu", "v_fc1", "v_fc2", "v")])
+    assert torch.all(e8.qscale * 416.0 >= amax * (1 - 1e-6))
+    e8.values()
+    e8.gae()
+    e8.begin_update()
+    e8.grad(None)
+    e8.apply()
+    assert torch.isfinite(m8.flat.data).all() and torch.isfinite(e8.values_buf).all()
 
 
 def test_rccl_world1_allreduce_and_training_step():
