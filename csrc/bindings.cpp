@@ -276,16 +276,38 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
 }
 
 void grad_gather(torch::Tensor slab, torch::Tensor src_off, int64_t nchunks, int64_t stride, torch::Tensor part,
-                 int64_t nblk, int64_t npart, int64_t A, double scale, torch::Tensor grad) {
+                 int64_t nblk, int64_t npart, int64_t A, double scale, torch::Tensor grad, torch::Tensor loss_out) {
   const int64_t n = grad.numel();
   check(grad, "grad", at::kFloat, n);
   check(src_off, "src_off", at::kInt, n);
   check(slab, "slab", at::kFloat, nchunks * stride);
   check(part, "part", at::kFloat, nblk * npart);
+  check(loss_out, "loss_out", at::kFloat, 8);
   TORCH_CHECK(npart >= 8 + A, "npart");
   launch_grad_gather(slab.data_ptr<float>(), src_off.data_ptr<int>(), (int)nchunks, (int)stride,
                      part.data_ptr<float>(), (int)nblk, (int)npart, (int)A, (float)scale, grad.data_ptr<float>(),
-                     (int)n, cur_stream());
+                     (int)n, loss_out.data_ptr<float>(), cur_stream());
+}
+
+void obs_reduce(torch::Tensor part, int64_t nblk, int64_t O, torch::Tensor s12) {
+  check(part, "part", at::kFloat, nblk * 2 * O);
+  check(s12, "s12", at::kDouble, 2 * O);
+  launch_obs_reduce(part.data_ptr<float>(), (int)nblk, (int)O, s12.data_ptr<double>(), cur_stream());
+}
+
+void obs_merge(torch::Tensor s12, double count, double n_a, torch::Tensor shift, torch::Tensor mean, torch::Tensor m2,
+               torch::Tensor mean_f32, torch::Tensor inv_std, double var_floor) {
+  const int64_t O = mean.numel();
+  TORCH_CHECK(count > 0, "count must be positive");
+  check(s12, "s12", at::kDouble, 2 * O);
+  check(shift, "shift", at::kFloat, O);
+  check(mean, "mean", at::kDouble, O);
+  check(m2, "m2", at::kDouble, O);
+  check(mean_f32, "mean_f32", at::kFloat, O);
+  check(inv_std, "inv_std", at::kFloat, O);
+  launch_obs_merge(s12.data_ptr<double>(), (int)O, count, n_a, shift.data_ptr<float>(), mean.data_ptr<double>(),
+                   m2.data_ptr<double>(), mean_f32.data_ptr<float>(), inv_std.data_ptr<float>(), var_floor,
+                   cur_stream());
 }
 
 void gae(torch::Tensor rewards, torch::Tensor values, torch::Tensor dones, torch::Tensor adv, torch::Tensor ret,
@@ -347,6 +369,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad", &wgrad);
   m.def("grad_gather", &grad_gather);
   m.def("gae", &gae);
+  m.def("obs_reduce", &obs_reduce);
+  m.def("obs_merge", &obs_merge);
   m.def("adam", &adam);
   m.def("pack", &pack);
   m.attr("arch") = "gfx950";

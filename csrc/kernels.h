@@ -106,7 +106,7 @@ size_t mlp_train_lds_bytes(int dt, const MlpArgs& a);
 void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
 void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int chunk_stride,
                         const float* part, int nblk, int npart, int A, float scale, float* grad,
-                        int n, hipStream_t s);
+                        int n, float* loss_out, hipStream_t s);
 void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
                 int T, int E, float gamma, float lam, hipStream_t s);
 void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, float b1, float b2,
@@ -115,6 +115,9 @@ void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, 
                  hipStream_t s);
 void launch_pack(const float* p, int n, void* wimg, const int* w_map, const int* wt_map, int dt,
                  const float* img_scale, hipStream_t s);
+void launch_obs_reduce(const float* part, int nblk, int O, double* s12, hipStream_t s);
+void launch_obs_merge(const double* s12, int O, double count, double n_a, const float* shift, double* mean,
+                      double* m2, float* mean_f32, float* inv_std, double var_floor, hipStream_t s);
 }
 
 // rows per workgroup of mlp_train_kernel: the fp32 tile set does not fit 160 KiB of LDS at 32

@@ -69,51 +69,68 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
   const int ntiles = (n_real + 15) >> 4;
   const int lr = lane & 15;
   const int lk = (lane >> 4) * 8;
-  for (int nt0 = wave * NT2; nt0 < ntiles; nt0 += NW * NT2) {
-    const bool two = (nt0 + 1) < ntiles;
-    f32x4 acc[NT2][RB];
-#pragma unroll
-    for (int t = 0; t < NT2; ++t)
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[t][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // B is fragment-major (FM): block (row tile, k-step) = 512 contiguous elements
-    const T* bp0 = B + fm_frag(nt0, 0, kdim, lane);
-    // the second tile's pointer is clamped to the first when it does not exist (loads stay in
-    // bounds; its results are discarded)
-    const T* bp1 = two ? bp0 + (size_t)ksteps * 512 : bp0;
-    const T* ap = A + lr * lda + lk;
-    Frag bc0[KC], bc1[KC], bn0[KC], bn1[KC];
-    // k-steps past the end re-load the last valid step (in bounds; never consumed)
+  const T* ap = A + lr * lda + lk;
+  // This wave's work is a flat stream of (tile pair, k-chunk) steps; the B fragments of step
+  // s+1 — including the FIRST chunk of the wave's next tile pair — are loaded while step s
+  // computes, so only the layer's very first chunk pays the L2 round trip.
+  const int first_pair = wave * NT2;
+  if (first_pair >= ntiles) return;
+  const int npairs = (ntiles - first_pair + NW * NT2 - 1) / (NW * NT2);
+  const int nsteps = npairs * nchunks;
+  auto bptr = [&](int nt0, bool two, int kc, int j, const T*& p0, const T*& p1) {
+    const int ks = min(kc * KC + j, ksteps - 1);   // past-the-end steps re-load the last one
+    p0 = B + fm_frag(nt0, ks, kdim, lane);
+    p1 = two ? p0 + (size_t)ksteps * 512 : p0;    // absent 2nd tile: alias (results discarded)
+  };
+  Frag bc0[KC], bc1[KC], bn0[KC], bn1[KC];
+  {
+    const bool two = (first_pair + 1) < ntiles;
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
-      const int ks = min(j, ksteps - 1);
-      bc0[j] = P::load(bp0 + ks * 512);
-      bc1[j] = P::load(bp1 + ks * 512);
+      const T *p0, *p1;
+      bptr(first_pair, two, 0, j, p0, p1);
+      bc0[j] = P::load(p0);
+      bc1[j] = P::load(p1);
     }
-    for (int kc = 0; kc < nchunks; ++kc) {
-      if (kc + 1 < nchunks) {
+  }
+  f32x4 acc[NT2][RB];
 #pragma unroll
-        for (int j = 0; j < KC; ++j) {
-          const int ks = min((kc + 1) * KC + j, ksteps - 1);
-          bn0[j] = P::load(bp0 + ks * 512);
-          bn1[j] = P::load(bp1 + ks * 512);
-        }
-      }
+  for (int t = 0; t < NT2; ++t)
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) acc[t][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int nt0 = first_pair, kc = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    const bool two = (nt0 + 1) < ntiles;
+    // ---- prefetch step s+1 ----
+    if (s + 1 < nsteps) {
+      int nt1 = nt0, kc1 = kc + 1;
+      if (kc1 == nchunks) { kc1 = 0; nt1 = nt0 + NW * NT2; }
+      const bool two1 = (nt1 + 1) < ntiles;
 #pragma unroll
       for (int j = 0; j < KC; ++j) {
-        const int ks = kc * KC + j;
-        if (ks < ksteps) {
+        const T *p0, *p1;
+        bptr(nt1, two1, kc1, j, p0, p1);
+        bn0[j] = P::load(p0);
+        bn1[j] = P::load(p1);
+      }
+    }
+    // ---- compute chunk kc of pair nt0 ----
 #pragma unroll
-          for (int rb = 0; rb < RB; ++rb) {
-            Frag a = P::load(ap + rb * 16 * lda + ks * 32);
-            acc[0][rb] = P::mma(acc[0][rb], a, bc0[j]);
-            acc[1][rb] = P::mma(acc[1][rb], a, bc1[j]);
-          }
+    for (int j = 0; j < KC; ++j) {
+      const int ks = kc * KC + j;
+      if (ks < ksteps) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          Frag a = P::load(ap + rb * 16 * lda + ks * 32);
+          acc[0][rb] = P::mma(acc[0][rb], a, bc0[j]);
+          acc[1][rb] = P::mma(acc[1][rb], a, bc1[j]);
         }
       }
-#pragma unroll
-      for (int j = 0; j < KC; ++j) { bc0[j] = bn0[j]; bc1[j] = bn1[j]; }
     }
+#pragma unroll
+    for (int j = 0; j < KC; ++j) { bc0[j] = bn0[j]; bc1[j] = bn1[j]; }
+    if (++kc < nchunks) continue;
+    // ---- pair complete: epilogue, then advance to the wave's next pair ----
 #pragma unroll
     for (int t = 0; t < NT2; ++t) {
       const int c = (nt0 + t) * 16 + lr;
@@ -146,6 +163,12 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
         }
       }
     }
+#pragma unroll
+    for (int t = 0; t < NT2; ++t)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[t][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    kc = 0;
+    nt0 += NW * NT2;
   }
 }
 

@@ -72,27 +72,34 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 //                    strided partial sums + LDS tree: fixed order, deterministic)
 // Workgroups [A, grid): grad[i] = scale * sum_c slab[c*stride + src_off[i]], i in [A, n)
 //                    (fixed chunk order: deterministic; no float atomics anywhere)
+// Workgroups [A, A+8): loss_out[q] = sum_b part[b*npart + q] (loss-term sums for logging).
 __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restrict__ slab,
                                                           const int* __restrict__ src_off, int nchunks,
                                                           int stride, const float* __restrict__ part,
                                                           int nblk, int npart, int A, float scale,
-                                                          float* __restrict__ grad, int n) {
-  if ((int)blockIdx.x < A) {
+                                                          float* __restrict__ grad, int n,
+                                                          float* __restrict__ loss_out) {
+  const int nred = A + 8;
+  if ((int)blockIdx.x < nred) {
     __shared__ float red[256];
     const int j = blockIdx.x;
+    const int col = j < A ? 8 + j : j - A;
     float s = 0.f;
-    for (int b = threadIdx.x; b < nblk; b += 256) s += part[(size_t)b * npart + 8 + j];
+    for (int b = threadIdx.x; b < nblk; b += 256) s += part[(size_t)b * npart + col];
     red[threadIdx.x] = s;
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
       if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
       __syncthreads();
     }
-    if (threadIdx.x == 0) grad[j] = red[0] * scale;
+    if (threadIdx.x == 0) {
+      if (j < A) grad[j] = red[0] * scale;
+      else loss_out[j - A] = red[0];
+    }
     return;
   }
-  const int nb = gridDim.x - A;
-  for (int i = A + (blockIdx.x - A) * 256 + threadIdx.x; i < n; i += nb * 256) {
+  const int nb = gridDim.x - nred;
+  for (int i = A + (blockIdx.x - nred) * 256 + threadIdx.x; i < n; i += nb * 256) {
     const int o = src_off[i];
     float s = 0.f;
     for (int c = 0; c < nchunks; ++c) s += slab[(size_t)c * stride + o];
@@ -112,12 +119,12 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
 
 extern "C" void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int chunk_stride,
                                    const float* part, int nblk, int npart, int A, float scale, float* grad,
-                                   int n, hipStream_t s) {
+                                   int n, float* loss_out, hipStream_t s) {
   int grid = (n - A + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
-  grid += A;
+  grid += A + 8;
   hipLaunchKernelGGL(grad_gather_kernel, dim3(grid), dim3(256), 0, s, slab, src_off, nchunks, chunk_stride,
-                     part, nblk, npart, A, scale, grad, n);
+                     part, nblk, npart, A, scale, grad, n, loss_out);
   HIP_CHECK_LAUNCH();
 }

@@ -31,6 +31,9 @@ class RunningObsStats:
         # fp32 images consumed by the normalisation prologue of the kernels
         self.mean_f32 = torch.zeros(self.O, dtype=torch.float32, device=self.device)
         self.inv_std_f32 = torch.ones(self.O, dtype=torch.float32, device=self.device)
+        # optional fused device merge (set by the HIP engine: csrc/obs.hip obs_merge); called as
+        # fn(s1, s2, count, n_a, shift) and updates mean / mean_diff / fp32 images in place
+        self.device_merge = None
         self._refresh()
 
     @property
@@ -58,6 +61,10 @@ class RunningObsStats:
                       shift: torch.Tensor) -> None:
         """Chan merge of a batch given by its moments about ``shift``."""
         if count <= 0:
+            return
+        if self.device_merge is not None and s1.is_cuda:
+            self.device_merge(s1, s2, float(count), float(self.n), shift)
+            self.n = self.n + count
             return
         s1 = s1.to(self.device, torch.float64)
         s2 = s2.to(self.device, torch.float64)

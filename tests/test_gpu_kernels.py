@@ -116,6 +116,31 @@ def test_rollout_matches_torch_engine(env_name):
     assert abs(ro_h["ep_count"] - ro_t["ep_count"]) < 0.5
 
 
+def test_obs_reduce_and_merge_kernels_match_torch_welford():
+    ext = _ext()
+    O, nblk = 37, 19
+    g = torch.Generator(device="cpu").manual_seed(4)
+    ref = RunningObsStats(O, DEV)
+    dev_st = RunningObsStats(O, DEV)
+    for it in range(3):
+        x = (torch.randn(nblk * 8, O, generator=g) * 3 + 10 * it).to(DEV)
+        shift = ref.shift().clone()
+        c, s1, s2 = RunningObsStats.moments(x, shift)
+        ref.merge_moments(c, s1, s2, shift)
+        # partials per block as the rollout kernel leaves them
+        d = (x - dev_st.shift()).view(nblk, 8, O)
+        part = torch.stack([d.sum(1), (d * d).sum(1)], 1).float().contiguous()
+        s12 = torch.zeros(2, O, dtype=torch.float64, device=DEV)
+        ext.obs_reduce(part, nblk, O, s12)
+        assert torch.allclose(s12[0], s1, rtol=1e-5, atol=1e-3)
+        ext.obs_merge(s12, float(nblk * 8), float(dev_st.n), dev_st.shift().clone(), dev_st.mean, dev_st.mean_diff,
+                      dev_st.mean_f32, dev_st.inv_std_f32, 1e-2)
+        dev_st.n += nblk * 8
+    assert torch.allclose(dev_st.mean, ref.mean, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(dev_st.mean_diff, ref.mean_diff, rtol=1e-4)
+    assert torch.allclose(dev_st.inv_std_f32, ref.inv_std_f32, rtol=1e-4)
+
+
 def test_gae_kernel_matches_oracle():
     ext = _ext()
     T, E = 33, 1031
