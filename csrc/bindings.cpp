@@ -64,7 +64,7 @@ void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len
              torch::Tensor mean, torch::Tensor inv_std, torch::Tensor shift, torch::Tensor x_out,
              torch::Tensor actions, torch::Tensor logp, torch::Tensor rewards, torch::Tensor dones,
              torch::Tensor mom, torch::Tensor epstat, std::vector<int64_t> ints, std::vector<int64_t> keys,
-             double reward_clip, torch::Tensor qscale) {
+             double reward_clip, torch::Tensor qscale, torch::Tensor xT_out, int64_t xT_rows) {
   TORCH_CHECK(ints.size() == 11, "ints: kind,E,O,A,S,T,t_base,buf_E,t0,limit,std_var");
   TORCH_CHECK(keys.size() == 4, "keys: env,term,reset,action");
   TORCH_CHECK(rows == 16 || rows == 32, "rows must be 16 or 32");
@@ -116,6 +116,18 @@ void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len
   a.rewards = rewards.data_ptr<float>();
   a.dones = dones.data_ptr<float>();
   a.mom = mom.data_ptr<float>();
+  a.xT_out = nullptr;
+  a.ldT = 0;
+  if (xT_out.defined() && xT_out.numel() > 0) {
+    // FM transposed copy of the T*E training rows: the kernel writes 8-row groups per 16-env tile
+    const int64_t ld = (int64_t)a.buf_E * (a.t_base + a.T);
+    TORCH_CHECK(a.t_base == 0, "xT_out is written by a whole-rollout launch (t_base == 0)");
+    TORCH_CHECK(a.E % 16 == 0 && ld % 32 == 0, "xT_out needs E % 16 == 0 and T*E % 32 == 0");
+    TORCH_CHECK(xT_rows >= L.d_in[0] && xT_rows % 16 == 0, "xT_out rows must cover d_in and be a multiple of 16");
+    check(xT_out, "xT_out", storage_type(dt == 2 ? 1 : (int)dt), xT_rows * ld);
+    a.xT_out = xT_out.data_ptr();
+    a.ldT = (int)ld;
+  }
   a.epstat = epstat.data_ptr<float>();
   launch_rollout((int)dt, a, (int)rows, cur_stream());
 }
@@ -186,7 +198,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
                int64_t A, torch::Tensor actions, torch::Tensor logp_old, torch::Tensor adv, torch::Tensor ret,
                torch::Tensor v_old, torch::Tensor mu_prev, torch::Tensor v_prev, std::vector<int64_t> opts,
                std::vector<double> fopts, std::vector<torch::Tensor> tbufs, int64_t ldT, torch::Tensor part,
-               bool check_idx) {
+               bool check_idx, bool xT_ready) {
   TORCH_CHECK(dt != 2, "the update runs in bf16 when dtype=fp8 (fp8 gradients underflow e4m3)");
   Layout L = parse_layout(layout);
   TORCH_CHECK(A > 0, "A");
@@ -233,6 +245,9 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   void** dst[11] = {&a.xT, &a.h1pT, &a.h2pT, &a.h1vT, &a.h2vT, &a.g1pT, &a.g2pT, &a.g3pT, &a.g1vT, &a.g2vT, &a.g3vT};
   for (int i = 0; i < 11; ++i) *dst[i] = tbufs[i].data_ptr();
   a.ldT = (int)ldT;
+  // a precomputed xT is only valid for the identity row order covering the whole buffer
+  TORCH_CHECK(!xT_ready || (a.idx == nullptr && row0 == 0 && ldT == M), "xT_ready needs a full-batch call");
+  a.xT_ready = xT_ready ? 1 : 0;
   a.part = part.data_ptr<float>();
   launch_mlp_train((int)dt, a, cur_stream());
 }

@@ -37,6 +37,8 @@ struct RolloutArgs {
   float* logp;         // [T][E]
   float* rewards;      // [T][E] (clipped)
   float* dones;        // [T][E]
+  void* xT_out;        // optional FM [rows][ldT] transposed copy of x rows t*E+e (wgrad operand)
+  int ldT;             // its row length (== T*E of the whole buffer)
   float* mom;          // [nblk][2][O]  sum(x-shift), sum((x-shift)^2)
   float* epstat;       // [nblk][2]     finished-episode return sum, count
 };
@@ -78,6 +80,7 @@ struct MlpArgs {
   void* xT; void* h1pT; void* h2pT; void* h1vT; void* h2vT;
   void* g1pT; void* g2pT; void* g3pT; void* g1vT; void* g2vT; void* g3vT;
   int ldT;                // = M (row length of every transposed buffer)
+  int xT_ready;           // 1: xT already holds this call's rows (full-batch: the rollout wrote it)
   float* part;            // [nblk][NPART] per-workgroup partial sums (loss terms, dlog_std)
   int npart;
 };

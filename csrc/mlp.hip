@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(MlpArgs a) {
   T* h2pT = reinterpret_cast<T*>(a.h2pT);
   T* h1vT = reinterpret_cast<T*>(a.h1vT);
   T* h2vT = reinterpret_cast<T*>(a.h2vT);
-  write_transposed<DT, ROWS>(X, ldx, a.d_in[0], a.xT, a.ldT, m0, tid);
+  if (!a.xT_ready) write_transposed<DT, ROWS>(X, ldx, a.d_in[0], a.xT, a.ldT, m0, tid);  // else: rollout wrote it
   layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[0], W + a.off_w[0], a.n_out[0], H1p, ld1p, a.scale[0], wave, lane,
                                      h1pT, a.ldT, m0);
   layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1v, ld1v, a.scale[3], wave, lane,
@@ -309,9 +309,9 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(MlpArgs a) {
   layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(DV, ldv, a.d_out[5], W + a.off_wt[5], a.n_out[4], H2v, ld2v, a.scale[5],
                                               wave, lane, reinterpret_cast<T*>(a.g2vT), a.ldT, m0);
   __syncthreads();
-  layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(H2p, ld2p, a.d_out[1], W + a.off_wt[1], a.n_out[0], H1p, ld1p, a.scale[1],
+  layer_gemm<DT, ROWS, NW, EPI_DTANH_GLOBAL>(H2p, ld2p, a.d_out[1], W + a.off_wt[1], a.n_out[0], H1p, ld1p, a.scale[1],
                                               wave, lane, reinterpret_cast<T*>(a.g1pT), a.ldT, m0);
-  layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(H2v, ld2v, a.d_out[4], W + a.off_wt[4], a.n_out[3], H1v, ld1v, a.scale[4],
+  layer_gemm<DT, ROWS, NW, EPI_DTANH_GLOBAL>(H2v, ld2v, a.d_out[4], W + a.off_wt[4], a.n_out[3], H1v, ld1v, a.scale[4],
                                               wave, lane, reinterpret_cast<T*>(a.g1vT), a.ldT, m0);
 }
 

@@ -21,7 +21,9 @@
 #pragma once
 #include "common.h"
 
-enum { EPI_TANH = 0, EPI_LINEAR_F32 = 1, EPI_DTANH_INPLACE = 2, EPI_LINEAR_T = 3 };
+// EPI_DTANH_GLOBAL: like EPI_DTANH_INPLACE but the result is only needed as the wgrad
+// operand, so it goes to outT alone (no LDS write-back) — used for the last dgrad layers.
+enum { EPI_TANH = 0, EPI_LINEAR_F32 = 1, EPI_DTANH_INPLACE = 2, EPI_LINEAR_T = 3, EPI_DTANH_GLOBAL = 4 };
 
 // tanh for the MFMA epilogues: exp + reciprocal on the transcendental unit (v_exp_f32,
 // v_rcp_f32) instead of the libm polynomial; |err| ~1e-7.  The fp32 path keeps tanhf (it is
@@ -149,10 +151,13 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
               out[r * ldo + c] = v;
             } else if constexpr (EPI == EPI_LINEAR_T) {
               out[r * ldo + c] = P::cvt(v);
-            } else {  // EPI_DTANH_INPLACE: out holds h = tanh(pre); write dpre = v * (1 - h^2)
+            } else if constexpr (EPI == EPI_DTANH_INPLACE) {  // out holds h = tanh(pre); dpre = v*(1-h^2)
               const float h = P::tof(out[r * ldo + c]);
               v = v * (1.0f - h * h);
               out[r * ldo + c] = P::cvt(v);
+            } else {  // EPI_DTANH_GLOBAL
+              const float h = P::tof(out[r * ldo + c]);
+              v = v * (1.0f - h * h);
             }
             vals[i] = v;
           }

@@ -98,6 +98,8 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
       float m = 0.f, is = 1.f, sh = 0.f;
       if (d < O) { m = a.mean[d]; is = a.inv_std[d]; sh = a.shift[d]; }
       float ls1 = 0.f, ls2 = 0.f;
+      typename PX::T grp[ROWS];   // this feature's ROWS consecutive buffer rows (xT groups of 8)
+#pragma unroll
       for (int r = 0; r < ROWS; ++r) {
         float xv;
         if (d < O) {
@@ -108,9 +110,26 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
           xv = (d == O) ? 1.f : 0.f;
         }
         xs[r * ld1 + d] = P::cvt(xv);
-        if (r < nvalid) xo[((size_t)tb * a.buf_E + e0 + r) * a.d1 + d] = PX::cvt(xv);
+        grp[r] = PX::cvt(xv);
+        if (r < nvalid) xo[((size_t)tb * a.buf_E + e0 + r) * a.d1 + d] = grp[r];
       }
       if (d < O) { s1[d] += ls1; s2[d] += ls2; }
+      // full-batch update operand: rows m = tb*E + e0 + r are contiguous 8-groups of the FM
+      // layout (host guarantees E % 16 == 0), written once per rollout instead of per epoch
+      if (a.xT_out != nullptr && !last) {
+        typename PX::T* xT = reinterpret_cast<typename PX::T*>(a.xT_out);
+        const int mrow = tb * a.buf_E + e0;
+#pragma unroll
+        for (int g = 0; g < ROWS / 8; ++g) {
+          typename PX::T* o = xT + fm_index(d, mrow + 8 * g, a.ldT);
+          if constexpr (sizeof(typename PX::T) == 2) {
+            *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(&grp[8 * g]);
+          } else {
+            reinterpret_cast<uint4*>(o)[0] = reinterpret_cast<const uint4*>(&grp[8 * g])[0];
+            reinterpret_cast<uint4*>(o)[1] = reinterpret_cast<const uint4*>(&grp[8 * g])[1];
+          }
+        }
+      }
     }
     if (last) break;
     __syncthreads();

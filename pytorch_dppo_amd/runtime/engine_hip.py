@@ -148,6 +148,11 @@ class HipEngine:
         self._loss_dev: Optional[torch.Tensor] = None
         self.local_stats: Optional[RunningObsStats] = None
         self.loss_sums = torch.zeros(NPART_FIXED, **f32)
+        self.empty_x = torch.empty(0, dtype=self.sdtype, **dev)
+        # the rollout can emit the full-batch x^T operand when the update is one full-batch step
+        self.xT_from_rollout = (self.mb == self.N and self.ldT == self.N and E % 16 == 0 and self.N % 32 == 0
+                                and params.obs_norm_update == "rollout")
+        self._xT_valid = False   # True once a rollout wrote x^T for the current buffer contents
         self.s12 = torch.zeros(2, O, dtype=torch.float64, **dev)
         stats.device_merge = self._device_merge
         env.reset()
@@ -253,16 +258,18 @@ class HipEngine:
         self.env.load_state_dict(d)
 
     # ------------------------------------------------------------------------------------------
-    def _launch_rollout(self, T: int, t_base: int, t0: int, norm: RunningObsStats, shift: torch.Tensor):
+    def _launch_rollout(self, T: int, t_base: int, t0: int, norm: RunningObsStats, shift: torch.Tensor,
+                        xT: Optional[torch.Tensor] = None):
         e = self.env
         kp = e.kernel_params()
         ints = [kp["kind"], self.E, self.O, self.A, e.state_dim, T, t_base, self.E, t0 & 0xFFFFFFFF,
                 kp["limit"], 1 if self.p.std_convention == "var" else 0]
         keys = [kp["key_env"], kp["key_term"], kp["key_reset"], self.key_action]
+        xt = xT if xT is not None else self.empty_x
         self.ext.rollout(self.dt_fwd, ROLL_ROWS, e.state, e.ep_len, e.ep_ret, self.wimg_fwd, self.layout,
                          self.scales, self.model.flat.data, norm.mean_f32, norm.inv_std_f32, shift, self.x_buf,
                          self.actions, self.logp, self.rewards, self.dones, self.mom, self.epstat, ints, keys,
-                         float(self.p.reward_clip), self.qscale)
+                         float(self.p.reward_clip), self.qscale, xt, self.x_rows[0])
 
     @torch.no_grad()
     def rollout(self) -> Dict:
@@ -270,7 +277,11 @@ class HipEngine:
         self.refresh_fwd_image()   # fp8: weights changed during the previous update
         shift = self.stats.shift().clone()
         if p.obs_norm_update == "rollout":
-            self._launch_rollout(self.T, 0, self.env.t, self.stats, shift)
+            # full-batch update: the rollout also writes the fragment-major x^T wgrad operand once,
+            # so the 10 epochs' fused kernels skip re-transposing X (xT_ready)
+            self._launch_rollout(self.T, 0, self.env.t, self.stats, shift,
+                                 self.xT if self.xT_from_rollout else None)
+            self._xT_valid = self.xT_from_rollout
             self.env.t += self.T
             self.ext.obs_reduce(self.mom, self.mom.shape[0], self.O, self.s12)
             s1, s2 = self.s12[0], self.s12[1]
@@ -334,7 +345,7 @@ class HipEngine:
         self.ext.mlp_train(self.dt, self.x_buf, idx_t, row0, M, self.wimg, self.layout, self.scales,
                            self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
                            self.ret, self.values_buf, self.mu_prev, self.v_prev, opts, fopts, self.tbufs,
-                           self.ldT, self.part, False)
+                           self.ldT, self.part, False, bool(idx is None and self._xT_valid))
         self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, self.tasks,
                        self.tasks_host, self.slab)
         self.ext.grad_gather(self.slab, self.src_off, self.nchunks, self.chunk_stride, self.part,

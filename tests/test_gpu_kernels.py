@@ -215,6 +215,28 @@ def test_fused_loss_backward_matches_autograd(env_name, dtype, value_loss, conv,
     assert abs(ll["loss_value"] - out["loss_value"].item()) < max(5e-3, 50 * tol) * (1 + abs(out["loss_value"].item()))
 
 
+def test_rollout_written_xT_equals_kernel_written_xT():
+    """full-batch: the x^T operand the rollout emits == the one mlp_train would transpose."""
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 4,
+                    batch_size=64 * 4, dtype="bf16")
+    eng, model, env, stats = _engine(p)
+    stats.observes(env.observe())
+    assert eng.xT_from_rollout
+    eng.rollout()
+    eng.values()
+    eng.gae()
+    eng.begin_update()
+    assert eng._xT_valid
+    xT_roll = eng.xT.clone()
+    eng.grad(None)
+    g_roll = eng.grad_flat.clone()
+    eng._xT_valid = False            # force the fused kernel to write x^T itself
+    eng.xT.zero_()
+    eng.grad(None)
+    assert torch.equal(eng.xT, xT_roll)
+    assert torch.equal(eng.grad_flat, g_roll)
+
+
 def test_dppo_ref_loss_two_steps_matches_autograd():
     p = dppo_preset(device="gpu", env_name="HalfCheetah-v2", num_envs=32, exploration_size=256,
                     batch_size=256, dtype="fp32", loss="dppo_ref", ent_coeff=0.01)
