@@ -13,6 +13,11 @@ namespace {
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// diagnostics only: phase-ablation mask for mlp_train (scripts/ablate_train.py); always 0 in
+// training runs (the results of an ablated call are not a gradient)
+int g_train_ablate = 0;
+void set_train_ablation(int64_t mask) { g_train_ablate = (int)mask; }
+
 at::ScalarType storage_type(int dt) {
   return dt == 0 ? at::kFloat : (dt == 1 ? at::kBFloat16 : at::kByte);
 }
@@ -248,6 +253,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   // a precomputed xT is only valid for the identity row order covering the whole buffer
   TORCH_CHECK(!xT_ready || (a.idx == nullptr && row0 == 0 && ldT == M), "xT_ready needs a full-batch call");
   a.xT_ready = xT_ready ? 1 : 0;
+  a.ablate = g_train_ablate;
   a.part = part.data_ptr<float>();
   launch_mlp_train((int)dt, a, cur_stream());
 }
@@ -384,6 +390,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad", &wgrad);
   m.def("grad_gather", &grad_gather);
   m.def("gae", &gae);
+  m.def("set_train_ablation", &set_train_ablation);
   m.def("obs_reduce", &obs_reduce);
   m.def("obs_merge", &obs_merge);
   m.def("adam", &adam);

@@ -81,6 +81,8 @@ struct MlpArgs {
   void* g1pT; void* g2pT; void* g3pT; void* g1vT; void* g2vT; void* g3vT;
   int ldT;                // = M (row length of every transposed buffer)
   int xT_ready;           // 1: xT already holds this call's rows (full-batch: the rollout wrote it)
+  int ablate;             // DIAGNOSTIC ONLY (scripts/ablate_train.py; 0 in every real run): bit0 no
+                          // transposed stores, bit1 skip v_fc1, bit2 skip dgrad chain, bit3 skip loss
   float* part;            // [nblk][NPART] per-workgroup partial sums (loss terms, dlog_std)
   int npart;
 };

@@ -178,15 +178,17 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(MlpArgs a) {
   // ---------------- forward ----------------
   // Activations go to the feature-major wgrad operands straight from the MFMA accumulators
   // (rows < n_real; the constant-1 bias row of each buffer is preset once by the host).
-  T* h1pT = reinterpret_cast<T*>(a.h1pT);
-  T* h2pT = reinterpret_cast<T*>(a.h2pT);
-  T* h1vT = reinterpret_cast<T*>(a.h1vT);
-  T* h2vT = reinterpret_cast<T*>(a.h2vT);
-  if (!a.xT_ready) write_transposed<DT, ROWS>(X, ldx, a.d_in[0], a.xT, a.ldT, m0, tid);  // else: rollout wrote it
+  const bool no_T = (a.ablate & 1) != 0;   // diagnostics only (see MlpArgs::ablate)
+  T* h1pT = no_T ? nullptr : reinterpret_cast<T*>(a.h1pT);
+  T* h2pT = no_T ? nullptr : reinterpret_cast<T*>(a.h2pT);
+  T* h1vT = no_T ? nullptr : reinterpret_cast<T*>(a.h1vT);
+  T* h2vT = no_T ? nullptr : reinterpret_cast<T*>(a.h2vT);
+  if (!a.xT_ready && !no_T) write_transposed<DT, ROWS>(X, ldx, a.d_in[0], a.xT, a.ldT, m0, tid);  // else: rollout wrote it
   layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[0], W + a.off_w[0], a.n_out[0], H1p, ld1p, a.scale[0], wave, lane,
                                      h1pT, a.ldT, m0);
-  layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1v, ld1v, a.scale[3], wave, lane,
-                                     h1vT, a.ldT, m0);
+  if (!(a.ablate & 2))
+    layer_gemm<DT, ROWS, NW, EPI_TANH>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1v, ld1v, a.scale[3], wave,
+                                       lane, h1vT, a.ldT, m0);
   __syncthreads();
   // X is dead: preset the tiles that alias its region
   preset_tile<DT>(H2p, ld2p, ROWS, a.n_out[1], tid, 256);
@@ -203,7 +205,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(MlpArgs a) {
   layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32>(H2v, ld2v, a.d_in[5], W + a.off_w[5], 1, V, 1, a.scale[5], wave, lane);
   __syncthreads();
   // ---------------- loss + dL/d(mu, log_std, v) per row ----------------
-  if (tid < ROWS) {
+  if (tid < ROWS && !(a.ablate & 8)) {
     const int r = tid;
     float* lrow = LOSS + r * NPART_FIXED;
 #pragma unroll
@@ -304,11 +306,16 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(MlpArgs a) {
   write_transposed<DT, ROWS>(DMU, ldmu, A, a.g3pT, a.ldT, m0, tid);
   write_transposed<DT, ROWS>(DV, ldv, 1, a.g3vT, a.ldT, m0, tid);
   // ---------------- dgrad chain (dY^T of every layer stored from the accumulators) --------
+  if (a.ablate & 4) return;   // diagnostics only
+  T* g2pT = no_T ? nullptr : reinterpret_cast<T*>(a.g2pT);
+  T* g2vT = no_T ? nullptr : reinterpret_cast<T*>(a.g2vT);
   layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(DMU, ldmu, a.d_out[2], W + a.off_wt[2], a.n_out[1], H2p, ld2p, a.scale[2],
-                                              wave, lane, reinterpret_cast<T*>(a.g2pT), a.ldT, m0);
+                                              wave, lane, g2pT, a.ldT, m0);
   layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE>(DV, ldv, a.d_out[5], W + a.off_wt[5], a.n_out[4], H2v, ld2v, a.scale[5],
-                                              wave, lane, reinterpret_cast<T*>(a.g2vT), a.ldT, m0);
+                                              wave, lane, g2vT, a.ldT, m0);
   __syncthreads();
+  // EPI_DTANH_GLOBAL's only output is the wgrad operand, so it always stores (ablation bit0
+  // does not apply here or the MFMAs would be dead code)
   layer_gemm<DT, ROWS, NW, EPI_DTANH_GLOBAL>(H2p, ld2p, a.d_out[1], W + a.off_wt[1], a.n_out[0], H1p, ld1p, a.scale[1],
                                               wave, lane, reinterpret_cast<T*>(a.g1pT), a.ldT, m0);
   layer_gemm<DT, ROWS, NW, EPI_DTANH_GLOBAL>(H2v, ld2v, a.d_out[4], W + a.off_wt[4], a.n_out[3], H1v, ld1v, a.scale[4],
