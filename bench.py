@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--batch-size", type=int, default=0, help="0 = full buffer (reference DPPO)")
     ap.add_argument("--overlap-rollout", action="store_true",
                     help="overlap the final gradient all-reduce with the next rollout (1-update lag)")
+    ap.add_argument("--graphs", action="store_true",
+                    help="replay the per-minibatch launch chains as hipGraphs (use_graphs)")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -65,7 +67,8 @@ def main():
     rows = E * T
     p = dppo_preset(device="gpu", env_name=args.env_name, num_envs=E, exploration_size=rows,
                     batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=args.dtype,
-                    num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout)
+                    num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
+                    use_graphs=args.graphs)
     w = DPPOWorker(p, ctx)
     for i in range(args.warmup):
         m = w.iteration_step()
@@ -96,7 +99,7 @@ def main():
                           "global_batch": rows * ctx.world_size, "seq_len": T,
                           "parallelism": f"dp{ctx.world_size}", "env": args.env_name, "num_envs_per_gpu": E,
                           "rollout_len": T, "num_epoch": args.num_epoch,
-                          "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout,
+                          "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout, "graphs": args.graphs,
                           "last_iter": {k: m[k] for k in ("loss", "mean_ep_return", "ms_rollout", "ms_values_gae",
                                                           "ms_update", "ms_obs_stats") if k in m}}}
         print(json.dumps(out), flush=True)

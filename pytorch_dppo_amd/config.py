@@ -67,11 +67,18 @@ class Params:
     log_jsonl: str = ""
     log_every: int = 1
     overlap_rollout: bool = False        # SURVEY §5.8 option (b)
-    use_graphs: bool = True              # capture the update into a hipGraph on GPU
+    use_graphs: bool = False             # replay the per-minibatch launch chains as hipGraphs (GPU engine)
     dist_timeout_s: float = 300.0
     verify_sync_every: int = 0           # debug param-checksum all-reduce period
     adam_betas: tuple = (0.9, 0.999)
     adam_eps: float = 1e-8
+    # ---- observability / failure detection ----------------------
+    log_csv: str = ""                    # learning-curve CSV (rank 0), the figs/*.png analogue
+    profile_dir: str = ""                # torch.profiler chrome traces (host + HIP timeline) per rank
+    profile_iters: str = "2:4"           # [start:stop) iterations captured when profile_dir is set
+    heartbeat_s: float = 0.0             # >0: per-rank heartbeat in the rendezvous store every N s
+    heartbeat_timeout_s: float = 120.0   # a peer silent this long is reported dead and this rank exits
+    check_finite: bool = False           # debug: stop with the failing phase when loss/params go non-finite
 
     # ------------------------------------------------------------------------------------
     def __post_init__(self):

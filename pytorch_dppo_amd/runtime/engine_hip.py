@@ -154,6 +154,11 @@ class HipEngine:
                                 and params.obs_norm_update == "rollout")
         self._xT_valid = False   # True once a rollout wrote x^T for the current buffer contents
         self.s12 = torch.zeros(2, O, dtype=torch.float64, **dev)
+        # hipGraph replay of the per-minibatch launch chains (see _launch)
+        self.use_graphs = bool(params.use_graphs)
+        self._graphs: Dict = {}
+        self._graph_warm: set = set()
+        self._capture_stream = torch.cuda.Stream(device=device) if self.use_graphs else None
         stats.device_merge = self._device_merge
         env.reset()
         self.params_changed()
@@ -339,22 +344,51 @@ class HipEngine:
                 raise IndexError(f"minibatch indices out of range [0, {self.N}): {lo}..{hi}")
             self.idx_dev[:M].copy_(idx.to(torch.int32), non_blocking=True)
             idx_t, row0 = self.idx_dev, 0
+        first, xt_ready = bool(self._first_step), bool(idx is None and self._xT_valid)
+        self._launch(("grad", idx is None, first, xt_ready), lambda: self._launch_grad(idx_t, row0, first, xt_ready))
+        self._first_step = False
+        self._loss_dev = self.loss_sums
+        return None
+
+    def _launch_grad(self, idx_t: torch.Tensor, row0: int, first: bool, xt_ready: bool) -> None:
+        p, M = self.p, self.mb
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
-                1 if p.std_convention == "var" else 0, 1 if self._first_step else 0, self.npart]
+                1 if p.std_convention == "var" else 0, 1 if first else 0, self.npart]
         fopts = [float(p.clip), float(p.ent_coeff)]
         self.ext.mlp_train(self.dt, self.x_buf, idx_t, row0, M, self.wimg, self.layout, self.scales,
                            self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
                            self.ret, self.values_buf, self.mu_prev, self.v_prev, opts, fopts, self.tbufs,
-                           self.ldT, self.part, False, bool(idx is None and self._xT_valid))
+                           self.ldT, self.part, False, xt_ready)
         self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, self.tasks,
                        self.tasks_host, self.slab)
         self.ext.grad_gather(self.slab, self.src_off, self.nchunks, self.chunk_stride, self.part,
                              self.ntrain_blk, self.npart, self.A, 1.0 / M, self.grad_flat, self.loss_sums)
         if p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])  # train.py:164
-        self._first_step = False
-        self._loss_dev = self.loss_sums
-        return None
+
+    def _launch(self, key, fn) -> None:
+        """Run a fixed launch chain directly, or as a captured hipGraph (``use_graphs``).
+
+        Every kernel in a chain reads its per-step state from device memory (Adam step counter, weight
+        images, minibatch index buffer), and every buffer it touches is allocated once in ``__init__`` and
+        only ever updated in place, so one capture per (chain, static-flag) key replays correctly for the
+        whole run. The first call of a key runs eagerly (warm-up: code objects loaded, LDS attributes
+        set), the second captures and replays.
+        """
+        if not self.use_graphs:
+            fn()
+            return
+        g = self._graphs.get(key)
+        if g is None:
+            if key not in self._graph_warm:
+                self._graph_warm.add(key)
+                fn()
+                return
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self._capture_stream):
+                fn()
+            self._graphs[key] = g
+        g.replay()
 
     @torch.no_grad()
     def apply(self, extra_grad: float = 0.0) -> None:
@@ -363,9 +397,10 @@ class HipEngine:
             self.grad_flat.add_(extra_grad)
         mx = float(p.max_grad_norm) if (p.max_grad_norm is not None and p.max_grad_norm > 0) else 0.0
         b1, b2 = p.adam_betas
-        self.ext.adam(self.model.flat.data, self.grad_flat, self.adam_m, self.adam_v, float(p.lr), float(b1),
-                      float(b2), float(p.adam_eps), mx, self.adam_state, self.norm_part, self.wimg, self.w_map,
-                      self.wt_map, self.dt, self.no_q)
+        self._launch(("adam",), lambda: self.ext.adam(
+            self.model.flat.data, self.grad_flat, self.adam_m, self.adam_v, float(p.lr), float(b1), float(b2),
+            float(p.adam_eps), mx, self.adam_state, self.norm_part, self.wimg, self.w_map, self.wt_map, self.dt,
+            self.no_q))
         self.adam_step += 1
         return None
 

@@ -21,6 +21,7 @@ import torch
 from ..config import Params
 from ..parallel.dist import DistContext, init_distributed
 from ..utils import checkpoint as ckpt
+from ..utils.heartbeat import start_heartbeat
 from ..utils.metrics import MetricsLogger
 
 
@@ -36,7 +37,7 @@ def run_worker(params: Params, ctx: DistContext, max_iters: Optional[int] = None
                evaluator: bool = True, quiet: bool = False):
     from .worker import DPPOWorker
     log = MetricsLogger(params.log_jsonl if ctx.is_main else "", enabled=ctx.is_main,
-                        stdout=ctx.is_main and not quiet)
+                        stdout=ctx.is_main and not quiet, csv_path=params.log_csv if ctx.is_main else "")
     w = DPPOWorker(params, ctx, log)
     if params.resume:
         sd = ckpt.load_model_state(params.resume)
@@ -55,10 +56,14 @@ def run_worker(params: Params, ctx: DistContext, max_iters: Optional[int] = None
         from .evaluator import EvaluatorHandle
         ev = EvaluatorHandle(params)
     history = []
+    hb = start_heartbeat(ctx, params.heartbeat_s, params.heartbeat_timeout_s)
+    prof = _Profiler(params, ctx)
     try:
         n = 0
         while not w.should_stop():
+            prof.before(n)
             m = w.iteration_step()
+            prof.after(n)
             history.append(m)
             n += 1
             if ctx.is_main and params.log_every and w.iteration % params.log_every == 0:
@@ -73,10 +78,49 @@ def run_worker(params: Params, ctx: DistContext, max_iters: Optional[int] = None
         if params.checkpoint_dir:
             save(w, ctx, params.checkpoint_dir)
     finally:
+        prof.close()
+        if hb is not None:
+            hb.stop()
         if ev is not None:
             ev.close()
         log.close()
     return w, history
+
+
+class _Profiler:
+    """``--profile-dir``: a torch.profiler window over iterations [a, b) (host ops + HIP kernels
+    + the PhaseTimer ranges), exported as one chrome trace per rank."""
+
+    def __init__(self, params: Params, ctx: DistContext):
+        self.dir = params.profile_dir
+        self.rank = ctx.rank
+        self.gpu = ctx.device.type == "cuda"
+        a, _, b = (params.profile_iters or "0:1").partition(":")
+        self.a = int(a or 0)
+        self.b = int(b) if b else self.a + 1
+        self.p = None
+
+    def before(self, n: int) -> None:
+        if self.dir and self.p is None and n == self.a:
+            from torch.profiler import ProfilerActivity, profile
+            acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if self.gpu else [])
+            self.p = profile(activities=acts, record_shapes=False)
+            self.p.__enter__()
+
+    def after(self, n: int) -> None:
+        if self.p is not None and n + 1 >= self.b:
+            self.close()
+
+    def close(self) -> None:
+        if self.p is None:
+            return
+        if self.gpu:
+            torch.cuda.synchronize()
+        self.p.__exit__(None, None, None)
+        os.makedirs(self.dir, exist_ok=True)
+        self.p.export_chrome_trace(os.path.join(self.dir, f"trace_rank{self.rank}.json"))
+        self.p = None
+        self.dir = ""
 
 
 def save(w, ctx: DistContext, path: str) -> None:

@@ -59,7 +59,7 @@ class DPPOWorker:
         self.env_steps = 0            # global (all ranks)
         self.updates = 0
         self.log = log
-        self.timer = PhaseTimer(self.device)
+        self.timer = PhaseTimer(self.device, annotate=bool(params.profile_dir))
         self._stats_initialised = False
         self.last_metrics: Dict = {}
         self._perm_gen = torch.Generator(device="cpu")
@@ -159,8 +159,22 @@ class DPPOWorker:
              "grad_norm": gnorm, **{k: v for k, v in losses.items()}, **tm.summary()}
         if p.verify_sync_every and self.iteration % p.verify_sync_every == 0:
             m["replicas_in_sync"] = self.ctx.verify_replicas(self.model.flat.data)
+        if p.check_finite:
+            self._check_finite(m)
         self.last_metrics = m
         return m
+
+    def _check_finite(self, m: Dict) -> None:
+        """debug mode: stop at the first iteration whose loss terms, gradient norm or
+        parameters are not finite, naming what broke (the phase timings are in ``m``)."""
+        bad = [k for k in ("loss", "loss_clip", "loss_value", "loss_ent", "grad_norm")
+               if k in m and not math.isfinite(m[k])]
+        if not bool(torch.isfinite(self.model.flat.data).all()):
+            bad.append("parameters")
+        if bool(torch.isfinite(self.stats.mean_f32).all()) is False:
+            bad.append("obs_stats.mean")
+        if bad:
+            raise FloatingPointError(f"rank {self.ctx.rank} iteration {self.iteration}: non-finite {bad}")
 
     def flush_pending(self) -> None:
         """complete a deferred (overlapped) all-reduce + Adam step, if any."""

@@ -16,12 +16,23 @@ import torch
 
 
 class PhaseTimer:
-    def __init__(self, device: torch.device):
+    """Per-phase wall time: HIP events on GPU (read once per iteration), perf_counter on CPU.
+
+    With ``annotate`` each phase is also a ``torch.profiler`` range, so the chrome traces of
+    ``--profile-dir`` show rollout / obs_stats / values_gae / update around the HIP kernels."""
+
+    def __init__(self, device: torch.device, annotate: bool = False):
         self.gpu = device.type == "cuda"
+        self.annotate = annotate
         self._open: Dict[str, object] = {}
+        self._ranges: Dict[str, object] = {}
         self._done: Dict[str, list] = {}
 
     def start(self, name: str) -> None:
+        if self.annotate:
+            r = torch.autograd.profiler.record_function(name)
+            r.__enter__()
+            self._ranges[name] = r
         if self.gpu:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
@@ -30,6 +41,9 @@ class PhaseTimer:
             self._open[name] = time.perf_counter()
 
     def stop(self, name: str) -> None:
+        r = self._ranges.pop(name, None)
+        if r is not None:
+            r.__exit__(None, None, None)
         s = self._open.pop(name)
         if self.gpu:
             e = torch.cuda.Event(enable_timing=True)
@@ -50,14 +64,27 @@ class PhaseTimer:
         return out
 
 
+CSV_COLUMNS = ("iteration", "env_steps", "updates", "steps_per_s", "mean_ep_return", "ep_count", "loss",
+               "loss_clip", "loss_value", "loss_ent", "approx_kl", "clipfrac", "grad_norm")
+
+
 class MetricsLogger:
-    def __init__(self, path: str = "", enabled: bool = True, stdout: bool = True):
+    """Rank-0 JSONL (every field) + optional learning-curve CSV (fixed columns) + stdout line."""
+
+    def __init__(self, path: str = "", enabled: bool = True, stdout: bool = True, csv_path: str = ""):
         self.enabled = enabled
         self.stdout = stdout
         self.f = None
+        self.csv = None
         if enabled and path:
             os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
             self.f = open(path, "a")
+        if enabled and csv_path:
+            os.makedirs(os.path.dirname(os.path.abspath(csv_path)), exist_ok=True)
+            fresh = not os.path.exists(csv_path) or os.path.getsize(csv_path) == 0
+            self.csv = open(csv_path, "a")
+            if fresh:
+                self.csv.write(",".join(CSV_COLUMNS) + "\n")
 
     def log(self, rec: Dict) -> None:
         if not self.enabled:
@@ -67,6 +94,9 @@ class MetricsLogger:
         if self.f:
             self.f.write(json.dumps(rec) + "\n")
             self.f.flush()
+        if self.csv:
+            self.csv.write(",".join("" if rec.get(c) is None else repr(rec[c]) for c in CSV_COLUMNS) + "\n")
+            self.csv.flush()
         if self.stdout:
             it = int(rec.get("iteration", 0))
             print(f"iter {it} env_steps {int(rec.get('env_steps', 0))} "
@@ -75,6 +105,8 @@ class MetricsLogger:
                   f"loss {rec.get('loss', float('nan')):.4f}", flush=True)
 
     def close(self) -> None:
-        if self.f:
-            self.f.close()
-            self.f = None
+        for name in ("f", "csv"):
+            fh = getattr(self, name)
+            if fh:
+                fh.close()
+                setattr(self, name, None)

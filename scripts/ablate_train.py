@@ -32,6 +32,7 @@ def main():
     model = ActorCritic(spec.obs_dim, spec.act_dim).to(dev)
     env = make_vec_env(spec, p.num_envs, device=dev)
     stats = RunningObsStats(spec.obs_dim, dev)
+    p.use_graphs = False   # the ablation mask is read at launch time
     eng = HipEngine(p, model, env, stats, dev, 0)
     stats.observes(env.observe())
     eng.rollout()

@@ -135,11 +135,39 @@ def test_dead_rank_makes_survivor_fail_fast_instead_of_deadlock(tmp_path):
     assert time.time() - t0 < 110
 
 
+def _worker_hang(rank, world, port, out_dir):
+    """rank 1 hangs OUTSIDE any collective (stuck host code); rank 0 is busy in a long
+    non-collective phase: only the heartbeat can notice (collective timeout is 600 s here)."""
+    from pytorch_dppo_amd.utils.heartbeat import start_heartbeat
+    ctx = _init(rank, world, port, timeout=600.0)
+    hb = start_heartbeat(ctx, 0.2, 1.5)   # default action: report + os._exit(75)
+    if rank == 1:
+        hb._stop.set()                     # the beacon thread dies with the "hung" process
+        time.sleep(60)
+        os._exit(0)
+    time.sleep(60)
+    os._exit(0)
+
+
+def test_heartbeat_detects_a_hung_rank_outside_collectives(tmp_path):
+    t0 = time.time()
+    procs = _spawn(_worker_hang, 2, str(tmp_path))
+    procs[0].join(30)
+    code0 = procs[0].exitcode
+    for p in procs:
+        if p.is_alive():
+            p.terminate()
+            p.join(5)
+    assert code0 == 75, code0
+    assert time.time() - t0 < 30
+
+
 def test_launcher_two_workers_checkpoint_and_resume(tmp_path):
     from pytorch_dppo_amd.runtime.launcher import launch
     ck = str(tmp_path / "ck")
     p = dppo_preset(env_name="Pendulum-v0", num_processes=2, num_envs=4, exploration_size=64, batch_size=64,
-                    num_epoch=2, hidden=(16, 16), max_iters=2, checkpoint_dir=ck, log_jsonl=str(tmp_path / "log.jsonl"))
+                    num_epoch=2, hidden=(16, 16), max_iters=2, checkpoint_dir=ck, log_jsonl=str(tmp_path / "log.jsonl"),
+                    heartbeat_s=0.5)
     launch(p)
     assert os.path.exists(os.path.join(ck, "model.pt"))
     assert os.path.exists(os.path.join(ck, "env_rank1.pt"))
