@@ -278,7 +278,9 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
     const int* t = tp + 6 * i;
     TORCH_CHECK(t[0] >= 0 && t[0] < 6, "task layer");
     TORCH_CHECK(t[1] + WGRAD_TILE <= g_rows[t[0]] && t[2] + WGRAD_TILE <= x_rows[t[0]], "task tile beyond operand rows");
-    TORCH_CHECK(t[3] >= 0 && t[4] <= ld && (t[4] - t[3]) % 32 == 0 && t[3] % 32 == 0, "task batch range");
+    // the kernel consumes 32-row k-steps in pairs: every range is a positive multiple of 64 rows
+    TORCH_CHECK(t[3] >= 0 && t[4] <= ld && t[4] > t[3] && (t[4] - t[3]) % 64 == 0 && t[3] % 32 == 0,
+                "task batch range (must be a positive multiple of 64 rows)");
     slab_need = std::max<int64_t>(slab_need, (int64_t)t[5] + WGRAD_TILE * WGRAD_TILE);
   }
   check(slab, "slab", at::kFloat, slab_need);
@@ -332,8 +334,9 @@ void obs_merge(torch::Tensor s12, double count, double n_a, torch::Tensor shift,
 }
 
 void gae(torch::Tensor rewards, torch::Tensor values, torch::Tensor dones, torch::Tensor adv, torch::Tensor ret,
-         double gamma, double lam) {
+         double gamma, double lam, int64_t mode) {
   TORCH_CHECK(rewards.dim() == 2, "rewards [T,E]");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "gae mode: 0 auto, 1 per-env lanes, 2 parallel-in-time scan");
   const int64_t T = rewards.size(0), E = rewards.size(1);
   check(rewards, "rewards", at::kFloat, T * E);
   check(values, "values", at::kFloat, (T + 1) * E);
@@ -341,7 +344,7 @@ void gae(torch::Tensor rewards, torch::Tensor values, torch::Tensor dones, torch
   check(adv, "adv", at::kFloat, T * E);
   check(ret, "ret", at::kFloat, T * E);
   launch_gae(rewards.data_ptr<float>(), values.data_ptr<float>(), dones.data_ptr<float>(), adv.data_ptr<float>(),
-             ret.data_ptr<float>(), (int)T, (int)E, (float)gamma, (float)lam, cur_stream());
+             ret.data_ptr<float>(), (int)T, (int)E, (float)gamma, (float)lam, (int)mode, cur_stream());
 }
 
 void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, double lr, double b1, double b2,

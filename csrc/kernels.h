@@ -113,7 +113,7 @@ void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int 
                         const float* part, int nblk, int npart, int A, float scale, float* grad,
                         int n, float* loss_out, hipStream_t s);
 void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
-                int T, int E, float gamma, float lam, hipStream_t s);
+                int T, int E, float gamma, float lam, int mode, hipStream_t s);
 void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, float b1, float b2,
                  float eps, float max_norm, float* state, float* norm_part, int nblk,
                  void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale,

@@ -66,73 +66,68 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
   constexpr int RB = ROWS / 16;
   constexpr int KC = KChunk<DT>::KC;
   constexpr int NT2 = 2;
+  // every quantity that steers control flow is wave-uniform and must live in SGPRs: with a
+  // VGPR `wave` the compiler turns the step loop into EXEC-masked regions and waits for ALL
+  // outstanding loads (vmcnt(0)) at each merge — the prefetch below would never overlap
+  wave = __builtin_amdgcn_readfirstlane(wave);
   const int ksteps = kdim >> 5;
   const int nchunks = (ksteps + KC - 1) / KC;
   const int ntiles = (n_real + 15) >> 4;
   const int lr = lane & 15;
-  const int lk = (lane >> 4) * 8;
-  const T* ap = A + lr * lda + lk;
-  // This wave's work is a flat stream of (tile pair, k-chunk) steps; the B fragments of step
-  // s+1 — including the FIRST chunk of the wave's next tile pair — are loaded while step s
-  // computes, so only the layer's very first chunk pays the L2 round trip.
+  const T* ap = A + lr * lda + (lane >> 4) * 8;
+  // This wave's work is a flat stream of (tile pair, k-chunk) steps; the A (LDS) and B (L2)
+  // fragments of step s+1 — including the FIRST chunk of the wave's next tile pair — are
+  // loaded while step s computes.  Two register sets alternate (s even: set 0 computes, set 1
+  // loads), so no fragment is ever copied between registers.
   const int first_pair = wave * NT2;
   if (first_pair >= ntiles) return;
   const int npairs = (ntiles - first_pair + NW * NT2 - 1) / (NW * NT2);
   const int nsteps = npairs * nchunks;
-  auto bptr = [&](int nt0, bool two, int kc, int j, const T*& p0, const T*& p1) {
-    const int ks = min(kc * KC + j, ksteps - 1);   // past-the-end steps re-load the last one
-    p0 = B + fm_frag(nt0, ks, kdim, lane);
-    p1 = two ? p0 + (size_t)ksteps * 512 : p0;    // absent 2nd tile: alias (results discarded)
-  };
-  Frag bc0[KC], bc1[KC], bn0[KC], bn1[KC];
-  {
-    const bool two = (first_pair + 1) < ntiles;
+  struct Buf { Frag b0[KC], b1[KC], a[KC][RB]; };
+  // The partner tile nt+1 of an (even) nt always exists in memory: every image's row count is
+  // a multiple of 32 (PackedLayout pads d_out / d_in to P32), so past n_real it is zero padding
+  // and its MFMA results are simply not stored.  Loading it unconditionally keeps the loads
+  // branch-free (a select between "reload" and "reuse" made the compiler wait vmcnt(0)).
+  auto load = [&](Buf& d, int nt, int kc_) {
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
-      const T *p0, *p1;
-      bptr(first_pair, two, 0, j, p0, p1);
-      bc0[j] = P::load(p0);
-      bc1[j] = P::load(p1);
+      const int ks = min(kc_ * KC + j, ksteps - 1);   // past-the-end steps re-load the last one
+      const T* p0 = B + fm_frag(nt, ks, kdim, lane);
+      d.b0[j] = P::load(p0);
+      d.b1[j] = P::load(p0 + (size_t)ksteps * 512);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) d.a[j][rb] = P::load(ap + rb * 16 * lda + ks * 32);
     }
-  }
+  };
   f32x4 acc[NT2][RB];
 #pragma unroll
   for (int t = 0; t < NT2; ++t)
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) acc[t][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int nt0 = first_pair, kc = 0;
-  for (int s = 0; s < nsteps; ++s) {
-    const bool two = (nt0 + 1) < ntiles;
-    // ---- prefetch step s+1 ----
-    if (s + 1 < nsteps) {
-      int nt1 = nt0, kc1 = kc + 1;
-      if (kc1 == nchunks) { kc1 = 0; nt1 = nt0 + NW * NT2; }
-      const bool two1 = (nt1 + 1) < ntiles;
+  auto compute = [&](const Buf& c, int kc_) {
+    if ((kc_ + 1) * KC <= ksteps) {   // full chunk: straight-line, no per-step branch
 #pragma unroll
-      for (int j = 0; j < KC; ++j) {
-        const T *p0, *p1;
-        bptr(nt1, two1, kc1, j, p0, p1);
-        bn0[j] = P::load(p0);
-        bn1[j] = P::load(p1);
-      }
-    }
-    // ---- compute chunk kc of pair nt0 ----
-#pragma unroll
-    for (int j = 0; j < KC; ++j) {
-      const int ks = kc * KC + j;
-      if (ks < ksteps) {
+      for (int j = 0; j < KC; ++j)
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
-          Frag a = P::load(ap + rb * 16 * lda + ks * 32);
-          acc[0][rb] = P::mma(acc[0][rb], a, bc0[j]);
-          acc[1][rb] = P::mma(acc[1][rb], a, bc1[j]);
+          acc[0][rb] = P::mma(acc[0][rb], c.a[j][rb], c.b0[j]);
+          acc[1][rb] = P::mma(acc[1][rb], c.a[j][rb], c.b1[j]);
+        }
+    } else {                           // ragged last chunk (kdim not a multiple of 32*KC)
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        if (kc_ * KC + j < ksteps) {
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb) {
+            acc[0][rb] = P::mma(acc[0][rb], c.a[j][rb], c.b0[j]);
+            acc[1][rb] = P::mma(acc[1][rb], c.a[j][rb], c.b1[j]);
+          }
         }
       }
     }
-#pragma unroll
-    for (int j = 0; j < KC; ++j) { bc0[j] = bn0[j]; bc1[j] = bn1[j]; }
-    if (++kc < nchunks) continue;
-    // ---- pair complete: epilogue, then advance to the wave's next pair ----
+  };
+  auto epilogue = [&](int nt0) {
+    const bool two = (nt0 + 1) < ntiles;
 #pragma unroll
     for (int t = 0; t < NT2; ++t) {
       const int c = (nt0 + t) * 16 + lr;
@@ -143,7 +138,8 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int r = rb * 16 + (lane >> 4) * 4 + i;
-            float v = acc[t][rb][i] * scale;
+            float v = acc[t][rb][i];
+            if constexpr (DT == DT_FP8) v *= scale;   // e4m3 weight scale; 1 for bf16 / fp32
             if constexpr (EPI == EPI_TANH) {
               v = act_tanh<DT>(v);
               out[r * ldo + c] = P::cvt(v);
@@ -172,9 +168,31 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
     for (int t = 0; t < NT2; ++t)
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) acc[t][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    kc = 0;
-    nt0 += NW * NT2;
+  };
+  Buf buf0, buf1;
+  int nt0 = first_pair, kc = 0;
+  load(buf0, nt0, 0);
+  // One step: prefetch step s+1 into `nx` (unconditionally: past the end it re-loads valid
+  // addresses, so the number of loads in flight is the same on every path and the compiler's
+  // waitcnt is exact), compute step s from `cur`, epilogue at the end of a pair.
+  auto step = [&](int s, const Buf& cur, Buf& nx) {
+    int nt1 = nt0, kc1 = kc + 1;
+    if (kc1 == nchunks) { kc1 = 0; nt1 = nt0 + NW * NT2; }
+    if (s + 1 >= nsteps) { nt1 = nt0; kc1 = kc; }
+    load(nx, nt1, kc1);
+    compute(cur, kc);
+    if (++kc == nchunks) {
+      epilogue(nt0);
+      kc = 0;
+      nt0 += NW * NT2;
+    }
+  };
+  int s = 0;
+  for (; s + 1 < nsteps; s += 2) {
+    step(s, buf0, buf1);
+    step(s + 1, buf1, buf0);
   }
+  if (s < nsteps) step(s, buf0, buf1);
 }
 
 __host__ __device__ inline size_t al16(size_t b) { return (b + 15) & ~size_t(15); }

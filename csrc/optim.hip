@@ -26,6 +26,62 @@ __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rew,
   }
 }
 
+// Parallel-in-time GAE for few envs and long rollouts (T >> E, e.g. ppo.py: 1 env x 2048 steps),
+// SURVEY K9.  The recurrence A_t = delta_t + c_t * A_{t+1}, c_t = gamma*lam*(1-d_t), is a chain
+// of affine maps x -> delta_t + c_t x; composition is associative:
+//   (D1, C1) o (D2, C2) = (D1 + C1*D2, C1*C2).
+// One workgroup per env: thread j composes the maps of its contiguous chunk of steps, a reverse
+// exclusive scan over the 256 chunk maps (in LDS, Hillis-Steele) gives each chunk its incoming
+// A_{t1}, and every thread replays its chunk to write adv / ret.  Same arithmetic per step as
+// gae_kernel; only the association of the products differs (fp32 rounding-level).
+__global__ __launch_bounds__(256) void gae_scan_kernel(const float* __restrict__ rew, const float* __restrict__ val,
+                                                       const float* __restrict__ done, float* __restrict__ adv,
+                                                       float* __restrict__ ret, int T, int E, float gamma,
+                                                       float lam) {
+  __shared__ float sD[256], sC[256];
+  const int e = blockIdx.x, j = threadIdx.x;
+  const int chunk = (T + 255) / 256;
+  const int t0 = min(T, j * chunk), t1 = min(T, t0 + chunk);
+  auto delta_c = [&](int t, float& delta, float& c) {
+    const size_t o = (size_t)t * E + e;
+    const float nt = 1.f - done[o];
+    delta = rew[o] + gamma * val[o + E] * nt - val[o];
+    c = gamma * lam * nt;
+  };
+  float D = 0.f, C = 1.f;
+  for (int t = t1 - 1; t >= t0; --t) {
+    float d, c;
+    delta_c(t, d, c);
+    D = d + c * D;
+    C = c * C;
+  }
+  sD[j] = D;
+  sC[j] = C;
+  __syncthreads();
+  // inclusive scan from the right: after it, (sD[j], sC[j]) = map_j o map_{j+1} o ... o map_255
+  for (int off = 1; off < 256; off <<= 1) {
+    float d2 = 0.f, c2 = 1.f;
+    const bool has = j + off < 256;
+    if (has) { d2 = sD[j + off]; c2 = sC[j + off]; }
+    __syncthreads();
+    if (has) {
+      sD[j] = sD[j] + sC[j] * d2;
+      sC[j] = sC[j] * c2;
+    }
+    __syncthreads();
+  }
+  // A at the end of this chunk = (maps of chunks j+1..255) applied to A_T = 0
+  float a = (j + 1 < 256) ? sD[j + 1] : 0.f;
+  for (int t = t1 - 1; t >= t0; --t) {
+    float d, c;
+    delta_c(t, d, c);
+    a = d + c * a;
+    const size_t o = (size_t)t * E + e;
+    adv[o] = a;
+    ret[o] = a + val[o];
+  }
+}
+
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, int n, float* __restrict__ part,
                                                     float* __restrict__ state) {
   __shared__ float red[256];
@@ -109,9 +165,15 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ p, 
 }  // namespace
 
 extern "C" void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
-                           int T, int E, float gamma, float lam, hipStream_t s) {
-  hipLaunchKernelGGL(gae_kernel, dim3((E + 255) / 256), dim3(256), 0, s, rewards, values, dones, adv, ret, T, E,
-                     gamma, lam);
+                           int T, int E, float gamma, float lam, int mode, hipStream_t s) {
+  // mode 0 = auto: the per-env lane scan keeps >= 1 full wave busy per env batch; with few envs
+  // and a long horizon its single dependent chain per lane is the latency, so scan in time.
+  const bool scan = mode == 2 || (mode == 0 && E <= 64 && T >= 512);
+  if (scan)
+    hipLaunchKernelGGL(gae_scan_kernel, dim3(E), dim3(256), 0, s, rewards, values, dones, adv, ret, T, E, gamma, lam);
+  else
+    hipLaunchKernelGGL(gae_kernel, dim3((E + 255) / 256), dim3(256), 0, s, rewards, values, dones, adv, ret, T, E,
+                       gamma, lam);
   HIP_CHECK_LAUNCH();
 }
 

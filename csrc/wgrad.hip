@@ -33,30 +33,44 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  Frag an[4], bn[4];
+  // Two register slots in ping-pong, the loop unrolled by two so each slot keeps fixed
+  // registers (no copies).  Every prefetch is unconditional (clamped to the last step; its
+  // data unused) and every MFMA in the loop is unconditional, so the number of loads in flight
+  // is path-independent and the compiler's waits stay partial (vmcnt(8): the next step's loads
+  // remain in flight while this step's MFMAs run).  The copy-rotation form this replaces
+  // drained vmcnt(0) at the top of every step.
+  const int nk = (tk.m1 - tk.m0) >> 5;
+  struct Slot { Frag a[4], b[4]; };
+  auto fetch = [&](Slot& d, int k) {
+    const size_t ko = (size_t)min(k, nk - 1) * 512;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    an[i] = P::load(gp + i * blk_row);
-    bn[i] = P::load(xp + i * blk_row);
-  }
-  const int lr = lane & 15;
-  for (int m = tk.m0; m < tk.m1; m += 32) {
-    Frag af[4], bf[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { af[i] = an[i]; bf[i] = bn[i]; }
-    if (m + 32 < tk.m1) {
-      const size_t ko = (size_t)((m + 32 - tk.m0) >> 5) * 512;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        an[i] = P::load(gp + i * blk_row + ko);
-        bn[i] = P::load(xp + i * blk_row + ko);
-      }
+    for (int i = 0; i < 4; ++i) {
+      d.a[i] = P::load(gp + i * blk_row + ko);
+      d.b[i] = P::load(xp + i * blk_row + ko);
     }
+  };
+  auto mma = [&](const Slot& c) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(acc[i][j], af[i], bf[j]);
+      for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(acc[i][j], c.a[i], c.b[j]);
+  };
+  // the host plan makes every chunk a multiple of 64 rows (two steps; checked in bindings.cpp)
+  Slot r0, r1;
+  fetch(r0, 0);
+  // sched_barrier pins the order "issue next step's loads, then this step's MFMAs" (the
+  // scheduler otherwise sinks each load next to its first use, which serialises on latency)
+  for (int k = 0; k < nk; k += 2) {
+    fetch(r1, k + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(r0);
+    __builtin_amdgcn_sched_barrier(0);
+    fetch(r0, k + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(r1);
+    __builtin_amdgcn_sched_barrier(0);
   }
+  const int lr = lane & 15;
   float* out = a.slab + tk.slab;
   const int col = wk * 64 + lr;
   const int rbase = wn * 64 + (lane >> 4) * 4;

@@ -58,7 +58,11 @@ def _digest(paths, extra: str) -> str:
 def _compile(src: str, cflags, verbose: bool) -> str:
     srcp = os.path.join(CSRC, src)
     deps = [srcp] + [os.path.join(CSRC, h) for h in HEADERS]
-    base = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+    # -amdgpu-mfma-vgpr-form: MFMA accumulators in ordinary VGPRs (gfx90a+ unified register
+    # file).  With AGPR accumulators the allocator shuffled them through VGPRs every loop turn
+    # (~1,600 v_accvgpr_* in mlp_train, 96 per wgrad k-step pair); with it those copies vanish.
+    base = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+            "-mllvm", "-amdgpu-mfma-vgpr-form"]
     flags = base + cflags
     key = _digest(deps, " ".join(flags))
     obj = os.path.join(BUILD, f"{os.path.splitext(src)[0]}-{key}.o")

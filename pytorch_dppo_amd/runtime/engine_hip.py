@@ -103,7 +103,7 @@ class HipEngine:
         self.epstat = torch.zeros(nroll, 2, **f32)
         # ---- update geometry ----
         self.mb = params.minibatch_rows()
-        self.ldT = _r(self.mb, 32)
+        self.ldT = _r(self.mb, 64)      # wgrad consumes k-steps in pairs (csrc/wgrad.hip)
         self.train_rows = int(self.ext.train_rows(self.dt))
         self.ntrain_blk = self.ldT // self.train_rows
         self.npart = NPART_FIXED + A
@@ -176,7 +176,7 @@ class HipEngine:
         want = -(-1024 // ntiles)                 # >= ~1024 workgroups in flight
         want = -(-want // 8) * 8                  # whole chunks per XCD (8 XCDs)
         nchunks = max(1, min(max_chunks, want))
-        mc = _r(-(-self.ldT // nchunks), 32)
+        mc = _r(-(-self.ldT // nchunks), 64)   # even number of 32-row k-steps per task
         chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
         self.nchunks = len(chunks)
         self.chunk_stride = ntiles * WT * WT
@@ -318,7 +318,7 @@ class HipEngine:
     def gae(self) -> None:
         T, E = self.T, self.E
         self.ext.gae(self.rewards.view(T, E), self.values_buf.view(T + 1, E), self.dones.view(T, E),
-                     self.adv.view(T, E), self.ret.view(T, E), float(self.p.gamma), float(self.p.gae_param))
+                     self.adv.view(T, E), self.ret.view(T, E), float(self.p.gamma), float(self.p.gae_param), 0)
         if self.p.normalize_adv:
             m, s = self.adv.mean(), self.adv.std()
             self.adv.sub_(m).div_(s + 1e-8)
