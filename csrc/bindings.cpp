@@ -17,6 +17,11 @@ hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 // training runs (the results of an ablated call are not a gradient)
 int g_train_ablate = 0;
 void set_train_ablation(int64_t mask) { g_train_ablate = (int)mask; }
+int g_wgrad_impl = 0;   // 0: LDS-DMA staged, 1: register-streamed (A/B diagnostics)
+void set_wgrad_impl(int64_t impl) {
+  TORCH_CHECK(impl == 0 || impl == 1, "wgrad impl: 0 LDS-DMA, 1 register");
+  g_wgrad_impl = (int)impl;
+}
 
 at::ScalarType storage_type(int dt) {
   return dt == 0 ? at::kFloat : (dt == 1 ? at::kBFloat16 : at::kByte);
@@ -295,6 +300,8 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
   a.tasks = reinterpret_cast<const WgradTask*>(tasks.data_ptr<int>());
   a.ntasks = ntasks;
   a.slab = slab.data_ptr<float>();
+  a.impl = g_wgrad_impl;
+  TORCH_CHECK(dt == 0 || dt == 1, "wgrad runs in fp32 or bf16 (the fp8 mode's update is bf16)");
   launch_wgrad((int)dt, a, cur_stream());
 }
 
@@ -394,6 +401,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_gather", &grad_gather);
   m.def("gae", &gae);
   m.def("set_train_ablation", &set_train_ablation);
+  m.def("set_wgrad_impl", &set_wgrad_impl);
   m.def("obs_reduce", &obs_reduce);
   m.def("obs_merge", &obs_merge);
   m.def("adam", &adam);

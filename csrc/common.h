@@ -104,13 +104,11 @@ template <int DT> struct Lds {
   __host__ __device__ static constexpr int stride(int d) { return d + PAD; }
 };
 
+// tanh from one v_exp_f32 and one v_rcp_f32 (no IEEE division); |err| ~1e-7, saturates cleanly
+// (e -> 0 as |x| grows).  Used by the env dynamics inside the rollout kernel.
 DEV float fast_tanh(float x) {
-  // tanh via exp: accurate to ~1 ulp of f32 for |x| < 9, saturates beyond
-  float ax = fabsf(x);
-  if (ax > 9.0f) return copysignf(1.0f, x);
-  float e = __expf(2.0f * ax);
-  float t = 1.0f - 2.0f / (e + 1.0f);
-  return copysignf(t, x);
+  const float e = __expf(-2.0f * fabsf(x));
+  return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), x);
 }
 
 // ---- counter RNG (must match utils/rng.py) -------------------------------------------------
@@ -118,16 +116,25 @@ DEV uint32_t hash_u32(uint32_t x) {
   x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
   return x;
 }
+// key chain: keyed = hash(hash(hash(env ^ base) ^ step) ^ dim).  key_es is the (env, step)
+// prefix, shared by every dim of one env step: kernels compute it once per env and step.
+DEV uint32_t key_es(uint32_t base, uint32_t env, uint32_t step) { return hash_u32(hash_u32(env ^ base) ^ step); }
 DEV uint32_t keyed(uint32_t base, uint32_t env, uint32_t step, uint32_t dim) {
-  uint32_t h = hash_u32(env ^ base);
-  h = hash_u32(h ^ step);
-  return hash_u32(h ^ dim);
+  return hash_u32(key_es(base, env, step) ^ dim);
 }
 DEV float uniform01(uint32_t h) { return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f); }
+// Box-Muller pair p: (r cos 2pi u2, r sin 2pi u2) = the normals of dims 2p and 2p+1
+// (utils/rng.py: gauss).  Hardware transcendentals: v_log_f32, v_sqrt_f32, and v_sin/v_cos,
+// which take the angle in revolutions, so 2*pi*u2 is never formed.
+DEV float2 gauss_pair(uint32_t kes, uint32_t p) {
+  const float u1 = uniform01(hash_u32(kes ^ (2u * p)));
+  const float u2 = uniform01(hash_u32(kes ^ (2u * p + 1u)));
+  const float r = __builtin_sqrtf(-2.0f * 0.6931471805599453f * __builtin_amdgcn_logf(u1));
+  return make_float2(r * __builtin_amdgcn_cosf(u2), r * __builtin_amdgcn_sinf(u2));
+}
 DEV float gauss(uint32_t base, uint32_t env, uint32_t step, uint32_t dim) {
-  float u1 = uniform01(keyed(base, env, step, 2u * dim));
-  float u2 = uniform01(keyed(base, env, step, 2u * dim + 1u));
-  return sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795864f * u2);
+  const float2 g = gauss_pair(key_es(base, env, step), dim >> 1);
+  return (dim & 1u) ? g.y : g.x;
 }
 
 #define HIP_CHECK_LAUNCH()                                                       \

@@ -101,6 +101,7 @@ struct WgradArgs {
   const WgradTask* tasks;
   int ntasks;
   float* slab;
+  int impl;            // 0: LDS-DMA staged (default), 1: register-streamed (A/B diagnostics)
 };
 
 extern "C" {

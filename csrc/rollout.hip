@@ -33,6 +33,8 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
   using P = Prec<DT>;
   using T = typename P::T;
   constexpr int NW = 4;
+  constexpr int NTHR = 64 * NW;
+  static_assert(ROWS % 4 == 0 && NTHR % ROWS == 0 && (NTHR / ROWS) <= 64, "rollout tiling");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int e0 = blockIdx.x * ROWS;
   const int nvalid = min(ROWS, a.E - e0);
@@ -54,6 +56,7 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
   int* eplen = cv.take<int>(ROWS);
   float* epret = cv.take<float>(ROWS);
   float* epacc = cv.take<float>(2 * ROWS);
+  uint32_t* kes = cv.take<uint32_t>(3 * ROWS);   // per-env key prefixes of this step: action, env, reset
 
   const T* W = reinterpret_cast<const T*>(a.W);
   const T* W1 = W + a.off_w1;
@@ -140,68 +143,92 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
     __syncthreads();
     layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32>(h2, ld3, a.d3, W3, a.n3, mu, A, sc3, wave, lane);
     __syncthreads();
-    // ---- (c) sample a = mu + sigma * eps ----
+    // ---- (c) sample a = mu + sigma * eps (one Box-Muller pair -> two action dims) ----
     const uint32_t kstep = a.t0 + (uint32_t)step;
-    for (int i = tid; i < ROWS * A; i += 256) {
-      int r = i / A, j = i - r * A;
-      float ls = a.log_std[j];
-      float lsig = a.std_var ? 0.5f * ls : ls;
-      float eps = gauss(a.key_action, (uint32_t)(e0 + r), kstep, (uint32_t)j);
-      float av = mu[i] + __expf(lsig) * eps;
-      act[i] = av;
-      epsb[i] = eps;
-      if (r < nvalid) a.actions[((size_t)tb * a.buf_E + e0 + r) * A + j] = av;
+    if (tid < ROWS) {   // (env, step) key prefixes, shared by every dim of the step
+      const uint32_t e = (uint32_t)(e0 + tid);
+      kes[tid] = key_es(a.key_action, e, kstep);
+      kes[ROWS + tid] = key_es(a.key_env, e, kstep);
+      kes[2 * ROWS + tid] = key_es(a.key_reset, e, kstep);
+    }
+    __syncthreads();
+    const int npa = (A + 1) >> 1;
+    for (int i = tid; i < ROWS * npa; i += NTHR) {
+      const int r = i / npa, q = i - r * npa;
+      const float2 g = gauss_pair(kes[r], (uint32_t)q);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * q + h;
+        if (j < A) {
+          const float ls = a.log_std[j];
+          const float lsig = a.std_var ? 0.5f * ls : ls;
+          const float eps = h ? g.y : g.x;
+          const float av = mu[r * A + j] + __expf(lsig) * eps;
+          act[r * A + j] = av;
+          epsb[r * A + j] = eps;
+          if (r < nvalid) a.actions[((size_t)tb * a.buf_E + e0 + r) * A + j] = av;
+        }
+      }
     }
     __syncthreads();
     // ---- (d) per-env: logp, reward, termination, episode bookkeeping ----
-    if (tid < ROWS) {
-      const int r = tid;
+    // LPE lanes per env (contiguous inside a wave) share the per-dim sums, then reduce by shuffles
+    {
+      constexpr int LPE = NTHR / ROWS;
+      const int r = tid / LPE, l = tid - r * LPE;
       const int e = e0 + r;
-      float lp = 0.f;
-      for (int j = 0; j < A; ++j) {
-        float ls = a.log_std[j];
-        float lsig = a.std_var ? 0.5f * ls : ls;
-        float ep = epsb[r * A + j];
-        lp += -0.5f * ep * ep - 0.5f * LOG_2PI_F - lsig;
-      }
-      float rew;
-      bool term = false;
-      if (a.kind == 1) {
-        float th = st[r * S], thd = st[r * S + 1];
-        float u = fminf(fmaxf(act[r * A], -2.f), 2.f);
-        float thn = fmodf(th + 3.14159265358979f, 6.28318530717959f);
-        if (thn < 0.f) thn += 6.28318530717959f;
-        thn -= 3.14159265358979f;
-        rew = -(thn * thn + 0.1f * thd * thd + 0.001f * u * u);
-      } else {
-        int na = min(A, O);
-        float acc = 0.f;
-        for (int j = 0; j < na; ++j) {
-          float ac = fminf(fmaxf(act[r * A + j], -1.f), 1.f);
-          float er = ac - tanhf(st[r * S + j]);
-          acc += er * er;
+      float lp = 0.f, err = 0.f;
+      const int na = min(A, O);
+      for (int j = l; j < A; j += LPE) {
+        const float ls = a.log_std[j];
+        const float lsig = a.std_var ? 0.5f * ls : ls;
+        const float ep = epsb[r * A + j];
+        lp += -0.5f * ep * ep - lsig;
+        if (a.kind != 1 && j < na) {
+          const float ac = fminf(fmaxf(act[r * A + j], -1.f), 1.f);
+          const float d = ac - fast_tanh(st[r * S + j]);
+          err += d * d;
         }
-        rew = 1.f - acc / (float)na;
-        term = uniform01(keyed(a.key_term, (uint32_t)e, kstep, 0u)) < SYN_TERM_P;
       }
-      int el = eplen[r] + 1;
-      float er_ = epret[r] + rew;
-      bool done = term || (el >= a.limit);
-      if (done) {
-        if (r < nvalid) { epacc[2 * r] += er_; epacc[2 * r + 1] += 1.f; }
-        el = 0;
-        er_ = 0.f;
+#pragma unroll
+      for (int o = LPE / 2; o > 0; o >>= 1) {
+        lp += __shfl_xor(lp, o, LPE);
+        err += __shfl_xor(err, o, LPE);
       }
-      eplen[r] = el;
-      epret[r] = er_;
-      done_s[r] = done ? 1.f : 0.f;
-      if (r < nvalid) {
-        size_t o = (size_t)tb * a.buf_E + e;
-        float rc = rew;
-        if (a.reward_clip > 0.f) rc = fminf(fmaxf(rc, -a.reward_clip), a.reward_clip);
-        a.logp[o] = lp;
-        a.rewards[o] = rc;
-        a.dones[o] = done ? 1.f : 0.f;
+      if (l == 0) {
+        lp -= 0.5f * LOG_2PI_F * (float)A;
+        float rew;
+        bool term = false;
+        if (a.kind == 1) {
+          float th = st[r * S], thd = st[r * S + 1];
+          float u = fminf(fmaxf(act[r * A], -2.f), 2.f);
+          float thn = fmodf(th + 3.14159265358979f, 6.28318530717959f);
+          if (thn < 0.f) thn += 6.28318530717959f;
+          thn -= 3.14159265358979f;
+          rew = -(thn * thn + 0.1f * thd * thd + 0.001f * u * u);
+        } else {
+          rew = 1.f - err / (float)na;
+          term = uniform01(keyed(a.key_term, (uint32_t)e, kstep, 0u)) < SYN_TERM_P;
+        }
+        int el = eplen[r] + 1;
+        float er_ = epret[r] + rew;
+        bool done = term || (el >= a.limit);
+        if (done) {
+          if (r < nvalid) { epacc[2 * r] += er_; epacc[2 * r + 1] += 1.f; }
+          el = 0;
+          er_ = 0.f;
+        }
+        eplen[r] = el;
+        epret[r] = er_;
+        done_s[r] = done ? 1.f : 0.f;
+        if (r < nvalid) {
+          size_t o = (size_t)tb * a.buf_E + e;
+          float rc = rew;
+          if (a.reward_clip > 0.f) rc = fminf(fmaxf(rc, -a.reward_clip), a.reward_clip);
+          a.logp[o] = lp;
+          a.rewards[o] = rc;
+          a.dones[o] = done ? 1.f : 0.f;
+        }
       }
     }
     __syncthreads();
@@ -225,18 +252,33 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
         }
       }
     } else {
-      for (int i = tid; i < ROWS * S; i += 256) {
-        int r = i / S, d = i - r * S;
-        uint32_t e = (uint32_t)(e0 + r);
-        float ns;
-        if (done_s[r] > 0.5f) {
-          ns = SYN_RESET * gauss(a.key_reset, e, kstep, (uint32_t)d);
-        } else {
-          float w = 0.5f + (float)(d % 7) / 7.0f;
-          float ac = fminf(fmaxf(act[r * A + (d % A)], -1.f), 1.f);
-          ns = SYN_DECAY * st[i] + SYN_DRIVE * tanhf(w * ac) + SYN_NOISE * gauss(a.key_env, e, kstep, (uint32_t)d);
+      // item = (dim pair p, group of 4 rows): one runtime division per item, the per-dim
+      // constants (drive weight, action index) once per item, one Box-Muller pair per 2 dims
+      const int np = (S + 1) >> 1;
+      for (int it = tid; it < np * (ROWS / 4); it += NTHR) {
+        const int rg = it / np, p = it - rg * np;
+        const int d0 = 2 * p, d1 = d0 + 1;
+        const bool has1 = d1 < S;
+        const float w0 = 0.5f + (float)(d0 % 7) / 7.0f, w1 = 0.5f + (float)(d1 % 7) / 7.0f;
+        const int j0 = d0 % A, j1 = d1 % A;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int r = rg * 4 + k;
+          float n0, n1;
+          if (done_s[r] > 0.5f) {
+            const float2 g = gauss_pair(kes[2 * ROWS + r], (uint32_t)p);
+            n0 = SYN_RESET * g.x;
+            n1 = SYN_RESET * g.y;
+          } else {
+            const float2 g = gauss_pair(kes[ROWS + r], (uint32_t)p);
+            const float a0 = fminf(fmaxf(act[r * A + j0], -1.f), 1.f);
+            const float a1 = fminf(fmaxf(act[r * A + j1], -1.f), 1.f);
+            n0 = SYN_DECAY * st[r * S + d0] + SYN_DRIVE * fast_tanh(w0 * a0) + SYN_NOISE * g.x;
+            n1 = has1 ? SYN_DECAY * st[r * S + d1] + SYN_DRIVE * fast_tanh(w1 * a1) + SYN_NOISE * g.y : 0.f;
+          }
+          st[r * S + d0] = n0;
+          if (has1) st[r * S + d1] = n1;
         }
-        st[i] = ns;
       }
     }
     __syncthreads();
@@ -270,6 +312,7 @@ size_t rollout_lds(const RolloutArgs& a) {
   b += 3 * al(sizeof(float) * ROWS * a.A);
   b += 2 * al(sizeof(float) * a.O);
   b += al(sizeof(float) * ROWS) + al(sizeof(int) * ROWS) + al(sizeof(float) * ROWS) + al(sizeof(float) * 2 * ROWS);
+  b += al(sizeof(uint32_t) * 3 * ROWS);
   return b;
 }
 

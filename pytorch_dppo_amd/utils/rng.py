@@ -67,8 +67,12 @@ def uniform01(h: torch.Tensor) -> torch.Tensor:
 
 
 def gauss(base: int, env: torch.Tensor, step, dim: torch.Tensor) -> torch.Tensor:
-    """Standard normal by Box-Muller from two keyed uniforms (dims 2d and 2d+1)."""
-    d2 = dim.to(torch.int64) * 2
-    u1 = uniform01(keyed(base, env, step, d2))
-    u2 = uniform01(keyed(base, env, step, d2 + 1))
-    return torch.sqrt(-2.0 * torch.log(u1)) * torch.cos((2.0 * math.pi) * u2)
+    """Standard normal by Box-Muller; dims 2p and 2p+1 share one uniform pair p (keys 2p, 2p+1)
+    and take its cosine and sine branch respectively, so a kernel draws two normals per pair."""
+    dim = dim.to(torch.int64)
+    p2 = (dim >> 1) * 2
+    u1 = uniform01(keyed(base, env, step, p2))
+    u2 = uniform01(keyed(base, env, step, p2 + 1))
+    r = torch.sqrt(-2.0 * torch.log(u1))
+    ang = (2.0 * math.pi) * u2
+    return r * torch.where((dim & 1) == 0, torch.cos(ang), torch.sin(ang))

@@ -18,8 +18,9 @@ from pytorch_dppo_amd.models.actor_critic import ActorCritic  # noqa: E402
 from pytorch_dppo_amd.runtime.engine_hip import HipEngine  # noqa: E402
 from pytorch_dppo_amd.utils.obs_stats import RunningObsStats  # noqa: E402
 
-VARIANTS = {"full": 0, "no_transposed_stores": 1, "no_v_fc1": 2, "no_dgrad": 4, "no_loss": 8,
-            "fwd_only_no_stores": 1 | 4 | 8}
+# name -> (mlp_train ablation mask, wgrad impl)
+VARIANTS = {"full": (0, 0), "wgrad_register_path": (0, 1), "no_transposed_stores": (1, 0), "no_v_fc1": (2, 0),
+            "no_dgrad": (4, 0), "no_loss": (8, 0), "fwd_only_no_stores": (1 | 4 | 8, 0)}
 
 
 def main():
@@ -42,8 +43,9 @@ def main():
     ext = eng.ext
     res = {k: [] for k in VARIANTS}
     for rnd in range(6):
-        for name, mask in VARIANTS.items():
+        for name, (mask, impl) in VARIANTS.items():
             ext.set_train_ablation(mask)
+            ext.set_wgrad_impl(impl)
             for _ in range(2):
                 eng.grad(None)   # warm
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -54,6 +56,7 @@ def main():
             torch.cuda.synchronize()
             res[name].append(s.elapsed_time(e) / 5 * 1e3)
     ext.set_train_ablation(0)
+    ext.set_wgrad_impl(0)
     out = {k: {"median_us": sorted(v)[len(v) // 2], "min_us": min(v)} for k, v in res.items()}
     print(json.dumps(out, indent=1))
 

@@ -377,3 +377,25 @@ def test_graph_replay_bit_identical_to_eager(batch):
     assert torch.equal(we.model.flat.data, wg.model.flat.data)
     assert torch.equal(we.engine.adam_m, wg.engine.adam_m)
     assert me["loss_value"] == mg["loss_value"]
+
+
+def test_wgrad_lds_dma_matches_register_path_bitwise():
+    """The LDS-DMA staged wgrad (default) and the register-streamed one accumulate the same
+    k-steps in the same order: gradients must agree bit for bit (fp32 and bf16)."""
+    for dt in ("fp32", "bf16"):
+        p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 8,
+                        batch_size=64 * 8, num_epoch=1, dtype=dt)
+        eng, model, env, st = _engine(p)
+        st.observes(env.observe())
+        eng.rollout()
+        eng.values()
+        eng.gae()
+        eng.begin_update()
+        ext = eng.ext
+        outs = []
+        for impl in (0, 1):
+            ext.set_wgrad_impl(impl)
+            eng.grad(None)
+            outs.append(eng.grad_flat.clone())
+        ext.set_wgrad_impl(0)
+        assert torch.equal(outs[0], outs[1]), (dt, (outs[0] - outs[1]).abs().max().item())
