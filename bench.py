@@ -78,14 +78,18 @@ def main():
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    # the production loop (run_worker): each iteration's metrics are read one iteration later,
+    # so the host enqueues the next rollout while the device still runs this update.  Every
+    # kernel of all K iterations is inside the timed region (closing synchronize below).
     for i in range(args.steps):
-        m = w.iteration_step()
-        if args.verbose and ctx.rank == 0:
-            print("step", i, json.dumps({k: round(v, 4) if isinstance(v, float) else v for k, v in m.items()}),
+        mi = w.iteration_step(defer=True)
+        if args.verbose and ctx.rank == 0 and mi:
+            print("step", i, json.dumps({k: round(v, 4) if isinstance(v, float) else v for k, v in mi.items()}),
                   file=sys.stderr, flush=True)
     ctx.barrier()
     torch.cuda.synchronize()
     el = torch.tensor([time.perf_counter() - t0], device=ctx.device, dtype=torch.float64)
+    m = w.finish_metrics() or m
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     total_steps = rows * ctx.world_size * args.steps

@@ -404,16 +404,25 @@ class HipEngine:
         self.adam_step += 1
         return None
 
-    def last_losses(self) -> Dict[str, float]:
+    def loss_vector(self) -> Optional[torch.Tensor]:
+        """device [loss sums of the last minibatch (8) | grad norm of the last Adam step] — staged
+        into host memory by the worker without a sync (``losses_from_vector`` decodes it)."""
         if self._loss_dev is None:
-            return {}
-        v = self._loss_dev.tolist()
+            return None
+        return torch.cat([self._loss_dev.reshape(-1), self.adam_state[2:3]])
+
+    @staticmethod
+    def losses_from_vector(v) -> Dict[str, float]:
         n = max(v[5], 1.0)
         out = {"loss_clip": v[0] / n, "loss_value": v[1] / n, "loss_ent": v[2] / n,
                "approx_kl": v[3] / n, "clipfrac": v[4] / n}
         out["loss"] = out["loss_clip"] + out["loss_value"] + out["loss_ent"]
-        out["grad_norm"] = float(self.adam_state[2])
+        out["grad_norm"] = float(v[NPART_FIXED])
         return out
+
+    def last_losses(self) -> Dict[str, float]:
+        vec = self.loss_vector()
+        return {} if vec is None else self.losses_from_vector(vec.tolist())
 
     def sync(self) -> None:
         torch.cuda.synchronize(self.device)

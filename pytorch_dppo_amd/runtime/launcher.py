@@ -60,20 +60,29 @@ def run_worker(params: Params, ctx: DistContext, max_iters: Optional[int] = None
     prof = _Profiler(params, ctx)
     try:
         n = 0
+        # GPU: metrics are resolved one iteration late, so the host never idles the device at
+        # an iteration boundary waiting for numbers it only logs
+        defer = ctx.device.type == "cuda"
+
+        def record(m):
+            if not m:
+                return
+            history.append(m)
+            if ctx.is_main and params.log_every and int(m["iteration"]) % params.log_every == 0:
+                log.log(m)
+
         while not w.should_stop():
             prof.before(n)
-            m = w.iteration_step()
+            record(w.iteration_step(defer=defer))
             prof.after(n)
-            history.append(m)
             n += 1
-            if ctx.is_main and params.log_every and w.iteration % params.log_every == 0:
-                log.log(m)
             if ev is not None and w.iteration % params.eval_every == 0:
                 ev.push(w.model.state_dict(), w.stats.state_dict(), w.iteration)
             if params.checkpoint_dir and params.checkpoint_every and w.iteration % params.checkpoint_every == 0:
                 save(w, ctx, params.checkpoint_dir)
             if max_iters is not None and n >= max_iters:
                 break
+        record(w.finish_metrics())
         w.flush_pending()
         if params.checkpoint_dir:
             save(w, ctx, params.checkpoint_dir)

@@ -64,6 +64,7 @@ class DPPOWorker:
         self.last_metrics: Dict = {}
         self._perm_gen = torch.Generator(device="cpu")
         self._pending = None          # (async all-reduce work, extra) under --overlap-rollout
+        self._staged = None           # metrics of the last deferred iteration (iteration_step(defer=True))
 
     # ---------------------------------------------------------------------------------------
     def _merge_stats(self, count, s1, s2, shift, count_uniform: bool = False) -> None:
@@ -87,11 +88,20 @@ class DPPOWorker:
         nmb = self.p.num_minibatches()
         return N, mb, nmb
 
-    def iteration_step(self) -> Dict:
-        """One DPPO iteration; returns the rank-0-relevant metrics dict."""
+    def iteration_step(self, defer: bool = False) -> Dict:
+        """One DPPO iteration.
+
+        ``defer=False``: returns this iteration's metrics (host sync at the end).
+        ``defer=True``: enqueues everything, stages the device-side metrics (loss sums, grad
+        norm, all-reduced episode stats, phase events) into pinned host memory behind an event,
+        and returns the metrics of the PREVIOUS iteration, which by then are complete — the host
+        never waits on the iteration it just launched, so the next rollout is enqueued while the
+        GPU still runs this update (no idle gap at the iteration boundary).  ``finish_metrics``
+        resolves the last one."""
         p, eng, tm = self.p, self.engine, self.timer
         self.init_stats()
         t0 = time.perf_counter()
+        tm.start("iteration")
         tm.start("rollout")
         ro = eng.rollout()
         # --overlap-rollout (SURVEY §5.8 option b): the previous iteration's final gradient
@@ -113,8 +123,6 @@ class DPPOWorker:
         tm.start("update")
         eng.begin_update()
         N, mb, nmb = self._minibatch_plan()
-        losses = {}
-        gnorm = 0.0
         mean = p.grad_reduce == "mean"
         self._perm_gen.manual_seed((p.seed * 1000003 + self.ctx.rank * 7919 + self.iteration) & 0x7FFFFFFF)
         for epoch in range(p.num_epoch):
@@ -143,25 +151,73 @@ class DPPOWorker:
                     eng.apply(extra)
                 self.updates += 1
         tm.stop("update")
-        eng.sync()
-        losses = eng.last_losses()
-        gnorm = losses.pop("grad_norm", 0.0)
-        dt = time.perf_counter() - t0
+        tm.stop("iteration")
         steps_local = eng.T * eng.E
         self.env_steps += steps_local * self.ctx.world_size
         self.iteration += 1
-        sc = self.ctx.allreduce_scalars({"ep_return_sum": ro["ep_return_sum"],
-                                         "ep_count": ro["ep_count"]})
-        m = {"iteration": self.iteration, "env_steps": self.env_steps, "updates": self.updates,
-             "iter_s": dt, "steps_per_s": steps_local * self.ctx.world_size / max(dt, 1e-9),
-             "ep_count": sc["ep_count"],
-             "mean_ep_return": (sc["ep_return_sum"] / sc["ep_count"]) if sc["ep_count"] > 0 else float("nan"),
-             "grad_norm": gnorm, **{k: v for k, v in losses.items()}, **tm.summary()}
-        if p.verify_sync_every and self.iteration % p.verify_sync_every == 0:
+        staged = self._stage_metrics(ro, t0, steps_local)
+        if not defer:
+            m = self._resolve_metrics(staged)
+            self.last_metrics = m
+            return m
+        prev, self._staged = self._staged, staged
+        m = self._resolve_metrics(prev) if prev is not None else {}
+        if m:
+            self.last_metrics = m
+        return m
+
+    def finish_metrics(self) -> Dict:
+        """resolve the metrics still staged by a deferred ``iteration_step`` (or {})."""
+        prev, self._staged = self._staged, None
+        m = self._resolve_metrics(prev) if prev is not None else {}
+        if m:
+            self.last_metrics = m
+        return m
+
+    def _stage_metrics(self, ro: Dict, t0: float, steps_local: int) -> Dict:
+        """Device-side metric values of this iteration -> one pinned host buffer (async)."""
+        eng = self.engine
+        dev = self.device
+        parts = [torch.stack([torch.as_tensor(ro["ep_return_sum"], dtype=torch.float64, device=dev).reshape(()),
+                              torch.as_tensor(ro["ep_count"], dtype=torch.float64, device=dev).reshape(())])]
+        parts[0] = self.ctx.allreduce_tensor_(parts[0])        # R5: episode stats over ranks
+        loss_dev = eng.loss_vector() if hasattr(eng, "loss_vector") else None
+        if loss_dev is not None:
+            parts.append(loss_dev.to(torch.float64))
+        flat = torch.cat([x.reshape(-1) for x in parts])
+        if dev.type == "cuda":
+            host = torch.empty(flat.numel(), dtype=torch.float64, pin_memory=True)
+            host.copy_(flat, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = flat, None
+        return {"host": host, "event": ev, "phases": self.timer.collect(), "has_loss": loss_dev is not None,
+                "iteration": self.iteration, "env_steps": self.env_steps, "updates": self.updates,
+                "host_s": time.perf_counter() - t0, "steps_local": steps_local}
+
+    def _resolve_metrics(self, st: Dict) -> Dict:
+        p = self.p
+        if st["event"] is not None:
+            st["event"].synchronize()
+        v = st["host"].tolist()
+        ep_ret, ep_cnt = v[0], v[1]
+        if st["has_loss"]:
+            losses = self.engine.losses_from_vector(v[2:])
+        else:
+            losses = self.engine.last_losses()
+        gnorm = losses.pop("grad_norm", 0.0)
+        phases = PhaseTimer.elapsed(st["phases"])
+        it_ms = phases.pop("ms_iteration", None)
+        dt = (it_ms / 1e3) if it_ms else st["host_s"]
+        m = {"iteration": st["iteration"], "env_steps": st["env_steps"], "updates": st["updates"],
+             "iter_s": dt, "steps_per_s": st["steps_local"] * self.ctx.world_size / max(dt, 1e-9),
+             "ep_count": ep_cnt, "mean_ep_return": (ep_ret / ep_cnt) if ep_cnt > 0 else float("nan"),
+             "grad_norm": gnorm, **losses, **phases}
+        if p.verify_sync_every and st["iteration"] % p.verify_sync_every == 0:
             m["replicas_in_sync"] = self.ctx.verify_replicas(self.model.flat.data)
         if p.check_finite:
             self._check_finite(m)
-        self.last_metrics = m
         return m
 
     def _check_finite(self, m: Dict) -> None:
@@ -169,12 +225,13 @@ class DPPOWorker:
         parameters are not finite, naming what broke (the phase timings are in ``m``)."""
         bad = [k for k in ("loss", "loss_clip", "loss_value", "loss_ent", "grad_norm")
                if k in m and not math.isfinite(m[k])]
+        it = m.get("iteration", self.iteration)
         if not bool(torch.isfinite(self.model.flat.data).all()):
             bad.append("parameters")
         if bool(torch.isfinite(self.stats.mean_f32).all()) is False:
             bad.append("obs_stats.mean")
         if bad:
-            raise FloatingPointError(f"rank {self.ctx.rank} iteration {self.iteration}: non-finite {bad}")
+            raise FloatingPointError(f"rank {self.ctx.rank} iteration {int(it)}: non-finite {bad}")
 
     def flush_pending(self) -> None:
         """complete a deferred (overlapped) all-reduce + Adam step, if any."""

@@ -52,16 +52,26 @@ class PhaseTimer:
         else:
             self._done.setdefault(name, []).append((time.perf_counter() - s) * 1e3)
 
-    def summary(self) -> Dict[str, float]:
+    def collect(self):
+        """hand over this iteration's finished phases (events are read later, see ``elapsed``)."""
+        done, self._done = self._done, {}
+        return (self.gpu, done)
+
+    @staticmethod
+    def elapsed(collected) -> Dict[str, float]:
+        gpu, done = collected
         out = {}
-        for k, lst in self._done.items():
-            if self.gpu:
-                torch.cuda.synchronize()
+        for k, lst in done.items():
+            if gpu:
+                for _, e in lst:
+                    e.synchronize()
                 out[f"ms_{k}"] = sum(s.elapsed_time(e) for s, e in lst)
             else:
                 out[f"ms_{k}"] = sum(lst)
-        self._done = {}
         return out
+
+    def summary(self) -> Dict[str, float]:
+        return PhaseTimer.elapsed(self.collect())
 
 
 CSV_COLUMNS = ("iteration", "env_steps", "updates", "steps_per_s", "mean_ep_return", "ep_count", "loss",

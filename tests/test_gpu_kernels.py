@@ -399,3 +399,26 @@ def test_wgrad_lds_dma_matches_register_path_bitwise():
             outs.append(eng.grad_flat.clone())
         ext.set_wgrad_impl(0)
         assert torch.equal(outs[0], outs[1]), (dt, (outs[0] - outs[1]).abs().max().item())
+
+
+def test_deferred_metrics_match_synchronous():
+    """iteration_step(defer=True) returns iteration i's metrics during iteration i+1; the values
+    must equal the synchronous path's (same seed, same work)."""
+    import math
+    from pytorch_dppo_amd.parallel.dist import DistContext
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    common = dict(device="gpu", env_name="Hopper-v2", num_envs=64, exploration_size=512, batch_size=512,
+                  num_epoch=2, dtype="bf16", seed=5)
+    ws = DPPOWorker(dppo_preset(**common), DistContext(device=DEV))
+    wd = DPPOWorker(dppo_preset(**common), DistContext(device=DEV))
+    sync = [ws.iteration_step() for _ in range(3)]
+    dfr = [wd.iteration_step(defer=True) for _ in range(3)] + [wd.finish_metrics()]
+    assert dfr[0] == {}
+    for a, b in zip(sync, dfr[1:]):
+        assert a["iteration"] == b["iteration"] and a["env_steps"] == b["env_steps"]
+        for k in ("loss", "loss_value", "grad_norm", "approx_kl", "ep_count"):
+            assert a[k] == b[k], (k, a[k], b[k])
+        assert (math.isnan(a["mean_ep_return"]) and math.isnan(b["mean_ep_return"])) or \
+            a["mean_ep_return"] == b["mean_ep_return"]
+        assert b["ms_update"] > 0 and b["steps_per_s"] > 0
+    assert torch.equal(ws.model.flat.data, wd.model.flat.data)
