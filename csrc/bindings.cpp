@@ -356,7 +356,9 @@ void gae(torch::Tensor rewards, torch::Tensor values, torch::Tensor dones, torch
 
 void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, double lr, double b1, double b2,
           double eps, double max_norm, torch::Tensor state, torch::Tensor norm_part, torch::Tensor wimg,
-          torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul) {
+          torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul, int64_t host_step) {
+  // host_step >= 1: the step number of this update (eager launch: one fused kernel when there is
+  // no clipping); 0: read the device counter (graph replay)
   const int64_t n = p.numel();
   check(p, "p", at::kFloat, n);
   check(g, "g", at::kFloat, n);
@@ -373,7 +375,8 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, do
   if (qmul.defined() && qmul.numel() > 0) { check(qmul, "qmul", at::kFloat, n); q = qmul.data_ptr<float>(); }
   launch_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (int)n, (float)lr,
               (float)b1, (float)b2, (float)eps, (float)max_norm, state.data_ptr<float>(), norm_part.data_ptr<float>(),
-              nblk, wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q, cur_stream());
+              nblk, wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q, (int)host_step,
+              cur_stream());
 }
 
 void pack(torch::Tensor p, torch::Tensor wimg, torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul) {
@@ -402,6 +405,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gae", &gae);
   m.def("set_train_ablation", &set_train_ablation);
   m.def("set_wgrad_impl", &set_wgrad_impl);
+  m.def("set_adam_fused", [](int64_t on) { set_adam_fused((int)on); });
   m.def("obs_reduce", &obs_reduce);
   m.def("obs_merge", &obs_merge);
   m.def("adam", &adam);

@@ -115,9 +115,10 @@ void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int 
                         int n, float* loss_out, hipStream_t s);
 void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
                 int T, int E, float gamma, float lam, int mode, hipStream_t s);
+void set_adam_fused(int on);
 void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, float b1, float b2,
                  float eps, float max_norm, float* state, float* norm_part, int nblk,
-                 void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale,
+                 void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale, int host_step,
                  hipStream_t s);
 void launch_pack(const float* p, int n, void* wimg, const int* w_map, const int* wt_map, int dt,
                  const float* img_scale, hipStream_t s);

@@ -99,6 +99,17 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
   }
 }
 
+// One Adam element update, shared by both Adam kernels so that they round identically (explicit
+// fmaf: no contraction choice is left to the compiler).  Returns the new parameter.
+DEV float adam_elem(float& m, float& v, float p, float gi, float b1, float b2, float step_size, float rbc2,
+                    float eps) {
+  const float mi = fmaf(b1, m, (1.f - b1) * gi);
+  const float vi = fmaf(b2, v, (1.f - b2) * (gi * gi));
+  m = mi;
+  v = vi;
+  return p - step_size * mi / fmaf(sqrtf(vi), rbc2, eps);
+}
+
 template <int DT>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int n, float lr,
@@ -126,12 +137,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   const float step_size = lr / bc1;
   const float rbc2 = 1.f / sqrtf(bc2);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const float gi = g[i] * coef;
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    float mi = m[i], vi = v[i];
+    const float pi = adam_elem(mi, vi, p[i], g[i] * coef, b1, b2, step_size, rbc2, eps);
     m[i] = mi;
     v[i] = vi;
-    const float pi = p[i] - step_size * mi / (sqrtf(vi) * rbc2 + eps);
     p[i] = pi;
     const int wi = w_map[i];
     if (wi >= 0) {
@@ -143,6 +152,44 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     state[0] = step;
     state[2] = norm;
+  }
+}
+
+// No-clip Adam (the DPPO preset: chief.py:17 has no clipping): no norm is needed before the
+// update, so there is no sumsq pass (the reported norm of the last step is computed when the
+// metrics are staged, once per iteration).  The step number comes from the host (eager
+// launches); block 0 mirrors it into state[0] for the device-counter path.  Graph replay keeps
+// the sumsq + adam pair, whose step counter lives on the device.
+template <int DT>
+__global__ __launch_bounds__(256) void adam_noclip_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                          float* __restrict__ m, float* __restrict__ v, int n,
+                                                          float lr, float b1, float b2, float eps, float step,
+                                                          float* __restrict__ state,
+                                                          typename Prec<DT>::T* __restrict__ wimg,
+                                                          const int* __restrict__ w_map,
+                                                          const int* __restrict__ wt_map,
+                                                          const float* __restrict__ qmul) {
+  using P = Prec<DT>;
+  const float bc1 = 1.f - powf(b1, step);
+  const float bc2 = 1.f - powf(b2, step);
+  const float step_size = lr / bc1;
+  const float rbc2 = 1.f / sqrtf(bc2);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    float mi = m[i], vi = v[i];
+    const float pi = adam_elem(mi, vi, p[i], g[i], b1, b2, step_size, rbc2, eps);
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+    const int wi = w_map[i];
+    if (wi >= 0) {
+      const typename P::T q = P::cvt(qmul ? pi * qmul[i] : pi);
+      wimg[wi] = q;
+      wimg[wt_map[i]] = q;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    state[0] = step;
+    state[1] = step;
   }
 }
 
@@ -177,9 +224,27 @@ extern "C" void launch_gae(const float* rewards, const float* values, const floa
   HIP_CHECK_LAUNCH();
 }
 
+static int g_adam_fused = 1;   // A/B switch (set_adam_fused): 0 forces the sumsq + adam pair
+extern "C" void set_adam_fused(int on) { g_adam_fused = on; }
+
 extern "C" void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, float b1, float b2,
                             float eps, float max_norm, float* state, float* norm_part, int nblk, void* wimg,
-                            const int* w_map, const int* wt_map, int dt, const float* img_scale, hipStream_t s) {
+                            const int* w_map, const int* wt_map, int dt, const float* img_scale, int host_step,
+                            hipStream_t s) {
+  if (max_norm <= 0.f && g_adam_fused && host_step > 0) {
+    const float step = (float)host_step;
+    if (dt == DT_F32)
+      hipLaunchKernelGGL(adam_noclip_kernel<DT_F32>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
+                         step, state, (float*)wimg, w_map, wt_map, img_scale);
+    else if (dt == DT_BF16)
+      hipLaunchKernelGGL(adam_noclip_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
+                         step, state, (__bf16*)wimg, w_map, wt_map, img_scale);
+    else
+      hipLaunchKernelGGL(adam_noclip_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
+                         step, state, (uint8_t*)wimg, w_map, wt_map, img_scale);
+    HIP_CHECK_LAUNCH();
+    return;
+  }
   hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, s, g, n, norm_part, state);
   if (dt == DT_F32)
     hipLaunchKernelGGL(adam_kernel<DT_F32>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,

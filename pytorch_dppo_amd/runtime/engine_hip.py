@@ -397,10 +397,13 @@ class HipEngine:
             self.grad_flat.add_(extra_grad)
         mx = float(p.max_grad_norm) if (p.max_grad_norm is not None and p.max_grad_norm > 0) else 0.0
         b1, b2 = p.adam_betas
+        # eager: the host knows the step number (one fused kernel without clipping); a captured
+        # graph must not bake it in, so graph replay reads the device counter instead
+        host_step = 0 if self.use_graphs else self.adam_step + 1
         self._launch(("adam",), lambda: self.ext.adam(
             self.model.flat.data, self.grad_flat, self.adam_m, self.adam_v, float(p.lr), float(b1), float(b2),
             float(p.adam_eps), mx, self.adam_state, self.norm_part, self.wimg, self.w_map, self.wt_map, self.dt,
-            self.no_q))
+            self.no_q, host_step))
         self.adam_step += 1
         return None
 
@@ -409,7 +412,11 @@ class HipEngine:
         into host memory by the worker without a sync (``losses_from_vector`` decodes it)."""
         if self._loss_dev is None:
             return None
-        return torch.cat([self._loss_dev.reshape(-1), self.adam_state[2:3]])
+        if self.p.max_grad_norm is not None and self.p.max_grad_norm > 0:
+            gn = self.adam_state[2:3]              # the clip pass computed it
+        else:                                      # no-clip Adam skips the norm: last step's gradient
+            gn = torch.linalg.vector_norm(self.grad_flat).reshape(1)
+        return torch.cat([self._loss_dev.reshape(-1), gn])
 
     @staticmethod
     def losses_from_vector(v) -> Dict[str, float]:

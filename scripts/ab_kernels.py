@@ -1,0 +1,70 @@
+"""In-process A/B timing of kernel variants on the bench configuration (diagnostics).
+
+Interleaved rounds in ONE process (cdna_hip_programming.md §5.4 rule 24):
+  adam:  fused no-clip Adam (1 launch) vs sumsq + Adam (2 launches)
+  wgrad: LDS-DMA staged vs register-streamed (inside eng.grad)
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from pytorch_dppo_amd.config import dppo_preset  # noqa: E402
+from pytorch_dppo_amd.envs import get_spec, make_vec_env  # noqa: E402
+from pytorch_dppo_amd.models.actor_critic import ActorCritic  # noqa: E402
+from pytorch_dppo_amd.runtime.engine_hip import HipEngine  # noqa: E402
+from pytorch_dppo_amd.utils.obs_stats import RunningObsStats  # noqa: E402
+
+
+def timed(fn, reps=10):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    dtype = sys.argv[1] if len(sys.argv) > 1 else "bf16"
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536, batch_size=65536,
+                    dtype=dtype, use_graphs=False)
+    spec = get_spec(p.env_name)
+    torch.manual_seed(0)
+    model = ActorCritic(spec.obs_dim, spec.act_dim).to(dev)
+    env = make_vec_env(spec, p.num_envs, device=dev)
+    stats = RunningObsStats(spec.obs_dim, dev)
+    eng = HipEngine(p, model, env, stats, dev, 0)
+    stats.observes(env.observe())
+    eng.rollout()
+    eng.values()
+    eng.gae()
+    eng.begin_update()
+    ext = eng.ext
+    eng.grad(None)
+    arms = {
+        "adam_fused": (lambda: ext.set_adam_fused(1), eng.apply),
+        "adam_sumsq_pair": (lambda: ext.set_adam_fused(0), eng.apply),
+        "grad_wgrad_lds_dma": (lambda: ext.set_wgrad_impl(0), lambda: eng.grad(None)),
+        "grad_wgrad_register": (lambda: ext.set_wgrad_impl(1), lambda: eng.grad(None)),
+        "rollout": (lambda: None, eng.rollout),
+        "values": (lambda: None, eng.values),
+    }
+    res = {k: [] for k in arms}
+    for _ in range(5):
+        for k, (setup, fn) in arms.items():
+            setup()
+            res[k].append(timed(fn))
+    ext.set_adam_fused(1)
+    ext.set_wgrad_impl(0)
+    print(json.dumps({k: {"median_us": sorted(v)[len(v) // 2], "min_us": min(v)} for k, v in res.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

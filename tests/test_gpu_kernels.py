@@ -285,6 +285,10 @@ def test_adam_kernel_matches_oracle(max_norm):
         g = torch.randn(n, device=DEV) * 0.3
         eng.grad_flat.copy_(g)
         eng.apply()
+        # step counter committed by the last block; the clip path also reports the pre-clip norm
+        assert float(eng.adam_state[0]) == step and float(eng.adam_state[3]) == 0.0
+        if max_norm:
+            assert abs(float(eng.adam_state[2]) - g.norm().item()) <= 1e-4 * g.norm().item()
         gr = g.clone()
         if max_norm:
             oracle.clip_grad_norm_(gr, max_norm)
