@@ -18,7 +18,7 @@ run() {  # name timeout cmd...
 STEPS=${STEPS:-"tests smoke bench"}
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -x -p no:cacheprovider; rc=$?; [ $rc -le 1 ] || exit $rc ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --timeout 120 --timeout-method thread; rc=$?; [ $rc -le 1 ] || exit $rc ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 600 python bench.py --steps ${BSTEPS:-5} --warmup 2 --verbose || exit $? ;;
     prof)  cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
