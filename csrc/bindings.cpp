@@ -17,6 +17,18 @@ hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 // training runs (the results of an ablated call are not a gradient)
 int g_train_ablate = 0;
 void set_train_ablation(int64_t mask) { g_train_ablate = (int)mask; }
+// diagnostics only: phase-timeline stamps of mlp_train (scripts/phase_timeline.py)
+unsigned long long* g_tstamp = nullptr;
+int g_tstamp_every = 1;
+int64_t g_tstamp_numel = 0;
+void set_train_tstamp(torch::Tensor buf, int64_t every) {
+  if (!buf.defined() || buf.numel() == 0) { g_tstamp = nullptr; return; }
+  g_tstamp_numel = buf.numel();
+  TORCH_CHECK(buf.scalar_type() == at::kLong && buf.is_cuda() && buf.is_contiguous(), "int64 device buffer");
+  TORCH_CHECK(every >= 1, "every");
+  g_tstamp = reinterpret_cast<unsigned long long*>(buf.data_ptr<int64_t>());
+  g_tstamp_every = (int)every;
+}
 int g_wgrad_impl = 0;   // 0: LDS-DMA staged, 1: register-streamed (A/B diagnostics)
 void set_wgrad_impl(int64_t impl) {
   TORCH_CHECK(impl == 0 || impl == 1, "wgrad impl: 0 LDS-DMA, 1 register");
@@ -225,7 +237,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   check(mu_prev, "mu_prev", at::kFloat, nrows * A);
   check(v_prev, "v_prev", at::kFloat, nrows);
   check(log_std_old, "log_std_old", at::kFloat, A);
-  const int ROWS = train_rows_for((int)dt);
+  const int ROWS = mlp_train_rows((int)dt, a);
   TORCH_CHECK(train_lds_bytes_impl((int)dt, L, A) <= 160 * 1024, "mlp_train tile does not fit LDS");
   const int64_t Mpad = ((M + ROWS - 1) / ROWS) * ROWS;
   TORCH_CHECK(ldT >= Mpad && ldT % 32 == 0, "ldT must cover M padded to the row tile and be a multiple of 32");
@@ -259,6 +271,12 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   TORCH_CHECK(!xT_ready || (a.idx == nullptr && row0 == 0 && ldT == M), "xT_ready needs a full-batch call");
   a.xT_ready = xT_ready ? 1 : 0;
   a.ablate = g_train_ablate;
+  if (g_tstamp != nullptr) {
+    const int64_t nw = ROWS == 64 ? 8 : 4;
+    TORCH_CHECK(g_tstamp_numel >= ((nblk + g_tstamp_every - 1) / g_tstamp_every) * nw * 16, "tstamp buffer too small");
+    a.tstamp = g_tstamp;
+    a.tstamp_every = g_tstamp_every;
+  }
   a.part = part.data_ptr<float>();
   launch_mlp_train((int)dt, a, cur_stream());
 }
@@ -267,7 +285,18 @@ int64_t train_lds_bytes(int64_t dt, std::vector<int64_t> layout, int64_t A) {
   return train_lds_bytes_impl((int)dt, parse_layout(layout), A);
 }
 
-int64_t train_rows(int64_t dt) { return train_rows_for((int)dt); }
+int64_t train_rows(int64_t dt, std::vector<int64_t> layout, int64_t A) {
+  const Layout L = parse_layout(layout);
+  MlpArgs a{};
+  for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
+  a.A = (int)A;
+  return mlp_train_rows((int)dt, a);
+}
+
+void set_mlp_rows(int64_t rows) {
+  TORCH_CHECK(rows == 0 || rows == 16 || rows == 32 || rows == 64, "rows: 0 (auto), 16, 32 or 64");
+  set_mlp_rows_override((int)rows);
+}
 
 void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor> xT, std::vector<int64_t> g_rows,
            std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab) {
@@ -400,6 +429,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_train", &mlp_train);
   m.def("train_lds_bytes", &train_lds_bytes);
   m.def("train_rows", &train_rows);
+  m.def("set_mlp_rows", &set_mlp_rows);
+  m.def("set_train_tstamp", &set_train_tstamp);
   m.def("wgrad", &wgrad);
   m.def("grad_gather", &grad_gather);
   m.def("gae", &gae);

@@ -85,6 +85,10 @@ struct MlpArgs {
                           // transposed stores, bit1 skip v_fc1, bit2 skip dgrad chain, bit3 skip loss
   float* part;            // [nblk][NPART] per-workgroup partial sums (loss terms, dlog_std)
   int npart;
+  // DIAGNOSTIC ONLY (scripts/phase_timeline.py; null in every real run): per-wave s_memtime
+  // stamps at the phase boundaries of every tstamp_every-th workgroup, [blk][NW][16]
+  unsigned long long* tstamp;
+  int tstamp_every;
 };
 
 struct WgradTask {
@@ -109,6 +113,8 @@ void launch_rollout(int dt, const RolloutArgs& a, int rows, hipStream_t s);
 void launch_mlp_value(int dt, const MlpArgs& a, hipStream_t s);
 void launch_mlp_train(int dt, const MlpArgs& a, hipStream_t s);
 size_t mlp_train_lds_bytes(int dt, const MlpArgs& a);
+int mlp_train_rows(int dt, const MlpArgs& a);   // row tile the launcher will use (LDS-fit)
+void set_mlp_rows_override(int rows);           // 0 auto; 16/32/64 force (A/B diagnostics)
 void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
 void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int chunk_stride,
                         const float* part, int nblk, int npart, int A, float scale, float* grad,
@@ -126,10 +132,6 @@ void launch_obs_reduce(const float* part, int nblk, int O, double* s12, hipStrea
 void launch_obs_merge(const double* s12, int O, double count, double n_a, const float* shift, double* mean,
                       double* m2, float* mean_f32, float* inv_std, double var_floor, hipStream_t s);
 }
-
-// rows per workgroup of mlp_train_kernel: the fp32 tile set does not fit 160 KiB of LDS at 32
-// rows for the Humanoid value head, so fp32 uses 16-row tiles (host side must agree).
-static inline constexpr int train_rows_for(int dt) { return dt == 0 ? 16 : 32; }
 
 // output tile (square) of one wgrad task; operand buffers are padded to multiples of it
 #define WGRAD_TILE 128

@@ -39,7 +39,10 @@ DEV float act_tanh(float x) {
   }
 }
 
-template <int DT> struct KChunk { static constexpr int KC = (DT == DT_F32) ? 2 : 4; };
+// k-steps per prefetch chunk.  With 2+ row blocks (32/64-row tiles) the A fragments of a chunk
+// multiply, and the cross-barrier BPre sets live alongside, so the chunk is 2 k-steps to keep
+// two register sets inside the 2-waves/SIMD VGPR budget (4 for the 16-row rollout tile).
+template <int DT, int RB> struct KChunk { static constexpr int KC = (DT == DT_F32) ? 2 : (RB >= 2 ? 2 : 4); };
 
 template <int DT>
 DEV void store4_T(typename Prec<DT>::T* dst, float v0, float v1, float v2, float v3) {
@@ -55,21 +58,50 @@ DEV void store4_T(typename Prec<DT>::T* dst, float v0, float v1, float v2, float
   }
 }
 
-template <int DT, int ROWS, int NW, int EPI, typename OutT>
+// B fragments of a wave's FIRST (tile pair, k-chunk) step of one layer_gemm call, loaded ahead
+// of time by layer_prefetch: weights do not depend on the previous layer, so their L2 latency
+// can overlap a barrier wait or another phase instead of stalling the layer's first MFMA.
+// (one type per k-chunk size, so 32- and 64-row calls with the same KC share a prefetch set)
+template <int DT, int KC> struct BPreK {
+  typename Prec<DT>::Frag b0[KC], b1[KC];
+};
+template <int DT, int RB> using BPre = BPreK<DT, KChunk<DT, RB>::KC>;
+
+template <int DT, int ROWS, int NW>
+DEV void layer_prefetch(BPre<DT, ROWS / 16>& pre, const typename Prec<DT>::T* __restrict__ B, int kdim,
+                        int n_real, int wave, int lane, int wrot = 0) {
+  using P = Prec<DT>;
+  constexpr int KC = KChunk<DT, ROWS / 16>::KC;
+  wave = __builtin_amdgcn_readfirstlane((wave + wrot) & (NW - 1));
+  const int ksteps = kdim >> 5;
+  const int first_pair = wave * 2;
+  if (first_pair >= ((n_real + 15) >> 4)) return;
+#pragma unroll
+  for (int j = 0; j < KC; ++j) {
+    const typename P::T* p0 = B + fm_frag(first_pair, min(j, ksteps - 1), kdim, lane);
+    pre.b0[j] = P::load(p0);
+    pre.b1[j] = P::load(p0 + (size_t)ksteps * 512);
+  }
+}
+
+template <int DT, int ROWS, int NW, int EPI, bool PRE = false, typename OutT>
 DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdim,
                     const typename Prec<DT>::T* __restrict__ B, int n_real,
                     OutT* out, int ldo, float scale, int wave, int lane,
-                    typename Prec<DT>::T* __restrict__ outT = nullptr, int ldT = 0, int m0 = 0) {
+                    typename Prec<DT>::T* __restrict__ outT = nullptr, int ldT = 0, int m0 = 0, int wrot = 0,
+                    const BPre<DT, ROWS / 16>* pre = nullptr) {
   using P = Prec<DT>;
   using T = typename P::T;
   using Frag = typename P::Frag;
   constexpr int RB = ROWS / 16;
-  constexpr int KC = KChunk<DT>::KC;
+  constexpr int KC = KChunk<DT, RB>::KC;
   constexpr int NT2 = 2;
   // every quantity that steers control flow is wave-uniform and must live in SGPRs: with a
   // VGPR `wave` the compiler turns the step loop into EXEC-masked regions and waits for ALL
   // outstanding loads (vmcnt(0)) at each merge — the prefetch below would never overlap
-  wave = __builtin_amdgcn_readfirstlane(wave);
+  // wrot rotates the wave -> tile-pair map so two back-to-back narrow layers (policy and
+  // value head, 4 pairs each) land on disjoint waves when NW = 8
+  wave = __builtin_amdgcn_readfirstlane((wave + wrot) & (NW - 1));
   const int ksteps = kdim >> 5;
   const int nchunks = (ksteps + KC - 1) / KC;
   const int ntiles = (n_real + 15) >> 4;
@@ -95,6 +127,14 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
       const T* p0 = B + fm_frag(nt, ks, kdim, lane);
       d.b0[j] = P::load(p0);
       d.b1[j] = P::load(p0 + (size_t)ksteps * 512);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) d.a[j][rb] = P::load(ap + rb * 16 * lda + ks * 32);
+    }
+  };
+  auto load_a0 = [&](Buf& d) {   // A fragments of chunk 0 (the B half came from layer_prefetch)
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const int ks = min(j, ksteps - 1);
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) d.a[j][rb] = P::load(ap + rb * 16 * lda + ks * 32);
     }
@@ -171,7 +211,16 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
   };
   Buf buf0, buf1;
   int nt0 = first_pair, kc = 0;
-  load(buf0, nt0, 0);
+  if constexpr (PRE) {
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      buf0.b0[j] = pre->b0[j];
+      buf0.b1[j] = pre->b1[j];
+    }
+    load_a0(buf0);
+  } else {
+    load(buf0, nt0, 0);
+  }
   // One step: prefetch step s+1 into `nx` (unconditionally: past the end it re-loads valid
   // addresses, so the number of loads in flight is the same on every path and the compiler's
   // waitcnt is exact), compute step s from `cur`, epilogue at the end of a pair.
@@ -210,14 +259,25 @@ struct LdsCarve {
   }
 };
 
-// Fill rows x ld of a padded activation tile: column `one_col` = 1, the rest 0.  Threads own
-// columns; rows are an outer loop (no per-element integer division).
+// Columns [c0, ld) of a rows x ld activation tile: column c0 = 1 (the constant bias input of
+// the next layer), the rest 0.  Columns < c0 are NOT touched: the producing layer's epilogue
+// writes every row of them (layer_gemm stores all ROWS rows of each column c < n_real).
 template <int DT>
-DEV void preset_tile(typename Prec<DT>::T* H, int ld, int rows, int one_col, int tid, int nthreads) {
+DEV void preset_pad(typename Prec<DT>::T* H, int ld, int rows, int c0, int tid, int nthreads) {
   using P = Prec<DT>;
   const typename P::T zero = P::cvt(0.f), one = P::cvt(1.f);
-  for (int c = tid; c < ld; c += nthreads) {
-    const typename P::T v = (c == one_col) ? one : zero;
-    for (int r = 0; r < rows; ++r) H[r * ld + c] = v;
+  for (int r = tid; r < rows; r += nthreads) {
+    typename P::T* h = H + r * ld;
+    h[c0] = one;
+    for (int c = c0 + 1; c < ld; ++c) h[c] = zero;
   }
+}
+
+// Zero a whole rows x ld tile with 16-byte stores (ld * sizeof(T) is a multiple of 16 for
+// every Lds<DT>::stride of a P32 width, and LdsCarve keeps tile bases 16-byte aligned).
+template <int DT>
+DEV void zero_tile(typename Prec<DT>::T* H, int ld, int rows, int tid, int nthreads) {
+  const int n16 = rows * ld * Prec<DT>::BYTES / 16;
+  uint4* h = reinterpret_cast<uint4*>(H);
+  for (int i = tid; i < n16; i += nthreads) h[i] = make_uint4(0, 0, 0, 0);
 }

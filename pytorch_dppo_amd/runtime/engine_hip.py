@@ -17,6 +17,7 @@ in the MFMA operand precision (fp32 / bf16), the bias folded into column K.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional
 
 import torch
@@ -31,6 +32,7 @@ STORAGE = {0: torch.float32, 1: torch.bfloat16, 2: torch.uint8}
 NPART_FIXED = 8
 WT = 128            # wgrad output tile (csrc/kernels.h WGRAD_TILE)
 ROLL_ROWS = 16
+WGRAD_TARGET_WGS = 256   # A/B (scripts/ab_kernels.py): 256 <= 512 <= 1024 us per grad step
 
 
 def _r(x: int, m: int) -> int:
@@ -104,10 +106,13 @@ class HipEngine:
         # ---- update geometry ----
         self.mb = params.minibatch_rows()
         self.ldT = _r(self.mb, 64)      # wgrad consumes k-steps in pairs (csrc/wgrad.hip)
-        self.train_rows = int(self.ext.train_rows(self.dt))
-        self.ntrain_blk = self.ldT // self.train_rows
         self.npart = NPART_FIXED + A
-        self.part = torch.zeros(self.ntrain_blk, self.npart, **f32)
+        # per-workgroup partials, sized for the smallest row tile (16) so a tile change
+        # (set_mlp_rows, A/B diagnostics) never outgrows it
+        self.part = torch.zeros(self.ldT // 16, self.npart, **f32)
+        if os.environ.get("DPPO_MLP_ROWS"):     # diagnostics: force the fused-kernel row tile
+            self.ext.set_mlp_rows(int(os.environ["DPPO_MLP_ROWS"]))
+        self.sync_tile()
         # transposed operand buffers (feature-major), heights padded to the wgrad tile
         lp1, lp2, lmu, lv1, lv2, lv = ls
         x_rows = [lp1.d_in, lp2.d_in, lmu.d_in, lv1.d_in, lv2.d_in, lv.d_in]
@@ -164,7 +169,13 @@ class HipEngine:
         self.params_changed()
 
     # ------------------------------------------------------------------------------------------
-    def _build_wgrad_plan(self, model: ActorCritic) -> None:
+    def _build_wgrad_plan(self, model: ActorCritic, target_wgs: Optional[int] = None) -> None:
+        """Task list of the grouped split-K wgrad launch: (layer, 128x128 tile, batch chunk).
+        ``target_wgs`` workgroups (default WGRAD_TARGET_WGS, env DPPO_WGRAD_WGS) set the
+        number of batch chunks: more chunks = more parallelism but more fp32 partial slabs
+        for grad_gather to sum."""
+        if target_wgs is None:
+            target_wgs = int(os.environ.get("DPPO_WGRAD_WGS", WGRAD_TARGET_WGS))
         ls = self.L.layers
         tiles = []  # (layer, n0, k0)
         for li, l in enumerate(ls):
@@ -173,7 +184,7 @@ class HipEngine:
                     tiles.append((li, n0, k0))
         ntiles = len(tiles)
         max_chunks = max(1, self.ldT // 256)
-        want = -(-1024 // ntiles)                 # >= ~1024 workgroups in flight
+        want = -(-target_wgs // ntiles)           # >= ~target_wgs workgroups in flight
         want = -(-want // 8) * 8                  # whole chunks per XCD (8 XCDs)
         nchunks = max(1, min(max_chunks, want))
         mc = _r(-(-self.ldT // nchunks), 64)   # even number of 32-row k-steps per task
@@ -222,6 +233,12 @@ class HipEngine:
         return base + (n % WT) * WT + (k % WT)
 
     # ------------------------------------------------------------------------------------------
+    def sync_tile(self) -> None:
+        """Row tile of the fused update kernel (64 rows when the layer set fits LDS, else 32;
+        16 at fp32) and the partial-sum rows it produces; re-query after ext.set_mlp_rows."""
+        self.train_rows = int(self.ext.train_rows(self.dt, self.layout, self.A))
+        self.ntrain_blk = self.ldT // self.train_rows
+
     def params_changed(self) -> None:
         """re-pack the weight images from the fp32 master (after init / load / broadcast)."""
         self.ext.pack(self.model.flat.data, self.wimg, self.w_map, self.wt_map, self.dt, self.no_q)

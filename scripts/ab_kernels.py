@@ -3,6 +3,7 @@
 Interleaved rounds in ONE process (cdna_hip_programming.md §5.4 rule 24):
   adam:  fused no-clip Adam (1 launch) vs sumsq + Adam (2 launches)
   wgrad: LDS-DMA staged vs register-streamed (inside eng.grad)
+  rows:  64-row / 8-wave vs 32-row / 4-wave tiles of the fused update and value kernels
 """
 import json
 import os
@@ -48,14 +49,28 @@ def main():
     eng.begin_update()
     ext = eng.ext
     eng.grad(None)
+
+    def rows(n):
+        ext.set_mlp_rows(n)
+        eng.sync_tile()
+
+    def knobs(adam=1, wgrad=0, r=0):   # every arm sets every knob (no state leaks between arms)
+        return lambda: (ext.set_adam_fused(adam), ext.set_wgrad_impl(wgrad), rows(r))
+
     arms = {
-        "adam_fused": (lambda: ext.set_adam_fused(1), eng.apply),
-        "adam_sumsq_pair": (lambda: ext.set_adam_fused(0), eng.apply),
-        "grad_wgrad_lds_dma": (lambda: ext.set_wgrad_impl(0), lambda: eng.grad(None)),
-        "grad_wgrad_register": (lambda: ext.set_wgrad_impl(1), lambda: eng.grad(None)),
-        "rollout": (lambda: None, eng.rollout),
-        "values": (lambda: None, eng.values),
+        "adam_fused": (knobs(adam=1), eng.apply),
+        "adam_sumsq_pair": (knobs(adam=0), eng.apply),
+        "grad_wgrad_lds_dma": (knobs(wgrad=0), lambda: eng.grad(None)),
+        "grad_wgrad_register": (knobs(wgrad=1), lambda: eng.grad(None)),
+        "rollout": (knobs(), eng.rollout),
+        "values_rows64": (knobs(r=64), eng.values),
+        "values_rows32": (knobs(r=32), eng.values),
+        "grad_rows64": (knobs(r=64), lambda: eng.grad(None)),
+        "grad_rows32": (knobs(r=32), lambda: eng.grad(None)),
     }
+    for t in (1024, 512, 256):
+        arms[f"grad_wgrad_wgs{t}"] = ((lambda t=t: (knobs()(), eng._build_wgrad_plan(model, t))),
+                                      lambda: eng.grad(None))
     res = {k: [] for k in arms}
     for _ in range(5):
         for k, (setup, fn) in arms.items():
@@ -63,6 +78,8 @@ def main():
             res[k].append(timed(fn))
     ext.set_adam_fused(1)
     ext.set_wgrad_impl(0)
+    rows(0)
+    eng._build_wgrad_plan(model)
     print(json.dumps({k: {"median_us": sorted(v)[len(v) // 2], "min_us": min(v)} for k, v in res.items()}, indent=1))
 
 

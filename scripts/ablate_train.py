@@ -41,9 +41,14 @@ def main():
     eng.gae()
     eng.begin_update()
     ext = eng.ext
-    res = {k: [] for k in VARIANTS}
+    rows_list = [int(r) for r in os.environ.get("ABLATE_ROWS", "64,32").split(",")]
+    res = {f"{k}@{r}": [] for r in rows_list for k in VARIANTS}
     for rnd in range(6):
-        for name, (mask, impl) in VARIANTS.items():
+        for key in res:
+            name, rows = key.split("@")
+            mask, impl = VARIANTS[name]
+            ext.set_mlp_rows(int(rows))
+            eng.sync_tile()
             ext.set_train_ablation(mask)
             ext.set_wgrad_impl(impl)
             for _ in range(2):
@@ -54,8 +59,9 @@ def main():
                 eng.grad(None)
             e.record()
             torch.cuda.synchronize()
-            res[name].append(s.elapsed_time(e) / 5 * 1e3)
+            res[key].append(s.elapsed_time(e) / 5 * 1e3)
     ext.set_train_ablation(0)
+    ext.set_mlp_rows(0)
     ext.set_wgrad_impl(0)
     out = {k: {"median_us": sorted(v)[len(v) // 2], "min_us": min(v)} for k, v in res.items()}
     print(json.dumps(out, indent=1))

@@ -1,0 +1,73 @@
+"""Per-phase cycle timeline of the fused update kernel (diagnostics).
+
+Lane 0 of every wave of every EVERY-th workgroup stamps s_memtime (shader clock) at the phase
+boundaries of mlp_train_kernel (csrc/mlp.hip STAMP(i)); this prints the median cycles per
+phase over the sampled workgroups, for each row tile.  Bench configuration (Humanoid dims,
+65,536-row full batch).
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from pytorch_dppo_amd.config import dppo_preset  # noqa: E402
+from pytorch_dppo_amd.envs import get_spec, make_vec_env  # noqa: E402
+from pytorch_dppo_amd.models.actor_critic import ActorCritic  # noqa: E402
+from pytorch_dppo_amd.runtime.engine_hip import HipEngine  # noqa: E402
+from pytorch_dppo_amd.utils.obs_stats import RunningObsStats  # noqa: E402
+
+PHASES = ["load_x+preset", "fc1 (p,v) own", "fc1 barrier wait", "preset", "fc2 own", "fc2 barrier wait",
+          "fc3 + sync", "loss + sync", "partials+dY^T stores", "dgrad fc3 own", "dgrad fc3 barrier",
+          "dgrad fc2 own"]
+EVERY = 16
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    dtype = sys.argv[1] if len(sys.argv) > 1 else "bf16"
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536, batch_size=65536,
+                    dtype=dtype, use_graphs=False)
+    spec = get_spec(p.env_name)
+    torch.manual_seed(0)
+    model = ActorCritic(spec.obs_dim, spec.act_dim).to(dev)
+    env = make_vec_env(spec, p.num_envs, device=dev)
+    stats = RunningObsStats(spec.obs_dim, dev)
+    eng = HipEngine(p, model, env, stats, dev, 0)
+    stats.observes(env.observe())
+    eng.rollout()
+    eng.values()
+    eng.gae()
+    eng.begin_update()
+    ext = eng.ext
+    out = {}
+    for rows in [int(r) for r in os.environ.get("TIMELINE_ROWS", "64,32").split(",")]:
+        ext.set_mlp_rows(rows)
+        eng.sync_tile()
+        nw = 8 if rows == 64 else 4
+        nblk = eng.ldT // rows
+        buf = torch.zeros(((nblk + EVERY - 1) // EVERY) * nw * 16, dtype=torch.int64, device=dev)
+        for _ in range(3):
+            eng.grad(None)
+        ext.set_train_tstamp(buf, EVERY)
+        eng.grad(None)
+        torch.cuda.synchronize()
+        ext.set_train_tstamp(torch.empty(0, dtype=torch.int64, device=dev), 1)
+        t = buf.view(-1, nw, 16).cpu().double()
+        d = t[:, :, 1:13] - t[:, :, 0:12]              # [blk][wave][phase]
+        tot = (t[:, :, 12] - t[:, :, 0])
+        res = {"rows": rows, "sampled_blocks": t.shape[0],
+               "total_cycles_median": float(tot.median()),
+               "phases_median_cycles(max over waves)": {ph: float(d[:, :, i].max(dim=1).values.median())
+                                                        for i, ph in enumerate(PHASES)},
+               "phases_median_cycles(mean over waves)": {ph: float(d[:, :, i].mean(dim=1).median())
+                                                         for i, ph in enumerate(PHASES)}}
+        out[f"rows{rows}"] = res
+    ext.set_mlp_rows(0)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -218,6 +218,34 @@ def test_fused_loss_backward_matches_autograd(env_name, dtype, value_loss, conv,
     assert abs(ll["loss_value"] - out["loss_value"].item()) < max(5e-3, 50 * tol) * (1 + abs(out["loss_value"].item()))
 
 
+@pytest.mark.parametrize("rows", [32, 64])
+@pytest.mark.parametrize("env_name,mb", [("Humanoid-v2", 200), ("HalfCheetah-v2", 320)])
+def test_fused_loss_backward_row_tiles(rows, env_name, mb):
+    """bf16 fused update at both row tiles (64 rows / 8 waves and 32 rows / 4 waves), with a
+    ragged last tile, vs autograd; and the value kernel at both tiles."""
+    ext = _ext()
+    p = ppo_preset(device="gpu", env_name=env_name, num_envs=64, exploration_size=64 * 8,
+                   batch_size=mb, dtype="bf16", ent_coeff=0.01)
+    ext.set_mlp_rows(rows)
+    try:
+        eng, model, _, _ = _engine(p)
+        assert eng.train_rows == rows
+        xq = _fill_buffer(eng, model)
+        idx = torch.randperm(eng.N, generator=torch.Generator().manual_seed(7))[:mb]
+        eng.begin_update()
+        eng.grad(idx)
+        g_ref, _ = _torch_grad(model, p, xq, eng, idx.to(DEV))
+        rel = (eng.grad_flat - g_ref).norm().item() / (g_ref.norm().item() + 1e-12)
+        assert rel < 6e-2, rel
+        eng.values()
+        with torch.no_grad():
+            _, _, v = model(eng.x_buf[:, :model.num_inputs].float())
+        err = (eng.values_buf - v.reshape(-1)).abs().max().item()
+        assert err / (v.abs().max().item() + 1e-3) < 3e-2, err
+    finally:
+        ext.set_mlp_rows(0)
+
+
 def test_rollout_written_xT_equals_kernel_written_xT():
     """full-batch: the x^T operand the rollout emits == the one mlp_train would transpose."""
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 4,
