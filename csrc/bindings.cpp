@@ -348,10 +348,14 @@ void grad_gather(torch::Tensor slab, torch::Tensor src_off, int64_t nchunks, int
                      (int)n, loss_out.data_ptr<float>(), cur_stream());
 }
 
-void obs_reduce(torch::Tensor part, int64_t nblk, int64_t O, torch::Tensor s12) {
+void obs_reduce(torch::Tensor part, int64_t nblk, int64_t O, torch::Tensor s12, torch::Tensor epstat,
+                torch::Tensor ep) {
   check(part, "part", at::kFloat, nblk * 2 * O);
   check(s12, "s12", at::kDouble, 2 * O);
-  launch_obs_reduce(part.data_ptr<float>(), (int)nblk, (int)O, s12.data_ptr<double>(), cur_stream());
+  check(epstat, "epstat", at::kFloat, nblk * 2);
+  check(ep, "ep", at::kDouble, 2);
+  launch_obs_reduce(part.data_ptr<float>(), (int)nblk, (int)O, s12.data_ptr<double>(), epstat.data_ptr<float>(),
+                    ep.data_ptr<double>(), cur_stream());
 }
 
 void obs_merge(torch::Tensor s12, double count, double n_a, torch::Tensor shift, torch::Tensor mean, torch::Tensor m2,
@@ -430,6 +434,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("train_lds_bytes", &train_lds_bytes);
   m.def("train_rows", &train_rows);
   m.def("set_mlp_rows", &set_mlp_rows);
+  m.def("set_rollout_waves", [](int64_t nw) {
+    TORCH_CHECK(nw == 4 || nw == 8, "rollout waves: 4 or 8");
+    set_rollout_waves((int)nw);
+  });
   m.def("set_train_tstamp", &set_train_tstamp);
   m.def("wgrad", &wgrad);
   m.def("grad_gather", &grad_gather);

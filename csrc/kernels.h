@@ -110,6 +110,7 @@ struct WgradArgs {
 
 extern "C" {
 void launch_rollout(int dt, const RolloutArgs& a, int rows, hipStream_t s);
+void set_rollout_waves(int nw);                 // 4 or 8 waves per rollout workgroup (A/B)
 void launch_mlp_value(int dt, const MlpArgs& a, hipStream_t s);
 void launch_mlp_train(int dt, const MlpArgs& a, hipStream_t s);
 size_t mlp_train_lds_bytes(int dt, const MlpArgs& a);
@@ -128,7 +129,8 @@ void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, 
                  hipStream_t s);
 void launch_pack(const float* p, int n, void* wimg, const int* w_map, const int* wt_map, int dt,
                  const float* img_scale, hipStream_t s);
-void launch_obs_reduce(const float* part, int nblk, int O, double* s12, hipStream_t s);
+void launch_obs_reduce(const float* part, int nblk, int O, double* s12, const float* epstat, double* ep,
+                       hipStream_t s);
 void launch_obs_merge(const double* s12, int O, double count, double n_a, const float* shift, double* mean,
                       double* m2, float* mean_f32, float* inv_std, double var_floor, hipStream_t s);
 }

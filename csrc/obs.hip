@@ -12,23 +12,47 @@
 
 namespace {
 
+// One workgroup per 64 consecutive (q, d) columns: lane = column (coalesced 256-B rows), the
+// 4 waves split the blocks (b = wave, wave + 4, ...), then a fixed-order LDS combine —
+// deterministic, and 64x more loads in flight than one thread per column walking all blocks.
+// The last workgroup also sums the per-block episode stats [nblk][2] -> ep[2] (fp64).
 __global__ __launch_bounds__(256) void obs_reduce_kernel(const float* __restrict__ part, int nblk, int O,
-                                                         double* __restrict__ s12) {
-  const int i = blockIdx.x * 256 + threadIdx.x;  // i in [0, 2*O): (q, d) = (i / O, i % O)
-  if (i >= 2 * O) return;
-  const int q = i / O, d = i - q * O;
-  const float* p = part + (size_t)q * O + d;
-  const size_t stride = (size_t)2 * O;
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  int b = 0;
-  for (; b + 4 <= nblk; b += 4) {
-    a0 += p[(size_t)(b + 0) * stride];
-    a1 += p[(size_t)(b + 1) * stride];
-    a2 += p[(size_t)(b + 2) * stride];
-    a3 += p[(size_t)(b + 3) * stride];
+                                                         double* __restrict__ s12, const float* __restrict__ epstat,
+                                                         double* __restrict__ ep) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ncol = 2 * O;
+  const int ngrp = (ncol + 63) / 64;
+  if ((int)blockIdx.x == ngrp) {   // episode stats
+    if (wave == 0) {
+      double a = 0.0, c = 0.0;
+      for (int b = lane; b < nblk; b += 64) { a += epstat[2 * b]; c += epstat[2 * b + 1]; }
+      red[0][lane] = a;
+      red[1][lane] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      double t = 0.0;
+      for (int l = 0; l < 64; ++l) t += red[threadIdx.x][l];
+      ep[threadIdx.x] = t;
+    }
+    return;
   }
-  for (; b < nblk; ++b) a0 += p[(size_t)b * stride];
-  s12[i] = (a0 + a1) + (a2 + a3);
+  const int i = blockIdx.x * 64 + lane;       // column i = q * O + d of the [2][O] partial
+  double a0 = 0.0, a1 = 0.0;
+  if (i < ncol) {
+    const float* p = part + i;
+    const size_t stride = (size_t)ncol;
+    int b = wave;
+    for (; b + 4 < nblk; b += 8) {
+      a0 += p[(size_t)b * stride];
+      a1 += p[(size_t)(b + 4) * stride];
+    }
+    for (; b < nblk; b += 4) a0 += p[(size_t)b * stride];
+  }
+  red[wave][lane] = a0 + a1;
+  __syncthreads();
+  if (wave == 0 && i < ncol) s12[i] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 __global__ __launch_bounds__(256) void obs_merge_kernel(const double* __restrict__ s12, int O, double count,
@@ -57,8 +81,9 @@ __global__ __launch_bounds__(256) void obs_merge_kernel(const double* __restrict
 
 }  // namespace
 
-extern "C" void launch_obs_reduce(const float* part, int nblk, int O, double* s12, hipStream_t s) {
-  hipLaunchKernelGGL(obs_reduce_kernel, dim3((2 * O + 255) / 256), dim3(256), 0, s, part, nblk, O, s12);
+extern "C" void launch_obs_reduce(const float* part, int nblk, int O, double* s12, const float* epstat, double* ep,
+                                  hipStream_t s) {
+  hipLaunchKernelGGL(obs_reduce_kernel, dim3((2 * O + 63) / 64 + 1), dim3(256), 0, s, part, nblk, O, s12, epstat, ep);
   HIP_CHECK_LAUNCH();
 }
 

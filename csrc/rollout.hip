@@ -28,11 +28,13 @@ DEV float env_obs(int kind, const float* st, int S, int r, int d) {
   return st[r * S + d];
 }
 
-template <int DT, int ROWS>
-__global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
+// NW waves per workgroup: a 16-env tile is one workgroup per CU at E = 4096, so the 8-wave
+// form (2 waves per SIMD) doubles the threads of the VALU-heavy observe / sample / env phases
+// and gives the SIMDs a second wave to hide latency with; the MFMA layers use the first waves.
+template <int DT, int ROWS, int NW>
+__global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   using P = Prec<DT>;
   using T = typename P::T;
-  constexpr int NW = 4;
   constexpr int NTHR = 64 * NW;
   static_assert(ROWS % 4 == 0 && NTHR % ROWS == 0 && (NTHR / ROWS) <= 64, "rollout tiling");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -70,19 +72,19 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
   const float sc3 = a.qscale ? a.qscale[2] : a.s3;
 
   // ---- load state, zero the padded activation tiles (pad columns stay constant) ----
-  for (int i = tid; i < ROWS * S; i += 256) {
+  for (int i = tid; i < ROWS * S; i += NTHR) {
     int r = i / S, d = i - r * S;
     st[i] = (r < nvalid) ? a.state[(size_t)(e0 + r) * S + d] : 0.f;
   }
-  for (int i = tid; i < ROWS * ld2; i += 256) {
+  for (int i = tid; i < ROWS * ld2; i += NTHR) {
     int c = i % ld2;
     h1[i] = P::cvt(c == a.n1 ? 1.f : 0.f);
   }
-  for (int i = tid; i < ROWS * ld3; i += 256) {
+  for (int i = tid; i < ROWS * ld3; i += NTHR) {
     int c = i % ld3;
     h2[i] = P::cvt(c == a.n2 ? 1.f : 0.f);
   }
-  for (int d = tid; d < O; d += 256) { s1[d] = 0.f; s2[d] = 0.f; }
+  for (int d = tid; d < O; d += NTHR) { s1[d] = 0.f; s2[d] = 0.f; }
   if (tid < ROWS) {
     int e = e0 + tid;
     eplen[tid] = (tid < nvalid) ? a.ep_len[e] : 0;
@@ -97,7 +99,7 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
     const int tb = a.t_base + step;
     const bool last = (step == a.T);  // bootstrap observation only
     // ---- (a) observe, moments, normalise -> LDS tile + global buffer row ----
-    for (int d = tid; d < a.d1; d += 256) {
+    for (int d = tid; d < a.d1; d += NTHR) {
       float m = 0.f, is = 1.f, sh = 0.f;
       if (d < O) { m = a.mean[d]; is = a.inv_std[d]; sh = a.shift[d]; }
       float ls1 = 0.f, ls2 = 0.f;
@@ -285,13 +287,13 @@ __global__ __launch_bounds__(256) void rollout_kernel(RolloutArgs a) {
   }
   __syncthreads();
   // ---- write back env state, episode trackers, partial moments / episode stats ----
-  for (int i = tid; i < nvalid * S; i += 256) a.state[(size_t)e0 * S + i] = st[i];
+  for (int i = tid; i < nvalid * S; i += NTHR) a.state[(size_t)e0 * S + i] = st[i];
   if (tid < nvalid) {
     a.ep_len[e0 + tid] = eplen[tid];
     a.ep_ret[e0 + tid] = epret[tid];
   }
   float* mom = a.mom + (size_t)blockIdx.x * 2 * O;
-  for (int d = tid; d < O; d += 256) { mom[d] = s1[d]; mom[O + d] = s2[d]; }
+  for (int d = tid; d < O; d += NTHR) { mom[d] = s1[d]; mom[O + d] = s2[d]; }
   if (tid == 0) {
     float sr = 0.f, sc = 0.f;
     for (int r = 0; r < ROWS; ++r) { sr += epacc[2 * r]; sc += epacc[2 * r + 1]; }
@@ -316,17 +318,28 @@ size_t rollout_lds(const RolloutArgs& a) {
   return b;
 }
 
-template <int DT, int ROWS>
-void launch_t(const RolloutArgs& a, hipStream_t s) {
-  size_t lds = rollout_lds<DT, ROWS>(a);
-  int nblk = (a.E + ROWS - 1) / ROWS;
+int g_rollout_waves = 8;   // 4 or 8 (set_rollout_waves: A/B diagnostics)
+
+template <int DT, int ROWS, int NW>
+void launch_nw(const RolloutArgs& a, hipStream_t s) {
+  const size_t lds = rollout_lds<DT, ROWS>(a);
+  const int nblk = (a.E + ROWS - 1) / ROWS;
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)rollout_kernel<DT, ROWS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((rollout_kernel<DT, ROWS>), dim3(nblk), dim3(256), lds, s, a);
+    (void)hipFuncSetAttribute((const void*)rollout_kernel<DT, ROWS, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  hipLaunchKernelGGL((rollout_kernel<DT, ROWS, NW>), dim3(nblk), dim3(NW * 64), lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
+template <int DT, int ROWS>
+void launch_t(const RolloutArgs& a, hipStream_t s) {
+  if (g_rollout_waves == 4) launch_nw<DT, ROWS, 4>(a, s);
+  else launch_nw<DT, ROWS, 8>(a, s);
+}
+
 }  // namespace
+
+extern "C" void set_rollout_waves(int nw) { g_rollout_waves = nw; }
 
 extern "C" void launch_rollout(int dt, const RolloutArgs& a, int rows, hipStream_t s) {
   if (rows == 32) {

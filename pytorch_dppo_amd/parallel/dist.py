@@ -33,11 +33,20 @@ class DistContext:
     local_rank: int = 0
     backend: str = "none"
     device: torch.device = torch.device("cpu")
+    # run the hot-path collectives even at world size 1, where a sum over one rank is the
+    # identity (tests use it to exercise the real RCCL call on the 1-GPU box)
+    force_collectives: bool = False
 
     @property
     def enabled(self) -> bool:
-        # a world-size-1 group still runs the real collective (bench at N=1 exercises RCCL)
         return dist.is_available() and dist.is_initialized()
+
+    @property
+    def collective(self) -> bool:
+        """hot-path reductions run: a group exists and has more than one rank (or forced).
+        At world size 1 every all-reduce is the identity, and an RCCL call still costs
+        ~10 us of stream handoff per epoch (rocprofv3 timeline), so it is skipped."""
+        return self.enabled and (self.world_size > 1 or self.force_collectives)
 
     @property
     def is_main(self) -> bool:
@@ -49,7 +58,7 @@ class DistContext:
 
         With ``async_op`` the returned work handle's ``wait()`` orders the consumer after
         the collective on the device stream (RCCL runs on its own stream)."""
-        if not self.enabled:
+        if not self.collective:
             return None
         work = dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, async_op=async_op)
         if mean:
@@ -69,7 +78,7 @@ class DistContext:
 
         ``count_uniform``: every rank contributed the same (host-known) count, so the global
         count is count * world_size and no device->host read is needed (the hot path)."""
-        if not self.enabled:
+        if not self.collective:
             return count, s1, s2
         O = s1.numel()
         if count_uniform:
@@ -90,12 +99,12 @@ class DistContext:
         parts = [vals[k].reshape(1).to(self.device, torch.float64) if torch.is_tensor(vals[k])
                  else torch.tensor([float(vals[k])], dtype=torch.float64, device=self.device) for k in keys]
         t = torch.cat(parts)
-        if self.enabled:
+        if self.collective:
             dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
         return {k: float(x) for k, x in zip(keys, t.tolist())}
 
     def allreduce_tensor_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
-        if self.enabled:
+        if self.collective:
             dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
                                    "min": dist.ReduceOp.MIN}[op])
         return t

@@ -103,6 +103,7 @@ class HipEngine:
         nroll = (E + ROLL_ROWS - 1) // ROLL_ROWS
         self.mom = torch.zeros(nroll, 2, O, **f32)
         self.epstat = torch.zeros(nroll, 2, **f32)
+        self.ep_sum = torch.zeros(2, dtype=torch.float64, device=device)
         # ---- update geometry ----
         self.mb = params.minibatch_rows()
         self.ldT = _r(self.mb, 64)      # wgrad consumes k-steps in pairs (csrc/wgrad.hip)
@@ -305,9 +306,10 @@ class HipEngine:
                                  self.xT if self.xT_from_rollout else None)
             self._xT_valid = self.xT_from_rollout
             self.env.t += self.T
-            self.ext.obs_reduce(self.mom, self.mom.shape[0], self.O, self.s12)
+            # one launch: moments [nblk][2][O] -> s12, episode stats [nblk][2] -> ep_sum
+            self.ext.obs_reduce(self.mom, self.mom.shape[0], self.O, self.s12, self.epstat, self.ep_sum)
             s1, s2 = self.s12[0], self.s12[1]
-            ep = self.epstat.double().sum(0)
+            ep = self.ep_sum
         else:
             self.local_stats = RunningObsStats(self.O, self.device)
             self.local_stats.copy_from(self.stats)

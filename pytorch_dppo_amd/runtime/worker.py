@@ -143,7 +143,7 @@ class DPPOWorker:
                 if p.compat and self.updates == 0:
                     extra = 1.0  # Q1: Shared_grad_buffers start at ones (model.py:51)
                 last = epoch == p.num_epoch - 1 and b == nmb - 1
-                if p.overlap_rollout and last and not mean and self.ctx.enabled:
+                if p.overlap_rollout and last and not mean and self.ctx.collective:
                     work = self.ctx.allreduce_grads(eng.grad_flat, async_op=True)
                     self._pending = (work, extra)      # applied after the next rollout launch
                 else:

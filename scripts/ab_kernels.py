@@ -62,7 +62,8 @@ def main():
         "adam_sumsq_pair": (knobs(adam=0), eng.apply),
         "grad_wgrad_lds_dma": (knobs(wgrad=0), lambda: eng.grad(None)),
         "grad_wgrad_register": (knobs(wgrad=1), lambda: eng.grad(None)),
-        "rollout": (knobs(), eng.rollout),
+        "rollout_8waves": (lambda: (knobs()(), ext.set_rollout_waves(8)), eng.rollout),
+        "rollout_4waves": (lambda: (knobs()(), ext.set_rollout_waves(4)), eng.rollout),
         "values_rows64": (knobs(r=64), eng.values),
         "values_rows32": (knobs(r=32), eng.values),
         "grad_rows64": (knobs(r=64), lambda: eng.grad(None)),
@@ -79,6 +80,7 @@ def main():
     ext.set_adam_fused(1)
     ext.set_wgrad_impl(0)
     rows(0)
+    ext.set_rollout_waves(8)
     eng._build_wgrad_plan(model)
     print(json.dumps({k: {"median_us": sorted(v)[len(v) // 2], "min_us": min(v)} for k, v in res.items()}, indent=1))
 

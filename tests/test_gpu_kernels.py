@@ -118,7 +118,7 @@ def test_rollout_matches_torch_engine(env_name):
 
 def test_obs_reduce_and_merge_kernels_match_torch_welford():
     ext = _ext()
-    O, nblk = 37, 19
+    O, nblk = 37, 19     # 2*O = 74 columns: two column groups, one ragged
     g = torch.Generator(device="cpu").manual_seed(4)
     ref = RunningObsStats(O, DEV)
     dev_st = RunningObsStats(O, DEV)
@@ -131,8 +131,12 @@ def test_obs_reduce_and_merge_kernels_match_torch_welford():
         d = (x - dev_st.shift()).view(nblk, 8, O)
         part = torch.stack([d.sum(1), (d * d).sum(1)], 1).float().contiguous()
         s12 = torch.zeros(2, O, dtype=torch.float64, device=DEV)
-        ext.obs_reduce(part, nblk, O, s12)
+        epstat = torch.rand(nblk, 2, generator=g).to(DEV)
+        ep = torch.zeros(2, dtype=torch.float64, device=DEV)
+        ext.obs_reduce(part, nblk, O, s12, epstat, ep)
         assert torch.allclose(s12[0], s1, rtol=1e-5, atol=1e-3)
+        assert torch.allclose(s12[1], s2, rtol=1e-5, atol=1e-2)
+        assert torch.allclose(ep, epstat.double().sum(0), rtol=1e-12)
         ext.obs_merge(s12, float(nblk * 8), float(dev_st.n), dev_st.shift().clone(), dev_st.mean, dev_st.mean_diff,
                       dev_st.mean_f32, dev_st.inv_std_f32, 1e-2)
         dev_st.n += nblk * 8
@@ -378,6 +382,7 @@ def test_rccl_world1_allreduce_and_training_step():
     from pytorch_dppo_amd.runtime.launcher import free_port
     from pytorch_dppo_amd.runtime.worker import DPPOWorker
     ctx = init_single_rank_collective(DEV, port=free_port())
+    ctx.force_collectives = True      # the identity sum still goes through RCCL
     try:
         g = torch.arange(1000, device=DEV, dtype=torch.float32)
         ctx.allreduce_grads(g)
