@@ -17,6 +17,15 @@ hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 // training runs (the results of an ablated call are not a gradient)
 int g_train_ablate = 0;
 void set_train_ablation(int64_t mask) { g_train_ablate = (int)mask; }
+// diagnostics only: per-phase cycle sums of the rollout kernel (scripts/phase_timeline.py)
+unsigned long long* g_roll_tstamp = nullptr;
+int64_t g_roll_tstamp_numel = 0;
+void set_rollout_tstamp(torch::Tensor buf) {
+  if (!buf.defined() || buf.numel() == 0) { g_roll_tstamp = nullptr; return; }
+  TORCH_CHECK(buf.scalar_type() == at::kLong && buf.is_cuda() && buf.is_contiguous(), "int64 device buffer");
+  g_roll_tstamp = reinterpret_cast<unsigned long long*>(buf.data_ptr<int64_t>());
+  g_roll_tstamp_numel = buf.numel();
+}
 // diagnostics only: phase-timeline stamps of mlp_train (scripts/phase_timeline.py)
 unsigned long long* g_tstamp = nullptr;
 int g_tstamp_every = 1;
@@ -151,6 +160,10 @@ void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len
     a.ldT = (int)ld;
   }
   a.epstat = epstat.data_ptr<float>();
+  if (g_roll_tstamp != nullptr) {
+    TORCH_CHECK(g_roll_tstamp_numel >= (int64_t)nblk * 8 * 8, "rollout tstamp buffer too small");
+    a.tstamp = g_roll_tstamp;
+  }
   launch_rollout((int)dt, a, (int)rows, cur_stream());
 }
 
@@ -439,6 +452,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     set_rollout_waves((int)nw);
   });
   m.def("set_train_tstamp", &set_train_tstamp);
+  m.def("set_rollout_tstamp", &set_rollout_tstamp);
   m.def("wgrad", &wgrad);
   m.def("grad_gather", &grad_gather);
   m.def("gae", &gae);

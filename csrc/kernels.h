@@ -41,6 +41,7 @@ struct RolloutArgs {
   int ldT;             // its row length (== T*E of the whole buffer)
   float* mom;          // [nblk][2][O]  sum(x-shift), sum((x-shift)^2)
   float* epstat;       // [nblk][2]     finished-episode return sum, count
+  unsigned long long* tstamp;  // DIAGNOSTIC ONLY (null in real runs): [nblk][NW][8] phase cycles
 };
 
 struct MlpArgs {

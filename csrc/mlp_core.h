@@ -39,10 +39,9 @@ DEV float act_tanh(float x) {
   }
 }
 
-// k-steps per prefetch chunk.  With 2+ row blocks (32/64-row tiles) the A fragments of a chunk
-// multiply, and the cross-barrier BPre sets live alongside, so the chunk is 2 k-steps to keep
-// two register sets inside the 2-waves/SIMD VGPR budget (4 for the 16-row rollout tile).
-template <int DT, int RB> struct KChunk { static constexpr int KC = (DT == DT_F32) ? 2 : (RB >= 2 ? 2 : 4); };
+// k-steps per prefetch chunk: 2, so two register sets plus the cross-barrier BPre set stay
+// inside the 2-waves/SIMD VGPR budget at every row tile (4 spilled once BPre was added).
+template <int DT, int RB> struct KChunk { static constexpr int KC = 2; };
 
 template <int DT>
 DEV void store4_T(typename Prec<DT>::T* dst, float v0, float v1, float v2, float v3) {

@@ -11,6 +11,8 @@
 // rows (mlp.hip), which is far more MFMA-efficient than T small ones.
 //
 // Reference: train.py:82-106 (one env, batch 1, python loop) and model.py:68-80.
+#include <type_traits>
+
 #include "kernels.h"
 #include "mlp_core.h"
 
@@ -20,12 +22,18 @@ constexpr float LOG_2PI_F = 1.8378770664093453f;
 constexpr float SYN_DECAY = 0.9f, SYN_DRIVE = 0.1f, SYN_NOISE = 0.05f, SYN_RESET = 0.1f;
 constexpr float SYN_TERM_P = 0.002f;
 
-DEV float env_obs(int kind, const float* st, int S, int r, int d) {
-  if (kind == 1) {  // pendulum: (cos th, sin th, thdot)
-    float th = st[r * S + 0];
+// observation of env r, dim d.  KIND is a template parameter: with a runtime kind the
+// pendulum's libm cosf/sinf (Payne-Hanek reduction, divergent per lane) was inlined into each
+// of the ROWS unrolled iterations of the synthetic env's observe loop (~2,500 dead
+// instructions per step and a 3x slower phase).
+template <int KIND>
+DEV float env_obs(const float* st, int S, int r, int d) {
+  if constexpr (KIND == 1) {  // pendulum: (cos th, sin th, thdot)
+    const float th = st[r * S + 0];
     return d == 0 ? cosf(th) : (d == 1 ? sinf(th) : st[r * S + 1]);
+  } else {
+    return st[r * S + d];
   }
-  return st[r * S + d];
 }
 
 // NW waves per workgroup: a 16-env tile is one workgroup per CU at E = 4096, so the 8-wave
@@ -59,6 +67,8 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   float* epret = cv.take<float>(ROWS);
   float* epacc = cv.take<float>(2 * ROWS);
   uint32_t* kes = cv.take<uint32_t>(3 * ROWS);   // per-env key prefixes of this step: action, env, reset
+  float* wdrv = cv.take<float>(S);                // synthetic dynamics: drive weight of state dim d
+  int* jdx = cv.take<int>(S);                     //                     action index driving dim d
 
   const T* W = reinterpret_cast<const T*>(a.W);
   const T* W1 = W + a.off_w1;
@@ -85,6 +95,10 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
     h2[i] = P::cvt(c == a.n2 ? 1.f : 0.f);
   }
   for (int d = tid; d < O; d += NTHR) { s1[d] = 0.f; s2[d] = 0.f; }
+  for (int d = tid; d < S; d += NTHR) {   // per-dim constants once per launch (no per-step modulo)
+    wdrv[d] = 0.5f + (float)(d % 7) / 7.0f;
+    jdx[d] = d % A;
+  }
   if (tid < ROWS) {
     int e = e0 + tid;
     eplen[tid] = (tid < nvalid) ? a.ep_len[e] : 0;
@@ -94,57 +108,99 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   }
   __syncthreads();
 
-  // sigma per action dim
+  // normalisation constants of this thread's first feature: fixed for the whole launch, so
+  // loaded once instead of once per step (the compiler cannot hoist them past the stores)
+  float hm = 0.f, his = 1.f, hsh = 0.f;
+  if (tid < O) { hm = a.mean[tid]; his = a.inv_std[tid]; hsh = a.shift[tid]; }
+  BPre<DT, ROWS / 16> pf;   // cross-barrier weight prefetch of each layer's first k-chunk
+  // bf16 / fp32: the LDS tile and the buffer share the element type (fp8 tiles feed a bf16 buffer)
+  constexpr bool XO_FROM_LDS = sizeof(T) == sizeof(typename PX::T) && sizeof(T) == 2;
+  // phase timeline (diagnostics, a.tstamp != null): per-wave shader-clock cycles summed over
+  // the steps for each phase, written by lane 0 of every wave of every workgroup
+  unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ph_t = a.tstamp ? __builtin_amdgcn_s_memtime() : 0ull;
+#define PH(i)                                                     \
+  do {                                                            \
+    if (a.tstamp != nullptr) {                                    \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+      ph_acc[i] += t_ - ph_t;                                     \
+      ph_t = t_;                                                  \
+    }                                                             \
+  } while (0)
   for (int step = 0; step <= a.T; ++step) {
     const int tb = a.t_base + step;
     const bool last = (step == a.T);  // bootstrap observation only
     // ---- (a) observe, moments, normalise -> LDS tile + global buffer row ----
-    for (int d = tid; d < a.d1; d += NTHR) {
-      float m = 0.f, is = 1.f, sh = 0.f;
-      if (d < O) { m = a.mean[d]; is = a.inv_std[d]; sh = a.shift[d]; }
-      float ls1 = 0.f, ls2 = 0.f;
-      typename PX::T grp[ROWS];   // this feature's ROWS consecutive buffer rows (xT groups of 8)
+    auto observe = [&](auto kind_tag) {
+      constexpr int KIND = decltype(kind_tag)::value;
+      for (int d = tid; d < a.d1; d += NTHR) {
+        float m = hm, is = his, sh = hsh;
+        if (d != tid && d < O) { m = a.mean[d]; is = a.inv_std[d]; sh = a.shift[d]; }
+        float ls1 = 0.f, ls2 = 0.f;
+        typename PX::T grp[ROWS];   // this feature's ROWS consecutive buffer rows (xT groups of 8)
 #pragma unroll
-      for (int r = 0; r < ROWS; ++r) {
-        float xv;
-        if (d < O) {
-          float o = env_obs(a.kind, st, S, r, d);
-          if (!last && r < nvalid) { float dd = o - sh; ls1 += dd; ls2 += dd * dd; }
-          xv = fminf(fmaxf((o - m) * is, -5.f), 5.f);
-        } else {
-          xv = (d == O) ? 1.f : 0.f;
-        }
-        xs[r * ld1 + d] = P::cvt(xv);
-        grp[r] = PX::cvt(xv);
-        if (r < nvalid) xo[((size_t)tb * a.buf_E + e0 + r) * a.d1 + d] = grp[r];
-      }
-      if (d < O) { s1[d] += ls1; s2[d] += ls2; }
-      // full-batch update operand: rows m = tb*E + e0 + r are contiguous 8-groups of the FM
-      // layout (host guarantees E % 16 == 0), written once per rollout instead of per epoch
-      if (a.xT_out != nullptr && !last) {
-        typename PX::T* xT = reinterpret_cast<typename PX::T*>(a.xT_out);
-        const int mrow = tb * a.buf_E + e0;
-#pragma unroll
-        for (int g = 0; g < ROWS / 8; ++g) {
-          typename PX::T* o = xT + fm_index(d, mrow + 8 * g, a.ldT);
-          if constexpr (sizeof(typename PX::T) == 2) {
-            *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(&grp[8 * g]);
+        for (int r = 0; r < ROWS; ++r) {
+          float xv;
+          if (d < O) {
+            float o = env_obs<KIND>(st, S, r, d);
+            if (!last && r < nvalid) { float dd = o - sh; ls1 += dd; ls2 += dd * dd; }
+            xv = fminf(fmaxf((o - m) * is, -5.f), 5.f);
           } else {
-            reinterpret_cast<uint4*>(o)[0] = reinterpret_cast<const uint4*>(&grp[8 * g])[0];
-            reinterpret_cast<uint4*>(o)[1] = reinterpret_cast<const uint4*>(&grp[8 * g])[1];
+            xv = (d == O) ? 1.f : 0.f;
+          }
+          xs[r * ld1 + d] = P::cvt(xv);
+          grp[r] = PX::cvt(xv);
+          if constexpr (!XO_FROM_LDS)
+            if (r < nvalid) xo[((size_t)tb * a.buf_E + e0 + r) * a.d1 + d] = grp[r];
+        }
+        if (d < O) { s1[d] += ls1; s2[d] += ls2; }
+        // full-batch update operand: rows m = tb*E + e0 + r are contiguous 8-groups of the FM
+        // layout (host guarantees E % 16 == 0), written once per rollout instead of per epoch
+        if (a.xT_out != nullptr && !last) {
+          typename PX::T* xT = reinterpret_cast<typename PX::T*>(a.xT_out);
+          const int mrow = tb * a.buf_E + e0;
+#pragma unroll
+          for (int g = 0; g < ROWS / 8; ++g) {
+            typename PX::T* o = xT + fm_index(d, mrow + 8 * g, a.ldT);
+            if constexpr (sizeof(typename PX::T) == 2) {
+              *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(&grp[8 * g]);
+            } else {
+              reinterpret_cast<uint4*>(o)[0] = reinterpret_cast<const uint4*>(&grp[8 * g])[0];
+              reinterpret_cast<uint4*>(o)[1] = reinterpret_cast<const uint4*>(&grp[8 * g])[1];
+            }
           }
         }
       }
+    };
+    if (a.kind == 1) observe(std::integral_constant<int, 1>{});
+    else observe(std::integral_constant<int, 0>{});
+    if (!last) layer_prefetch<DT, ROWS, NW>(pf, W1, a.d1, a.n1, wave, lane);
+    __syncthreads();
+    if constexpr (XO_FROM_LDS) {
+      // row-major buffer rows from the normalised LDS tile: one 16-byte store per 8 features
+      // instead of ROWS 2-byte stores per feature (fire-and-forget, overlaps the MFMA layers)
+      const int ch = a.d1 / 8;
+      for (int i = tid; i < nvalid * ch; i += NTHR) {
+        const int r = i / ch, c = i - r * ch;
+        *reinterpret_cast<uint4*>(xo + ((size_t)tb * a.buf_E + e0 + r) * a.d1 + c * 8) =
+            *reinterpret_cast<const uint4*>(xs + r * ld1 + c * 8);
+      }
     }
     if (last) break;
-    __syncthreads();
+    PH(0);   // (a) observe -> after its barrier
     // ---- (b) policy MLP ----
-    layer_gemm<DT, ROWS, NW, EPI_TANH>(xs, ld1, a.d1, W1, a.n1, h1, ld2, sc1, wave, lane);
+    layer_gemm<DT, ROWS, NW, EPI_TANH, true>(xs, ld1, a.d1, W1, a.n1, h1, ld2, sc1, wave, lane, nullptr, 0, 0, 0, &pf);
+    layer_prefetch<DT, ROWS, NW>(pf, W2, a.d2, a.n2, wave, lane);
     __syncthreads();
-    layer_gemm<DT, ROWS, NW, EPI_TANH>(h1, ld2, a.d2, W2, a.n2, h2, ld3, sc2, wave, lane);
+    PH(1);
+    layer_gemm<DT, ROWS, NW, EPI_TANH, true>(h1, ld2, a.d2, W2, a.n2, h2, ld3, sc2, wave, lane, nullptr, 0, 0, 0, &pf);
+    layer_prefetch<DT, ROWS, NW>(pf, W3, a.d3, a.n3, wave, lane);
     __syncthreads();
-    layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32>(h2, ld3, a.d3, W3, a.n3, mu, A, sc3, wave, lane);
+    PH(2);
+    layer_gemm<DT, ROWS, NW, EPI_LINEAR_F32, true>(h2, ld3, a.d3, W3, a.n3, mu, A, sc3, wave, lane, nullptr, 0, 0, 0,
+                                                   &pf);
     __syncthreads();
+    PH(3);   // fc1, fc2, fc3 (each incl. barrier)
     // ---- (c) sample a = mu + sigma * eps (one Box-Muller pair -> two action dims) ----
     const uint32_t kstep = a.t0 + (uint32_t)step;
     if (tid < ROWS) {   // (env, step) key prefixes, shared by every dim of the step
@@ -173,6 +229,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
       }
     }
     __syncthreads();
+    PH(4);   // (c) sample
     // ---- (d) per-env: logp, reward, termination, episode bookkeeping ----
     // LPE lanes per env (contiguous inside a wave) share the per-dim sums, then reduce by shuffles
     {
@@ -234,6 +291,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
       }
     }
     __syncthreads();
+    PH(5);   // (d) logp / reward
     // ---- (e) state transition (+ in-place reset on done) ----
     if (a.kind == 1) {
       if (tid < ROWS) {
@@ -254,38 +312,46 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
         }
       }
     } else {
-      // item = (dim pair p, group of 4 rows): one runtime division per item, the per-dim
-      // constants (drive weight, action index) once per item, one Box-Muller pair per 2 dims
+      // item = (row r, dim pair p), consecutive threads on consecutive pairs of one row: the
+      // 16 x S/2 items spread evenly over the threads (one Box-Muller pair per item) and the
+      // per-dim constants come from LDS tables filled once per launch
       const int np = (S + 1) >> 1;
-      for (int it = tid; it < np * (ROWS / 4); it += NTHR) {
-        const int rg = it / np, p = it - rg * np;
+      int r = tid / np, p = tid - r * np;
+      const int sr = NTHR / np, sp = NTHR - sr * np;
+      while (r < ROWS) {
         const int d0 = 2 * p, d1 = d0 + 1;
         const bool has1 = d1 < S;
-        const float w0 = 0.5f + (float)(d0 % 7) / 7.0f, w1 = 0.5f + (float)(d1 % 7) / 7.0f;
-        const int j0 = d0 % A, j1 = d1 % A;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int r = rg * 4 + k;
-          float n0, n1;
-          if (done_s[r] > 0.5f) {
-            const float2 g = gauss_pair(kes[2 * ROWS + r], (uint32_t)p);
-            n0 = SYN_RESET * g.x;
-            n1 = SYN_RESET * g.y;
-          } else {
-            const float2 g = gauss_pair(kes[ROWS + r], (uint32_t)p);
-            const float a0 = fminf(fmaxf(act[r * A + j0], -1.f), 1.f);
-            const float a1 = fminf(fmaxf(act[r * A + j1], -1.f), 1.f);
-            n0 = SYN_DECAY * st[r * S + d0] + SYN_DRIVE * fast_tanh(w0 * a0) + SYN_NOISE * g.x;
-            n1 = has1 ? SYN_DECAY * st[r * S + d1] + SYN_DRIVE * fast_tanh(w1 * a1) + SYN_NOISE * g.y : 0.f;
+        float n0, n1;
+        if (done_s[r] > 0.5f) {
+          const float2 g = gauss_pair(kes[2 * ROWS + r], (uint32_t)p);
+          n0 = SYN_RESET * g.x;
+          n1 = SYN_RESET * g.y;
+        } else {
+          const float2 g = gauss_pair(kes[ROWS + r], (uint32_t)p);
+          const float a0 = fminf(fmaxf(act[r * A + jdx[d0]], -1.f), 1.f);
+          n0 = SYN_DECAY * st[r * S + d0] + SYN_DRIVE * fast_tanh(wdrv[d0] * a0) + SYN_NOISE * g.x;
+          n1 = 0.f;
+          if (has1) {
+            const float a1 = fminf(fmaxf(act[r * A + jdx[d1]], -1.f), 1.f);
+            n1 = SYN_DECAY * st[r * S + d1] + SYN_DRIVE * fast_tanh(wdrv[d1] * a1) + SYN_NOISE * g.y;
           }
-          st[r * S + d0] = n0;
-          if (has1) st[r * S + d1] = n1;
         }
+        st[r * S + d0] = n0;
+        if (has1) st[r * S + d1] = n1;
+        r += sr;
+        p += sp;
+        if (p >= np) { p -= np; ++r; }
       }
     }
     __syncthreads();
+    PH(6);   // (e) env transition
   }
   __syncthreads();
+  if (a.tstamp != nullptr && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a.tstamp[((size_t)blockIdx.x * NW + wave) * 8 + i] = ph_acc[i];
+  }
+#undef PH
   // ---- write back env state, episode trackers, partial moments / episode stats ----
   for (int i = tid; i < nvalid * S; i += NTHR) a.state[(size_t)e0 * S + i] = st[i];
   if (tid < nvalid) {
@@ -315,6 +381,7 @@ size_t rollout_lds(const RolloutArgs& a) {
   b += 2 * al(sizeof(float) * a.O);
   b += al(sizeof(float) * ROWS) + al(sizeof(int) * ROWS) + al(sizeof(float) * ROWS) + al(sizeof(float) * 2 * ROWS);
   b += al(sizeof(uint32_t) * 3 * ROWS);
+  b += al(sizeof(float) * a.S) + al(sizeof(int) * a.S);
   return b;
 }
 
@@ -333,7 +400,8 @@ void launch_nw(const RolloutArgs& a, hipStream_t s) {
 
 template <int DT, int ROWS>
 void launch_t(const RolloutArgs& a, hipStream_t s) {
-  if (g_rollout_waves == 4) launch_nw<DT, ROWS, 4>(a, s);
+  // fp32 operands: the 8-wave form spills (fp32 fragments are twice the registers)
+  if (g_rollout_waves == 4 || DT == DT_F32) launch_nw<DT, ROWS, 4>(a, s);
   else launch_nw<DT, ROWS, 8>(a, s);
 }
 

@@ -66,6 +66,18 @@ def main():
                                                          for i, ph in enumerate(PHASES)}}
         out[f"rows{rows}"] = res
     ext.set_mlp_rows(0)
+    # rollout: per-wave cycles per phase summed over the T steps, median over workgroups
+    nblk = (eng.E + 15) // 16
+    rb = torch.zeros(nblk * 8 * 8, dtype=torch.int64, device=dev)
+    eng.rollout()
+    ext.set_rollout_tstamp(rb)
+    eng.rollout()
+    torch.cuda.synchronize()
+    ext.set_rollout_tstamp(torch.empty(0, dtype=torch.int64, device=dev))
+    r = rb.view(nblk, 8, 8).cpu().double()
+    names = ["observe+norm (a)", "fc1", "fc2", "fc3", "sample (c)", "logp/reward (d)", "env step (e)"]
+    out["rollout_per_step_cycles"] = {n: float(r[:, :, i].max(dim=1).values.median()) / eng.T
+                                      for i, n in enumerate(names)}
     print(json.dumps(out, indent=1))
 
 
