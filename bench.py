@@ -53,6 +53,10 @@ def main():
                     help="overlap the final gradient all-reduce with the next rollout (1-update lag)")
     ap.add_argument("--graphs", action="store_true",
                     help="replay the per-minibatch launch chains as hipGraphs (use_graphs)")
+    ap.add_argument("--grad-buckets", default="off", choices=["auto", "on", "off"],
+                    help="bucketed gradient all-reduce overlapping the wgrad (auto: multi-rank)")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="diagnostics: run the hot-path RCCL collectives even at world size 1")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -63,12 +67,13 @@ def main():
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         ctx = init_single_rank_collective(dev, port=int(os.environ.get("MASTER_PORT", "29561")))
+    ctx.force_collectives = args.force_collectives
     E, T = args.num_envs, args.rollout_len
     rows = E * T
     p = dppo_preset(device="gpu", env_name=args.env_name, num_envs=E, exploration_size=rows,
                     batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=args.dtype,
                     num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
-                    use_graphs=args.graphs)
+                    use_graphs=args.graphs, grad_buckets=args.grad_buckets)
     w = DPPOWorker(p, ctx)
     for i in range(args.warmup):
         m = w.iteration_step()
@@ -104,6 +109,7 @@ def main():
                           "parallelism": f"dp{ctx.world_size}", "env": args.env_name, "num_envs_per_gpu": E,
                           "rollout_len": T, "num_epoch": args.num_epoch,
                           "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout, "graphs": args.graphs,
+                          "grad_buckets": bool(w.bucketed),
                           "last_iter": {k: m[k] for k in ("loss", "mean_ep_return", "ms_rollout", "ms_values_gae",
                                                           "ms_update", "ms_obs_stats") if k in m}}}
         print(json.dumps(out), flush=True)

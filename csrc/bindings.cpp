@@ -347,9 +347,15 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
   launch_wgrad((int)dt, a, cur_stream());
 }
 
+// i_lo/i_hi: flat parameter range gathered from the slabs (-1, -1: [A, n)); with_partials: also
+// the log_std gradients and the loss sums (the range must then start at or after A)
 void grad_gather(torch::Tensor slab, torch::Tensor src_off, int64_t nchunks, int64_t stride, torch::Tensor part,
-                 int64_t nblk, int64_t npart, int64_t A, double scale, torch::Tensor grad, torch::Tensor loss_out) {
+                 int64_t nblk, int64_t npart, int64_t A, double scale, torch::Tensor grad, torch::Tensor loss_out,
+                 int64_t i_lo, int64_t i_hi, bool with_partials) {
   const int64_t n = grad.numel();
+  if (i_lo < 0) i_lo = A;
+  if (i_hi < 0) i_hi = n;
+  TORCH_CHECK(A <= i_lo && i_lo <= i_hi && i_hi <= n, "gather range must lie in [A, n)");
   check(grad, "grad", at::kFloat, n);
   check(src_off, "src_off", at::kInt, n);
   check(slab, "slab", at::kFloat, nchunks * stride);
@@ -358,7 +364,7 @@ void grad_gather(torch::Tensor slab, torch::Tensor src_off, int64_t nchunks, int
   TORCH_CHECK(npart >= 8 + A, "npart");
   launch_grad_gather(slab.data_ptr<float>(), src_off.data_ptr<int>(), (int)nchunks, (int)stride,
                      part.data_ptr<float>(), (int)nblk, (int)npart, (int)A, (float)scale, grad.data_ptr<float>(),
-                     (int)n, loss_out.data_ptr<float>(), cur_stream());
+                     (int)i_lo, (int)i_hi, with_partials ? 1 : 0, loss_out.data_ptr<float>(), cur_stream());
 }
 
 void obs_reduce(torch::Tensor part, int64_t nblk, int64_t O, torch::Tensor s12, torch::Tensor epstat,

@@ -118,9 +118,11 @@ size_t mlp_train_lds_bytes(int dt, const MlpArgs& a);
 int mlp_train_rows(int dt, const MlpArgs& a);   // row tile the launcher will use (LDS-fit)
 void set_mlp_rows_override(int rows);           // 0 auto; 16/32/64 force (A/B diagnostics)
 void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
+// grad[i] for i in [i_lo, i_hi) from the slabs; with_partials: also log_std grads [0, A) and the
+// 8 loss sums from the per-workgroup partials
 void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int chunk_stride,
                         const float* part, int nblk, int npart, int A, float scale, float* grad,
-                        int n, float* loss_out, hipStream_t s);
+                        int i_lo, int i_hi, int with_partials, float* loss_out, hipStream_t s);
 void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
                 int T, int E, float gamma, float lam, int mode, hipStream_t s);
 void set_adam_fused(int on);

@@ -179,18 +179,20 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
       for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * WGRAD_TILE + col + 16 * j] = acc[i][j][q];
 }
 
-// Workgroups [0, A): grad[j] = scale * sum_b part[b*npart + 8 + j]  (log_std, one WG per dim,
-//                    strided partial sums + LDS tree: fixed order, deterministic)
-// Workgroups [A, grid): grad[i] = scale * sum_c slab[c*stride + src_off[i]], i in [A, n)
-//                    (fixed chunk order: deterministic; no float atomics anywhere)
-// Workgroups [A, A+8): loss_out[q] = sum_b part[b*npart + q] (loss-term sums for logging).
+// With the partials pass (nred = A + 8 > 0):
+//   Workgroups [0, A): grad[j] = scale * sum_b part[b*npart + 8 + j]  (log_std, one WG per dim,
+//                      strided partial sums + LDS tree: fixed order, deterministic)
+//   Workgroups [A, A+8): loss_out[q] = sum_b part[b*npart + q] (loss-term sums for logging).
+// Workgroups [nred, grid): grad[i] = scale * sum_c slab[c*stride + src_off[i]], i in [i_lo, i_hi)
+//                    (fixed chunk order: deterministic; no float atomics anywhere).  A bucketed
+//                    gradient (all-reduce of one flat range overlapping the next range's wgrad)
+//                    gathers each range with its own launch.
 __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restrict__ slab,
                                                           const int* __restrict__ src_off, int nchunks,
                                                           int stride, const float* __restrict__ part,
                                                           int nblk, int npart, int A, float scale,
-                                                          float* __restrict__ grad, int n,
-                                                          float* __restrict__ loss_out) {
-  const int nred = A + 8;
+                                                          float* __restrict__ grad, int i_lo, int i_hi,
+                                                          int nred, float* __restrict__ loss_out) {
   if ((int)blockIdx.x < nred) {
     __shared__ float red[256];
     const int j = blockIdx.x;
@@ -210,7 +212,7 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
     return;
   }
   const int nb = gridDim.x - nred;
-  for (int i = A + (blockIdx.x - nred) * 256 + threadIdx.x; i < n; i += nb * 256) {
+  for (int i = i_lo + (blockIdx.x - nred) * 256 + threadIdx.x; i < i_hi; i += nb * 256) {
     const int o = src_off[i];
     float s = 0.f;
     for (int c = 0; c < nchunks; ++c) s += slab[(size_t)c * stride + o];
@@ -239,12 +241,13 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
 
 extern "C" void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int chunk_stride,
                                    const float* part, int nblk, int npart, int A, float scale, float* grad,
-                                   int n, float* loss_out, hipStream_t s) {
-  int grid = (n - A + 255) / 256;
+                                   int i_lo, int i_hi, int with_partials, float* loss_out, hipStream_t s) {
+  int grid = (i_hi - i_lo + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
-  grid += A + 8;
+  const int nred = with_partials ? A + 8 : 0;
+  grid += nred;
   hipLaunchKernelGGL(grad_gather_kernel, dim3(grid), dim3(256), 0, s, slab, src_off, nchunks, chunk_stride,
-                     part, nblk, npart, A, scale, grad, n, loss_out);
+                     part, nblk, npart, A, scale, grad, i_lo, i_hi, nred, loss_out);
   HIP_CHECK_LAUNCH();
 }

@@ -137,6 +137,9 @@ class HipEngine:
         for buf, r in ((self.h1pT, lp1.fan_out), (self.h2pT, lp2.fan_out), (self.h1vT, lv1.fan_out),
                        (self.h2vT, lv2.fan_out)):
             buf.view(-1)[fm_index(torch.full_like(cols, r), cols, self.ldT)] = 1.0
+        self.split_grad = False          # bucketed gradient (enable_bucketed_grad, multi-rank)
+        self._pending_reduce = []        # async all-reduce works of the current step's buckets
+        self._reduce_stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None
         self._build_wgrad_plan(model)
         # ---- optimizer state ----
         n = model.num_params
@@ -170,56 +173,81 @@ class HipEngine:
         self.params_changed()
 
     # ------------------------------------------------------------------------------------------
-    def _build_wgrad_plan(self, model: ActorCritic, target_wgs: Optional[int] = None) -> None:
-        """Task list of the grouped split-K wgrad launch: (layer, 128x128 tile, batch chunk).
-        ``target_wgs`` workgroups (default WGRAD_TARGET_WGS, env DPPO_WGRAD_WGS) set the
-        number of batch chunks: more chunks = more parallelism but more fp32 partial slabs
-        for grad_gather to sum."""
+    def _build_wgrad_plan(self, model: ActorCritic, target_wgs: Optional[int] = None,
+                          split: Optional[bool] = None) -> None:
+        """Task lists of the grouped split-K wgrad launches: (layer, 128x128 tile, batch chunk).
+
+        One *bucket* = one wgrad launch + one grad_gather launch over a contiguous flat range of
+        the gradient.  Unbucketed (default): every layer in one bucket.  ``split`` (bucketed
+        gradient, multi-rank): bucket 0 = v_fc1, v_fc2, mu, v (flat [v_fc1.weight, n): 83 % of
+        the parameters, all-reduced asynchronously while) bucket 1 = p_fc1, p_fc2 + log_std +
+        loss sums (flat [0, v_fc1.weight)) computes — each bucket chunked for ~target_wgs
+        workgroups, with its own fp32 partial slab.  ``target_wgs`` defaults to
+        WGRAD_TARGET_WGS (env DPPO_WGRAD_WGS)."""
         if target_wgs is None:
             target_wgs = int(os.environ.get("DPPO_WGRAD_WGS", WGRAD_TARGET_WGS))
+        if split is None:
+            split = self.split_grad
         ls = self.L.layers
-        tiles = []  # (layer, n0, k0)
-        for li, l in enumerate(ls):
-            for n0 in range(0, l.fan_out, WT):
-                for k0 in range(0, l.fan_in + 1, WT):
-                    tiles.append((li, n0, k0))
-        ntiles = len(tiles)
-        max_chunks = max(1, self.ldT // 256)
-        want = -(-target_wgs // ntiles)           # >= ~target_wgs workgroups in flight
-        want = -(-want // 8) * 8                  # whole chunks per XCD (8 XCDs)
-        nchunks = max(1, min(max_chunks, want))
-        mc = _r(-(-self.ldT // nchunks), 64)   # even number of 32-row k-steps per task
-        chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
-        self.nchunks = len(chunks)
-        self.chunk_stride = ntiles * WT * WT
-        tile_off = {t: i * WT * WT for i, t in enumerate(tiles)}
-        # XCD-aware order: workgroups b, b+8, b+16, ... are dealt to the same XCD (observed
-        # round-robin placement; speed only), so all tiles of a batch chunk — which share the
-        # chunk's operand rows — are given consecutive slots of ONE XCD and hit its L2.
-        per_xcd = [[] for _ in range(8)]
-        for ci, (m0, m1) in enumerate(chunks):
-            for t in tiles:
-                per_xcd[ci % 8].append([t[0], t[1], t[2], m0, m1, ci * self.chunk_stride + tile_off[t]])
-        tasks = []
-        j = 0
-        while any(j < len(q) for q in per_xcd):
-            for q in per_xcd:
-                if j < len(q):
-                    tasks.append(q[j])
-            j += 1
-        self.tasks_host = torch.tensor(tasks, dtype=torch.int32).reshape(-1).contiguous()
-        self.tasks = self.tasks_host.to(self.device)
-        self.slab = torch.zeros(self.nchunks * self.chunk_stride, device=self.device, dtype=torch.float32)
-        # flat index -> offset of its element in the chunk-0 slab
+        names = [l.name for l in ls]
+        if split:
+            groups = [[names.index(n) for n in ("v_fc1", "v_fc2", "mu", "v")],
+                      [names.index(n) for n in ("p_fc1", "p_fc2")]]
+            cut = model.offsets["v_fc1.weight"][0]
+            ranges = [(cut, model.num_params), (self.A, cut)]
+        else:
+            groups = [list(range(len(ls)))]
+            ranges = [(self.A, model.num_params)]
         src = torch.full((model.num_params,), -1, dtype=torch.int64)
-        for li, l in enumerate(ls):
-            woff, wn = model.offsets[f"{l.name}.weight"]
-            nn_ = torch.arange(l.fan_out).repeat_interleave(l.fan_in)
-            kk = torch.arange(l.fan_in).repeat(l.fan_out)
-            src[woff:woff + wn] = self._slab_index(tile_off, li, nn_, kk)
-            boff, bn = model.offsets[f"{l.name}.bias"]
-            nb = torch.arange(l.fan_out)
-            src[boff:boff + bn] = self._slab_index(tile_off, li, nb, torch.full_like(nb, l.fan_in))
+        self.buckets = []
+        for bi, (layers, (lo, hi)) in enumerate(zip(groups, ranges)):
+            tiles = []  # (layer, n0, k0)
+            for li in layers:
+                l = ls[li]
+                for n0 in range(0, l.fan_out, WT):
+                    for k0 in range(0, l.fan_in + 1, WT):
+                        tiles.append((li, n0, k0))
+            ntiles = len(tiles)
+            max_chunks = max(1, self.ldT // 256)
+            # the small policy bucket: half the workgroups (its gather sums every chunk's slab)
+            tw = target_wgs if bi == 0 else max(64, target_wgs // 2)
+            want = -(-tw // ntiles)                   # >= ~tw workgroups in flight
+            want = -(-want // 8) * 8                  # whole chunks per XCD (8 XCDs)
+            nchunks = max(1, min(max_chunks, want))
+            mc = _r(-(-self.ldT // nchunks), 64)   # even number of 32-row k-steps per task
+            chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
+            chunk_stride = ntiles * WT * WT
+            tile_off = {t: i * WT * WT for i, t in enumerate(tiles)}
+            # XCD-aware order: workgroups b, b+8, b+16, ... are dealt to the same XCD (observed
+            # round-robin placement; speed only), so all tiles of a batch chunk — which share the
+            # chunk's operand rows — are given consecutive slots of ONE XCD and hit its L2.
+            per_xcd = [[] for _ in range(8)]
+            for ci, (m0, m1) in enumerate(chunks):
+                for t in tiles:
+                    per_xcd[ci % 8].append([t[0], t[1], t[2], m0, m1, ci * chunk_stride + tile_off[t]])
+            tasks = []
+            j = 0
+            while any(j < len(q) for q in per_xcd):
+                for q in per_xcd:
+                    if j < len(q):
+                        tasks.append(q[j])
+                j += 1
+            tasks_host = torch.tensor(tasks, dtype=torch.int32).reshape(-1).contiguous()
+            # flat index -> offset of its element in this bucket's chunk-0 slab
+            for li in layers:
+                l = ls[li]
+                woff, wn = model.offsets[f"{l.name}.weight"]
+                nn_ = torch.arange(l.fan_out).repeat_interleave(l.fan_in)
+                kk = torch.arange(l.fan_in).repeat(l.fan_out)
+                src[woff:woff + wn] = self._slab_index(tile_off, li, nn_, kk)
+                boff, bn = model.offsets[f"{l.name}.bias"]
+                nb = torch.arange(l.fan_out)
+                src[boff:boff + bn] = self._slab_index(tile_off, li, nb, torch.full_like(nb, l.fan_in))
+            self.buckets.append({
+                "tasks_host": tasks_host, "tasks": tasks_host.to(self.device),
+                "slab": torch.zeros(len(chunks) * chunk_stride, device=self.device, dtype=torch.float32),
+                "nchunks": len(chunks), "chunk_stride": chunk_stride, "lo": lo, "hi": hi,
+                "partials": bi == len(groups) - 1})
         src[src < 0] = 0  # log_std entries (handled from the partials)
         self.src_off = src.to(torch.int32).to(self.device)
 
@@ -348,7 +376,27 @@ class HipEngine:
 
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
-    def grad(self, idx: Optional[torch.Tensor]) -> None:
+    def enable_bucketed_grad(self, on: bool = True) -> bool:
+        """Bucketed gradient (multi-rank): the value-side range's all-reduce runs on RCCL's stream
+        while the policy range's wgrad computes (grad(idx, reducer)).  Not with hipGraph replay
+        (a collective cannot sit inside the captured chain).  Returns whether it is on."""
+        on = bool(on) and not self.use_graphs
+        if on != self.split_grad:
+            self.split_grad = on
+            self._build_wgrad_plan(self.model)
+        return on
+
+    def wait_reduce(self) -> None:
+        """order the compute stream after every bucket all-reduce of the last grad() call."""
+        for w in self._pending_reduce:
+            if w is not None:
+                w.wait()
+        self._pending_reduce = []
+
+    def grad(self, idx: Optional[torch.Tensor], reducer=None) -> None:
+        """one minibatch gradient into grad_flat.  ``reducer(t) -> work`` (bucketed mode): called
+        on each bucket's flat range as soon as it is gathered (async all-reduce); finish with
+        wait_reduce() before apply()."""
         p = self.p
         M = self.mb
         if idx is None:
@@ -364,12 +412,17 @@ class HipEngine:
             self.idx_dev[:M].copy_(idx.to(torch.int32), non_blocking=True)
             idx_t, row0 = self.idx_dev, 0
         first, xt_ready = bool(self._first_step), bool(idx is None and self._xT_valid)
-        self._launch(("grad", idx is None, first, xt_ready), lambda: self._launch_grad(idx_t, row0, first, xt_ready))
+        if reducer is not None:
+            assert not self.use_graphs, "bucketed all-reduce cannot run inside a captured graph"
+            self._launch_grad(idx_t, row0, first, xt_ready, reducer)
+        else:
+            self._launch(("grad", idx is None, first, xt_ready),
+                         lambda: self._launch_grad(idx_t, row0, first, xt_ready))
         self._first_step = False
         self._loss_dev = self.loss_sums
         return None
 
-    def _launch_grad(self, idx_t: torch.Tensor, row0: int, first: bool, xt_ready: bool) -> None:
+    def _launch_grad(self, idx_t: torch.Tensor, row0: int, first: bool, xt_ready: bool, reducer=None) -> None:
         p, M = self.p, self.mb
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
                 1 if p.std_convention == "var" else 0, 1 if first else 0, self.npart]
@@ -378,10 +431,30 @@ class HipEngine:
                            self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
                            self.ret, self.values_buf, self.mu_prev, self.v_prev, opts, fopts, self.tbufs,
                            self.ldT, self.part, False, xt_ready)
-        self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, self.tasks,
-                       self.tasks_host, self.slab)
-        self.ext.grad_gather(self.slab, self.src_off, self.nchunks, self.chunk_stride, self.part,
-                             self.ntrain_blk, self.npart, self.A, 1.0 / M, self.grad_flat, self.loss_sums)
+        ready = []
+        for bi, b in enumerate(self.buckets):
+            self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
+                           b["tasks_host"], b["slab"])
+            self.ext.grad_gather(b["slab"], self.src_off, b["nchunks"], b["chunk_stride"], self.part,
+                                 self.ntrain_blk, self.npart, self.A, 1.0 / M, self.grad_flat, self.loss_sums,
+                                 b["lo"], b["hi"], b["partials"])
+            if reducer is not None and bi < len(self.buckets) - 1:
+                ev = torch.cuda.Event()
+                ev.record()
+                ready.append((b, ev))
+        if reducer is not None:
+            # Bucketed gradient.  Every bucket's kernels are enqueued first; then each earlier
+            # bucket's all-reduce is issued from a side stream that waits on that bucket's
+            # gather event, so RCCL reduces it while the later buckets' wgrad runs on the compute
+            # stream — and the host-side cost of the collective call overlaps GPU work instead of
+            # leaving the GPU idle between launches.
+            for b, ev in ready:
+                self._reduce_stream.wait_event(ev)
+                with torch.cuda.stream(self._reduce_stream):
+                    self._pending_reduce.append(reducer(self.grad_flat[b["lo"]:b["hi"]]))
+            b = self.buckets[-1]
+            lo = 0 if b["partials"] else b["lo"]        # the partials bucket also owns log_std
+            self._pending_reduce.append(reducer(self.grad_flat[lo:b["hi"]]))
         if p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])  # train.py:164
 

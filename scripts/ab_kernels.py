@@ -69,7 +69,7 @@ def main():
         "grad_rows64": (knobs(r=64), lambda: eng.grad(None)),
         "grad_rows32": (knobs(r=32), lambda: eng.grad(None)),
     }
-    for t in (1024, 512, 256):
+    for t in (1024, 512, 256, 100):
         arms[f"grad_wgrad_wgs{t}"] = ((lambda t=t: (knobs()(), eng._build_wgrad_plan(model, t))),
                                       lambda: eng.grad(None))
     res = {k: [] for k in arms}

@@ -397,6 +397,51 @@ def test_rccl_world1_allreduce_and_training_step():
         dist.destroy_process_group()
 
 
+def test_bucketed_grad_allreduce_matches_single_bucket():
+    """Bucketed gradient (value-side range all-reduced on RCCL's stream while the policy-side
+    wgrad computes) == one-bucket gradient, through the real RCCL path at world size 1; then a
+    full bucketed worker iteration."""
+    import torch.distributed as dist
+    from pytorch_dppo_amd.parallel.dist import init_single_rank_collective
+    from pytorch_dppo_amd.runtime.launcher import free_port
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    ctx = init_single_rank_collective(DEV, port=free_port())
+    ctx.force_collectives = True
+    try:
+        p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 8,
+                        batch_size=64 * 8, num_epoch=3, dtype="bf16", grad_buckets="off", seed=3)
+        w = DPPOWorker(p, ctx)
+        assert not w.bucketed and len(w.engine.buckets) == 1
+        eng = w.engine
+        w.init_stats()
+        eng.rollout()
+        eng.values()
+        eng.gae()
+        eng.begin_update()
+        eng.grad(None)
+        g1 = eng.grad_flat.clone()
+        l1 = eng.loss_sums.clone()
+        assert eng.enable_bucketed_grad(True)
+        b0, b1 = eng.buckets
+        assert b1["partials"] and b0["hi"] == w.model.num_params and b1["hi"] == b0["lo"]
+        eng.grad(None, reducer=lambda t: ctx.allreduce_grads(t, async_op=True))
+        assert len(eng._pending_reduce) == 2
+        eng.wait_reduce()
+        torch.cuda.synchronize()
+        # same kernels; only the split-K chunking (fp32 summation order) differs between plans
+        assert torch.allclose(eng.grad_flat, g1, rtol=1e-5, atol=1e-7), (eng.grad_flat - g1).abs().max()
+        assert torch.equal(eng.loss_sums, l1)
+        p2 = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 8,
+                         batch_size=64 * 8, num_epoch=3, dtype="bf16", grad_buckets="on", seed=3,
+                         verify_sync_every=1)
+        w2 = DPPOWorker(p2, ctx)
+        assert w2.bucketed
+        m = w2.iteration_step()
+        assert math.isfinite(m["loss"]) and m["updates"] == 3 and m["replicas_in_sync"] is True
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.parametrize("batch", ["full", "minibatch"])
 def test_graph_replay_bit_identical_to_eager(batch):
     """use_graphs replays captured hipGraphs of the grad / Adam chains; the result must be bit-identical
