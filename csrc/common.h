@@ -137,6 +137,18 @@ DEV float gauss(uint32_t base, uint32_t env, uint32_t step, uint32_t dim) {
   return (dim & 1u) ? g.y : g.x;
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) is a driver call (~µs of host time): issue it
+// once per kernel instantiation and only raise it (the attribute is a per-function maximum).
+template <auto Kernel>
+inline void set_max_lds_once(size_t bytes) {
+  static size_t set = 0;   // one static per kernel (template on the function pointer itself)
+  if (bytes > set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(Kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+    set = bytes;
+  }
+}
+
 #define HIP_CHECK_LAUNCH()                                                       \
   do {                                                                           \
     hipError_t e__ = hipGetLastError();                                          \

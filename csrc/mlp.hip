@@ -513,8 +513,7 @@ int value_rows_t(const MlpArgs& a) {
 template <int DT, int ROWS, int NW>
 void train_launch(const MlpArgs& a, hipStream_t s) {
   const size_t lds = train_lds<DT, ROWS>(a);
-  (void)hipFuncSetAttribute((const void*)mlp_train_kernel<DT, ROWS, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
+  set_max_lds_once<mlp_train_kernel<DT, ROWS, NW>>(lds);
   const int nblk = (a.M + ROWS - 1) / ROWS;
   hipLaunchKernelGGL((mlp_train_kernel<DT, ROWS, NW>), dim3(nblk), dim3(NW * 64), lds, s, a);
   HIP_CHECK_LAUNCH();
@@ -523,8 +522,7 @@ void train_launch(const MlpArgs& a, hipStream_t s) {
 template <int DT, int ROWS, int NW>
 void value_launch(const MlpArgs& a, hipStream_t s) {
   const size_t lds = value_lds<DT, ROWS>(a);
-  (void)hipFuncSetAttribute((const void*)mlp_value_kernel<DT, ROWS, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
+  set_max_lds_once<mlp_value_kernel<DT, ROWS, NW>>(lds);
   const int nblk = (a.M + ROWS - 1) / ROWS;
   hipLaunchKernelGGL((mlp_value_kernel<DT, ROWS, NW>), dim3(nblk), dim3(NW * 64), lds, s, a);
   HIP_CHECK_LAUNCH();

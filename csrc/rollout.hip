@@ -392,8 +392,7 @@ void launch_nw(const RolloutArgs& a, hipStream_t s) {
   const size_t lds = rollout_lds<DT, ROWS>(a);
   const int nblk = (a.E + ROWS - 1) / ROWS;
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)rollout_kernel<DT, ROWS, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+    set_max_lds_once<rollout_kernel<DT, ROWS, NW>>(lds);
   hipLaunchKernelGGL((rollout_kernel<DT, ROWS, NW>), dim3(nblk), dim3(NW * 64), lds, s, a);
   HIP_CHECK_LAUNCH();
 }

@@ -229,11 +229,11 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
     else hipLaunchKernelGGL(wgrad_reg_kernel<DT_BF16>, dim3(a.ntasks), dim3(256), 0, s, a);
   } else if (dt == DT_F32) {
     const size_t lds = wgrad_lds_bytes<DT_F32>();
-    (void)hipFuncSetAttribute((const void*)wgrad_kernel<DT_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    set_max_lds_once<wgrad_kernel<DT_F32>>(lds);
     hipLaunchKernelGGL(wgrad_kernel<DT_F32>, dim3(a.ntasks), dim3(256), lds, s, a);
   } else {
     const size_t lds = wgrad_lds_bytes<DT_BF16>();
-    (void)hipFuncSetAttribute((const void*)wgrad_kernel<DT_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    set_max_lds_once<wgrad_kernel<DT_BF16>>(lds);
     hipLaunchKernelGGL(wgrad_kernel<DT_BF16>, dim3(a.ntasks), dim3(256), lds, s, a);
   }
   HIP_CHECK_LAUNCH();
