@@ -399,8 +399,8 @@ void launch_nw(const RolloutArgs& a, hipStream_t s) {
 
 template <int DT, int ROWS>
 void launch_t(const RolloutArgs& a, hipStream_t s) {
-  // fp32 operands: the 8-wave form spills (fp32 fragments are twice the registers)
-  if (g_rollout_waves == 4 || DT == DT_F32) launch_nw<DT, ROWS, 4>(a, s);
+  // fp32 operands and 32-env tiles: the 8-wave form spills (twice the fragment registers)
+  if (g_rollout_waves == 4 || DT == DT_F32 || ROWS > 16) launch_nw<DT, ROWS, 4>(a, s);
   else launch_nw<DT, ROWS, 8>(a, s);
 }
 
