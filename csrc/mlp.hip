@@ -235,6 +235,14 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_train_kernel(MlpArgs a) {
   constexpr int SNW = SPLIT ? 4 : NW;             // "waves" of a split call
   const int sw = SPLIT ? (wave & 3) : wave;       // wave index inside a split call
   const int sh = SPLIT ? (wave >> 2) * HR : 0;    // first row of this wave's half
+  // fc2 alone IS split at 8 waves: value fc2 has 4x the K of policy fc2, so with whole pairs
+  // four waves idle at the barrier; as (pair, row-half) items every wave takes one policy and
+  // one value half-pair (phase timeline: fc2 + barrier 18.1 k -> 16.1 k cycles per tile).
+  constexpr bool SPLIT2 = (NW == 8);
+  constexpr int HR2 = SPLIT2 ? ROWS / 2 : ROWS;
+  constexpr int SNW2 = SPLIT2 ? 4 : NW;
+  const int sw2 = SPLIT2 ? (wave & 3) : wave;
+  const int sh2 = SPLIT2 ? (wave >> 2) * HR2 : 0;
   load_rows<DT, NT>(reinterpret_cast<const T*>(a.x_buf), a.idx, a.row0, m0, nvalid, a.d_in[0], X, ldx, ROWS, tid,
                     [&] {
                       layer_prefetch<DT, HR, SNW>(pf_p, W + a.off_w[0], a.d_in[0], a.n_out[0], sw, lane);
@@ -259,8 +267,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_train_kernel(MlpArgs a) {
     layer_gemm<DT, ROWS, NW, EPI_TANH, true>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1v, ld1v, a.scale[3],
                                              wave, lane, h1vT, a.ldT, m0, VR, &pf_v);
   STAMP(2);
-  layer_prefetch<DT, HR, SNW>(pf_p, W + a.off_w[1], a.d_in[1], a.n_out[1], sw, lane);
-  layer_prefetch<DT, HR, SNW>(pf_v, W + a.off_w[4], a.d_in[4], a.n_out[4], sw, lane, SPLIT ? 0 : VR);
+  layer_prefetch<DT, HR2, SNW2>(pf_p, W + a.off_w[1], a.d_in[1], a.n_out[1], sw2, lane);
+  layer_prefetch<DT, HR2, SNW2>(pf_v, W + a.off_w[4], a.d_in[4], a.n_out[4], sw2, lane, SPLIT2 ? 0 : VR);
   __syncthreads();
   STAMP(3);
   // X is dead: preset the tiles that alias its region
@@ -270,10 +278,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_train_kernel(MlpArgs a) {
   zero_tile<DT>(DV, ldv, ROWS, tid, NT);
   __syncthreads();
   STAMP(4);
-  layer_gemm<DT, HR, SNW, EPI_TANH, true>(H1p + sh * ld1p, ld1p, a.d_in[1], W + a.off_w[1], a.n_out[1], H2p + sh * ld2p,
-                                          ld2p, a.scale[1], sw, lane, h2pT, a.ldT, m0 + sh, 0, &pf_p);
-  layer_gemm<DT, HR, SNW, EPI_TANH, true>(H1v + sh * ld1v, ld1v, a.d_in[4], W + a.off_w[4], a.n_out[4], H2v + sh * ld2v,
-                                          ld2v, a.scale[4], sw, lane, h2vT, a.ldT, m0 + sh, SPLIT ? 0 : VR, &pf_v);
+  layer_gemm<DT, HR2, SNW2, EPI_TANH, true>(H1p + sh2 * ld1p, ld1p, a.d_in[1], W + a.off_w[1], a.n_out[1],
+                                            H2p + sh2 * ld2p, ld2p, a.scale[1], sw2, lane, h2pT, a.ldT, m0 + sh2, 0,
+                                            &pf_p);
+  layer_gemm<DT, HR2, SNW2, EPI_TANH, true>(H1v + sh2 * ld1v, ld1v, a.d_in[4], W + a.off_w[4], a.n_out[4],
+                                            H2v + sh2 * ld2v, ld2v, a.scale[4], sw2, lane, h2vT, a.ldT, m0 + sh2,
+                                            SPLIT2 ? 0 : VR, &pf_v);
   STAMP(5);
   layer_prefetch<DT, ROWS, NW>(pf_p, W + a.off_w[2], a.d_in[2], A, wave, lane);
   layer_prefetch<DT, ROWS, NW>(pf_v, W + a.off_w[5], a.d_in[5], 1, wave, lane, VR);
