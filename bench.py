@@ -57,6 +57,8 @@ def main():
                     help="bucketed gradient all-reduce overlapping the wgrad (auto: multi-rank)")
     ap.add_argument("--force-collectives", action="store_true",
                     help="diagnostics: run the hot-path RCCL collectives even at world size 1")
+    ap.add_argument("--verify-sync", action="store_true",
+                    help="after the timed steps, check every rank holds bit-identical parameters")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -95,6 +97,13 @@ def main():
     torch.cuda.synchronize()
     el = torch.tensor([time.perf_counter() - t0], device=ctx.device, dtype=torch.float64)
     m = w.finish_metrics() or m
+    if args.verify_sync:
+        in_sync = ctx.verify_replicas(w.model.flat.data)
+        if ctx.rank == 0:
+            print(f"replicas_in_sync {in_sync}", file=sys.stderr, flush=True)
+        if not in_sync:
+            raise SystemExit("replicas diverged")
+    el = el.to(ctx.device)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     total_steps = rows * ctx.world_size * args.steps

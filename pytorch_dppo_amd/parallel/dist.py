@@ -157,12 +157,16 @@ def init_distributed(device: str = "cpu", rank: Optional[int] = None, world_size
             raise RuntimeError("device=gpu but no HIP device visible")
         torch.cuda.set_device(local_rank % ndev)
         dev = torch.device("cuda", local_rank % ndev)
-        backend = "nccl"
+        # DPPO_DIST_BACKEND=gloo: diagnostics only — several ranks sharing one GPU (RCCL refuses
+        # two ranks on one device), to exercise the multi-rank GPU engine path on a 1-GPU box
+        backend = os.environ.get("DPPO_DIST_BACKEND", "nccl")
     else:
         dev = torch.device("cpu")
         backend = "gloo"
     ctx = DistContext(rank=rank, world_size=world_size, local_rank=local_rank, backend=backend,
                       device=dev)
+    if backend not in ("nccl", "gloo"):
+        raise ValueError(f"unsupported backend {backend}")
     if world_size > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", master_addr)
         if master_port is not None:

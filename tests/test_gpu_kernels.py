@@ -504,3 +504,24 @@ def test_deferred_metrics_match_synchronous():
             a["mean_ep_return"] == b["mean_ep_return"]
         assert b["ms_update"] > 0 and b["steps_per_s"] > 0
     assert torch.equal(ws.model.flat.data, wd.model.flat.data)
+
+
+@pytest.mark.parametrize("extra", [[], ["--grad-buckets", "on", "--overlap-rollout"]])
+def test_two_ranks_on_one_gpu_stay_in_sync(extra):
+    """The multi-rank GPU engine path (one process per rank, flat-gradient all-reduce, obs-stat
+    merge, replicated Adam) with 2 ranks sharing the box's GPU: RCCL refuses two ranks on one
+    device, so the collectives run on gloo (DPPO_DIST_BACKEND=gloo, diagnostics only); the
+    ranks must end with bit-identical parameters (bench.py --verify-sync)."""
+    import os
+    import subprocess
+    import sys
+    from pytorch_dppo_amd.runtime.launcher import free_port
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DPPO_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--num-envs", "512", "--verify-sync"] + extra
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "replicas_in_sync True" in r.stderr, r.stderr[-2000:]
+    assert '"n_gpus": 2' in r.stdout
