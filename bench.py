@@ -15,7 +15,9 @@ grows (weak scaling).  Model: the reference actor-critic (model.py), random init
 operands with fp32 master weights/accumulation.
 
 Timing: W untimed warmup iterations; barrier + device sync; K timed iterations; barrier +
-device sync; the max over ranks of the elapsed time.  Rank 0 prints ONE JSON line.
+device sync; the max over ranks of the elapsed time.  Rank 0 prints ONE JSON line.  The
+per-phase HIP-event instrumentation of the worker is off by default here (--phase-timing N
+samples it): it is diagnostics, and each timed event record idles the GPU ~10 us.
 """
 import argparse
 import json
@@ -57,6 +59,9 @@ def main():
                     help="bucketed gradient all-reduce overlapping the wgrad (auto: multi-rank)")
     ap.add_argument("--force-collectives", action="store_true",
                     help="diagnostics: run the hot-path RCCL collectives even at world size 1")
+    ap.add_argument("--phase-timing", type=int, default=0,
+                    help="per-phase HIP-event timing every N iterations (0 = off: instrumentation only, "
+                         "each timed event record idles the GPU ~10 us)")
     ap.add_argument("--verify-sync", action="store_true",
                     help="after the timed steps, check every rank holds bit-identical parameters")
     ap.add_argument("--verbose", action="store_true")
@@ -75,7 +80,8 @@ def main():
     p = dppo_preset(device="gpu", env_name=args.env_name, num_envs=E, exploration_size=rows,
                     batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=args.dtype,
                     num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
-                    use_graphs=args.graphs, grad_buckets=args.grad_buckets)
+                    use_graphs=args.graphs, grad_buckets=args.grad_buckets,
+                    phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
     w = DPPOWorker(p, ctx)
     for i in range(args.warmup):
         m = w.iteration_step()

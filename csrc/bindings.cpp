@@ -406,6 +406,15 @@ void gae(torch::Tensor rewards, torch::Tensor values, torch::Tensor dones, torch
              ret.data_ptr<float>(), (int)T, (int)E, (float)gamma, (float)lam, (int)mode, cur_stream());
 }
 
+void metrics_pack(torch::Tensor ep, torch::Tensor loss8, torch::Tensor norm_part, torch::Tensor out) {
+  check(ep, "ep", at::kDouble, 2);
+  check(loss8, "loss8", at::kFloat, 8);
+  check(norm_part, "norm_part", at::kFloat, 1);
+  check(out, "out", at::kDouble, 11);
+  launch_metrics_pack(ep.data_ptr<double>(), loss8.data_ptr<float>(), norm_part.data_ptr<float>(),
+                      (int)norm_part.numel(), out.data_ptr<double>(), cur_stream());
+}
+
 void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, double lr, double b1, double b2,
           double eps, double max_norm, torch::Tensor state, torch::Tensor norm_part, torch::Tensor wimg,
           torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul, int64_t host_step) {
@@ -469,5 +478,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("obs_merge", &obs_merge);
   m.def("adam", &adam);
   m.def("pack", &pack);
+  m.def("metrics_pack", &metrics_pack);
   m.attr("arch") = "gfx950";
 }

@@ -136,6 +136,10 @@ void launch_obs_reduce(const float* part, int nblk, int O, double* s12, const fl
                        hipStream_t s);
 void launch_obs_merge(const double* s12, int O, double count, double n_a, const float* shift, double* mean,
                       double* m2, float* mean_f32, float* inv_std, double var_floor, hipStream_t s);
+// out f64[11] = [episode return sum, count | 8 loss sums | gradient L2 norm from the nblk
+// per-block sums of squares the last Adam launch left in norm_part]
+void launch_metrics_pack(const double* ep, const float* loss8, const float* norm_part, int nblk, double* out,
+                         hipStream_t s);
 }
 
 // output tile (square) of one wgrad task; operand buffers are padded to multiples of it

@@ -156,15 +156,16 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 }
 
 // No-clip Adam (the DPPO preset: chief.py:17 has no clipping): no norm is needed before the
-// update, so there is no sumsq pass (the reported norm of the last step is computed when the
-// metrics are staged, once per iteration).  The step number comes from the host (eager
+// update, so there is no sumsq pass; each block leaves the partial sum of squares of the
+// gradient it consumed in norm_part (fixed-order block tree), which metrics_pack sums once per
+// iteration for the reported gradient norm.  The step number comes from the host (eager
 // launches); block 0 mirrors it into state[0] for the device-counter path.  Graph replay keeps
 // the sumsq + adam pair, whose step counter lives on the device.
 template <int DT>
 __global__ __launch_bounds__(256) void adam_noclip_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                           float* __restrict__ m, float* __restrict__ v, int n,
                                                           float lr, float b1, float b2, float eps, float step,
-                                                          float* __restrict__ state,
+                                                          float* __restrict__ state, float* __restrict__ norm_part,
                                                           typename Prec<DT>::T* __restrict__ wimg,
                                                           const int* __restrict__ w_map,
                                                           const int* __restrict__ wt_map,
@@ -174,9 +175,12 @@ __global__ __launch_bounds__(256) void adam_noclip_kernel(float* __restrict__ p,
   const float bc2 = 1.f - powf(b2, step);
   const float step_size = lr / bc1;
   const float rbc2 = 1.f / sqrtf(bc2);
+  float ss = 0.f;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     float mi = m[i], vi = v[i];
-    const float pi = adam_elem(mi, vi, p[i], g[i], b1, b2, step_size, rbc2, eps);
+    const float gi = g[i];
+    ss = fmaf(gi, gi, ss);
+    const float pi = adam_elem(mi, vi, p[i], gi, b1, b2, step_size, rbc2, eps);
     m[i] = mi;
     v[i] = vi;
     p[i] = pi;
@@ -187,6 +191,14 @@ __global__ __launch_bounds__(256) void adam_noclip_kernel(float* __restrict__ p,
       wimg[wt_map[i]] = q;
     }
   }
+  __shared__ float red[256];
+  red[threadIdx.x] = ss;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) norm_part[blockIdx.x] = red[0];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     state[0] = step;
     state[1] = step;
@@ -210,6 +222,35 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ p, 
 }
 
 }  // namespace
+
+// Per-iteration metric staging in ONE launch (replaces ~6 small torch ops at the iteration tail):
+// out[0..1] = episode (return sum, count), out[2..9] = the 8 loss-term sums of the last
+// minibatch, out[10] = L2 norm of the last gradient, from the per-block sums of squares every
+// Adam path leaves in norm_part (fixed order: deterministic).
+__global__ __launch_bounds__(256) void metrics_pack_kernel(const double* __restrict__ ep,
+                                                           const float* __restrict__ loss8,
+                                                           const float* __restrict__ norm_part, int nblk,
+                                                           double* __restrict__ out) {
+  __shared__ double red[256];
+  const int t = threadIdx.x;
+  double s = 0.0;
+  for (int b = t; b < nblk; b += 256) s += (double)norm_part[b];
+  red[t] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  if (t == 0) out[10] = sqrt(red[0]);
+  if (t < 2) out[t] = ep[t];
+  if (t < 8) out[2 + t] = (double)loss8[t];
+}
+
+extern "C" void launch_metrics_pack(const double* ep, const float* loss8, const float* norm_part, int nblk,
+                                    double* out, hipStream_t s) {
+  hipLaunchKernelGGL(metrics_pack_kernel, dim3(1), dim3(256), 0, s, ep, loss8, norm_part, nblk, out);
+  HIP_CHECK_LAUNCH();
+}
 
 extern "C" void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
                            int T, int E, float gamma, float lam, int mode, hipStream_t s) {
@@ -235,13 +276,13 @@ extern "C" void launch_adam(float* p, const float* g, float* m, float* v, int n,
     const float step = (float)host_step;
     if (dt == DT_F32)
       hipLaunchKernelGGL(adam_noclip_kernel<DT_F32>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
-                         step, state, (float*)wimg, w_map, wt_map, img_scale);
+                         step, state, norm_part, (float*)wimg, w_map, wt_map, img_scale);
     else if (dt == DT_BF16)
       hipLaunchKernelGGL(adam_noclip_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
-                         step, state, (__bf16*)wimg, w_map, wt_map, img_scale);
+                         step, state, norm_part, (__bf16*)wimg, w_map, wt_map, img_scale);
     else
       hipLaunchKernelGGL(adam_noclip_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
-                         step, state, (uint8_t*)wimg, w_map, wt_map, img_scale);
+                         step, state, norm_part, (uint8_t*)wimg, w_map, wt_map, img_scale);
     HIP_CHECK_LAUNCH();
     return;
   }

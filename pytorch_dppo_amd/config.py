@@ -84,6 +84,8 @@ class Params:
     heartbeat_s: float = 0.0             # >0: per-rank heartbeat in the rendezvous store every N s
     heartbeat_timeout_s: float = 120.0   # a peer silent this long is reported dead and this rank exits
     check_finite: bool = False           # debug: stop with the failing phase when loss/params go non-finite
+    phase_timing: int = 1                # per-phase HIP-event timing every N iterations (0 = off; each
+                                         # event record idles the GPU ~10 us, see PhaseTimer)
 
     # ------------------------------------------------------------------------------------
     def __post_init__(self):

@@ -157,6 +157,7 @@ class HipEngine:
         self._loss_dev: Optional[torch.Tensor] = None
         self.local_stats: Optional[RunningObsStats] = None
         self.loss_sums = torch.zeros(NPART_FIXED, **f32)
+        self.metrics_buf = torch.zeros(2 + NPART_FIXED + 1, dtype=torch.float64, **dev)
         self.empty_x = torch.empty(0, dtype=self.sdtype, **dev)
         # the rollout can emit the full-batch x^T operand when the update is one full-batch step
         self.xT_from_rollout = (self.mb == self.N and self.ldT == self.N and E % 16 == 0 and self.N % 32 == 0
@@ -353,7 +354,7 @@ class HipEngine:
                 ep += self.epstat.double().sum(0)
         # everything stays on the device: no host sync inside the iteration
         return {"count": float(self.N), "s1": s1, "s2": s2, "shift": shift,
-                "ep_return_sum": ep[0], "ep_count": ep[1]}
+                "ep_return_sum": ep[0], "ep_count": ep[1], "ep2": ep}
 
     @torch.no_grad()
     def values(self) -> None:
@@ -371,7 +372,8 @@ class HipEngine:
             self.adv.sub_(m).div_(s + 1e-8)
 
     def begin_update(self) -> None:
-        self.log_std_old.copy_(self.model.flat.data[:self.A])
+        if self.p.loss == "dppo_ref":   # only the reference loss reads the previous log_std
+            self.log_std_old.copy_(self.model.flat.data[:self.A])
         self._first_step = True
 
     # ------------------------------------------------------------------------------------------
@@ -498,6 +500,18 @@ class HipEngine:
             self.no_q, host_step))
         self.adam_step += 1
         return None
+
+    def pack_metrics(self, ep2: torch.Tensor) -> Optional[torch.Tensor]:
+        """device f64[11] = [episode return sum, count | loss sums (8) | grad norm], written by ONE
+        launch (csrc/optim.hip metrics_pack, 256 threads over the Adam partials) instead of ~6
+        small torch ops per iteration; the buffer is reused (stream order keeps the previous D2H
+        copy ahead of the next pack)."""
+        if self._loss_dev is None:
+            return None
+        # every Adam path (fused no-clip, sumsq + clip, graph replay) leaves the per-block sums of
+        # squares of the gradient it applied in norm_part
+        self.ext.metrics_pack(ep2, self._loss_dev, self.norm_part, self.metrics_buf)
+        return self.metrics_buf
 
     def loss_vector(self) -> Optional[torch.Tensor]:
         """device [loss sums of the last minibatch (8) | grad norm of the last Adam step] — staged

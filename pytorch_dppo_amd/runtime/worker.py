@@ -105,6 +105,7 @@ class DPPOWorker:
         GPU still runs this update (no idle gap at the iteration boundary).  ``finish_metrics``
         resolves the last one."""
         p, eng, tm = self.p, self.engine, self.timer
+        tm.enabled = p.phase_timing > 0 and self.iteration % p.phase_timing == 0
         self.init_stats()
         t0 = time.perf_counter()
         tm.start("iteration")
@@ -192,13 +193,16 @@ class DPPOWorker:
         """Device-side metric values of this iteration -> one pinned host buffer (async)."""
         eng = self.engine
         dev = self.device
-        parts = [torch.stack([torch.as_tensor(ro["ep_return_sum"], dtype=torch.float64, device=dev).reshape(()),
-                              torch.as_tensor(ro["ep_count"], dtype=torch.float64, device=dev).reshape(())])]
-        parts[0] = self.ctx.allreduce_tensor_(parts[0])        # R5: episode stats over ranks
-        loss_dev = eng.loss_vector() if hasattr(eng, "loss_vector") else None
-        if loss_dev is not None:
-            parts.append(loss_dev.to(torch.float64))
-        flat = torch.cat([x.reshape(-1) for x in parts])
+        ep2 = ro.get("ep2")
+        flat = None
+        if ep2 is not None and hasattr(eng, "pack_metrics") and getattr(eng, "_loss_dev", None) is not None:
+            # GPU engine: all-reduce the [return sum, count] pair in place (R5), then one launch
+            # packs it with the loss sums and the gradient norm
+            flat = eng.pack_metrics(self.ctx.allreduce_tensor_(ep2))
+        if flat is not None:
+            loss_dev = flat
+        else:
+            flat, loss_dev = self._stage_parts(ro)
         if dev.type == "cuda":
             host = torch.empty(flat.numel(), dtype=torch.float64, pin_memory=True)
             host.copy_(flat, non_blocking=True)
@@ -209,6 +213,18 @@ class DPPOWorker:
         return {"host": host, "event": ev, "phases": self.timer.collect(), "has_loss": loss_dev is not None,
                 "iteration": self.iteration, "env_steps": self.env_steps, "updates": self.updates,
                 "host_s": time.perf_counter() - t0, "steps_local": steps_local}
+
+    def _stage_parts(self, ro: Dict):
+        """generic staging (CPU engine): [ep return sum, count] (+ loss vector) as one f64 tensor."""
+        eng = self.engine
+        dev = self.device
+        parts = [torch.stack([torch.as_tensor(ro["ep_return_sum"], dtype=torch.float64, device=dev).reshape(()),
+                              torch.as_tensor(ro["ep_count"], dtype=torch.float64, device=dev).reshape(())])]
+        parts[0] = self.ctx.allreduce_tensor_(parts[0])        # R5: episode stats over ranks
+        loss_dev = eng.loss_vector() if hasattr(eng, "loss_vector") else None
+        if loss_dev is not None:
+            parts.append(loss_dev.to(torch.float64))
+        return torch.cat([x.reshape(-1) for x in parts]), loss_dev
 
     def _resolve_metrics(self, st: Dict) -> Dict:
         p = self.p

@@ -506,6 +506,24 @@ def test_deferred_metrics_match_synchronous():
     assert torch.equal(ws.model.flat.data, wd.model.flat.data)
 
 
+@pytest.mark.parametrize("max_norm", [None, 0.5])
+def test_packed_metrics_match_torch(max_norm):
+    """One-launch metric staging (Adam's per-block sums of squares + loss sums + episode stats)
+    == the torch reductions of the same device state."""
+    from pytorch_dppo_amd.parallel.dist import DistContext
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    p = dppo_preset(device="gpu", env_name="Walker2d-v2", num_envs=64, exploration_size=64 * 4,
+                    batch_size=64 * 4, num_epoch=2, dtype="bf16", max_grad_norm=max_norm)
+    w = DPPOWorker(p, DistContext(device=DEV))
+    m = w.iteration_step()
+    eng = w.engine
+    gn = torch.linalg.vector_norm(eng.grad_flat.double()).item()
+    assert abs(m["grad_norm"] - gn) <= 1e-5 * max(gn, 1.0), (m["grad_norm"], gn)
+    ls = eng.loss_sums.double()
+    assert abs(m["loss_clip"] - (ls[0] / max(ls[5], 1)).item()) < 1e-9
+    assert torch.equal(eng.metrics_buf[:2], eng.ep_sum)
+
+
 @pytest.mark.parametrize("extra", [[], ["--grad-buckets", "on", "--overlap-rollout"]])
 def test_two_ranks_on_one_gpu_stay_in_sync(extra):
     """The multi-rank GPU engine path (one process per rank, flat-gradient all-reduce, obs-stat
