@@ -44,6 +44,48 @@ DEV float act_tanh(float x) {
 
 // k-steps per prefetch chunk: 2, so two register sets plus the cross-barrier BPre set stay
 // inside the 2-waves/SIMD VGPR budget at every row tile (4 spilled once BPre was added).
+// 4-wide tanh for the epilogues: f32x4 arithmetic lowers to packed 2-wide f32 VALU ops.
+template <int DT>
+DEV f32x4 act_tanh4(f32x4 x) {
+  if constexpr (DT == DT_F32) {
+    return f32x4{tanhf(x[0]), tanhf(x[1]), tanhf(x[2]), tanhf(x[3])};
+  } else {
+    const f32x4 y = x * (2.0f * 1.4426950408889634f);
+    f32x4 e;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_exp2f(y[i]);
+    e = e + 1.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_rcpf(e[i]);
+    return __builtin_elementwise_fma(e, f32x4{-2.f, -2.f, -2.f, -2.f}, f32x4{1.f, 1.f, 1.f, 1.f});
+  }
+}
+
+// f32x4 -> 4 storage elements (bf16: two v_cvt_pk_bf16_f32)
+template <int DT>
+DEV void cvt4(const f32x4& v, typename Prec<DT>::T (&q)[4]) {
+  using P = Prec<DT>;
+  if constexpr (DT == DT_BF16) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    *reinterpret_cast<bf16x4*>(q) = __builtin_convertvector(v, bf16x4);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = P::cvt(v[i]);
+  }
+}
+
+// 4 converted values -> 4 consecutive elements of a transposed (FM) operand row
+template <int DT>
+DEV void store4q_T(typename Prec<DT>::T* dst, const typename Prec<DT>::T (&q)[4]) {
+  if constexpr (DT == DT_F32) {
+    *reinterpret_cast<float4*>(dst) = make_float4(q[0], q[1], q[2], q[3]);
+  } else if constexpr (DT == DT_BF16) {
+    *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(q);
+  } else {
+    *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(q);
+  }
+}
+
 template <int DT, int RB> struct KChunk { static constexpr int KC = 2; };
 
 template <int DT>
@@ -168,6 +210,11 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
       }
     }
   };
+  // Epilogue of one tile pair: per (tile, row block) a lane holds 4 consecutive rows of one
+  // column.  The 4 values go through the activation with packed 2-wide f32 math (v_pk_mul /
+  // v_pk_add / v_pk_fma; exp2 / rcp stay scalar on the transcendental unit), are converted to
+  // the storage type ONCE, and that one conversion feeds both the LDS tile (2-byte row stores)
+  // and the 8-byte transposed wgrad-operand store.
   auto epilogue = [&](int nt0) {
     const bool two = (nt0 + 1) < ntiles;
 #pragma unroll
@@ -176,32 +223,45 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
       if (c < n_real && (t == 0 || two)) {
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
-          float vals[4];
+          const int r0 = rb * 16 + (lane >> 4) * 4;
+          f32x4 v = acc[t][rb];
+          if constexpr (DT == DT_FP8) v *= scale;   // e4m3 weight scale; 1 for bf16 / fp32
+          if constexpr (EPI == EPI_LINEAR_F32) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = rb * 16 + (lane >> 4) * 4 + i;
-            float v = acc[t][rb][i];
-            if constexpr (DT == DT_FP8) v *= scale;   // e4m3 weight scale; 1 for bf16 / fp32
+            for (int i = 0; i < 4; ++i) out[(r0 + i) * ldo + c] = v[i];
+          } else {
             if constexpr (EPI == EPI_TANH) {
-              v = act_tanh<DT>(v);
-              out[r * ldo + c] = P::cvt(v);
-            } else if constexpr (EPI == EPI_LINEAR_F32) {
-              out[r * ldo + c] = v;
-            } else if constexpr (EPI == EPI_LINEAR_T) {
-              out[r * ldo + c] = P::cvt(v);
-            } else if constexpr (EPI == EPI_DTANH_INPLACE) {  // out holds h = tanh(pre); dpre = v*(1-h^2)
-              const float h = P::tof(out[r * ldo + c]);
-              v = v * (1.0f - h * h);
-              out[r * ldo + c] = P::cvt(v);
-            } else {  // EPI_DTANH_GLOBAL
-              const float h = P::tof(out[r * ldo + c]);
+              v = act_tanh4<DT>(v);
+            } else if constexpr (EPI == EPI_DTANH_INPLACE || EPI == EPI_DTANH_GLOBAL) {
+              // out holds h = tanh(pre) of this layer's input; dpre = v * (1 - h^2)
+              f32x4 h;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) h[i] = P::tof(out[(r0 + i) * ldo + c]);
               v = v * (1.0f - h * h);
             }
-            vals[i] = v;
-          }
-          if (outT != nullptr) {  // FM wgrad operand: 4 consecutive m of feature c are contiguous
-            store4_T<DT>(outT + fm_index(c, m0 + rb * 16 + (lane >> 4) * 4, ldT), vals[0], vals[1], vals[2],
-                         vals[3]);
+            typename P::T q[4];
+            cvt4<DT>(v, q);
+            if constexpr (EPI != EPI_DTANH_GLOBAL) {
+              if constexpr (DT == DT_BF16) {
+                // 2-byte row stores straight from the two packed dwords (ds_write_b16 /
+                // ds_write_b16_d16_hi): no second per-value conversion
+                uint32_t wx = reinterpret_cast<const uint32_t*>(q)[0];
+                uint32_t wy = reinterpret_cast<const uint32_t*>(q)[1];
+                // opaque: otherwise LLVM folds trunc(cvt_pk(a, b)) back into a per-value cvt
+                asm volatile("" : "+v"(wx), "+v"(wy));
+                const uint2 w = make_uint2(wx, wy);
+                uint16_t* o16 = reinterpret_cast<uint16_t*>(out);
+                o16[(r0 + 0) * ldo + c] = (uint16_t)w.x;
+                o16[(r0 + 1) * ldo + c] = (uint16_t)(w.x >> 16);
+                o16[(r0 + 2) * ldo + c] = (uint16_t)w.y;
+                o16[(r0 + 3) * ldo + c] = (uint16_t)(w.y >> 16);
+              } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) out[(r0 + i) * ldo + c] = q[i];
+              }
+            }
+            if (outT != nullptr)   // FM wgrad operand: 4 consecutive m of feature c are contiguous
+              store4q_T<DT>(outT + fm_index(c, m0 + r0, ldT), q);
           }
         }
       }
