@@ -83,7 +83,8 @@ struct MlpArgs {
   int ldT;                // = M (row length of every transposed buffer)
   int xT_ready;           // 1: xT already holds this call's rows (full-batch: the rollout wrote it)
   int ablate;             // DIAGNOSTIC ONLY (scripts/ablate_train.py; 0 in every real run): bit0 no
-                          // transposed stores, bit1 skip v_fc1, bit2 skip dgrad chain, bit3 skip loss
+                          // transposed stores, bit1 skip v_fc1, bit2 skip dgrad chain, bit3 skip loss,
+                          // bit4 skip the observation loads (zero X tile)
   float* part;            // [nblk][NPART] per-workgroup partial sums (loss terms, dlog_std)
   int npart;
   // DIAGNOSTIC ONLY (scripts/phase_timeline.py; null in every real run): per-wave s_memtime

@@ -41,7 +41,8 @@ DEV float group_sum(float x) {
 // batch is in flight, so the HBM latency is paid once per tile instead of once per item.
 template <int DT, int NT, typename F>
 DEV void load_rows(const typename Prec<DT>::T* xb, const int* idx, int row0, int m0, int nvalid,
-                   int d, typename Prec<DT>::T* X, int ldx, int ROWS, int tid, F&& between) {
+                   int d, typename Prec<DT>::T* X, int ldx, int ROWS, int tid, F&& between,
+                   bool skip = false) {
   constexpr int E16 = 16 / Prec<DT>::BYTES;
   constexpr int B = 8;
   const int chunks = d / E16;
@@ -58,7 +59,7 @@ DEV void load_rows(const typename Prec<DT>::T* xb, const int* idx, int row0, int
       v[j] = make_uint4(0, 0, 0, 0);
       if (r < ROWS) {
         off[j] = r * ldx + c * E16;
-        if (r < nvalid) {
+        if (r < nvalid && !skip) {
           const int src = idx ? idx[m0 + r] : row0 + m0 + r;
           v[j] = *reinterpret_cast<const uint4*>(xb + (size_t)src * d + c * E16);
         }
@@ -114,8 +115,9 @@ DEV void write_transposed(const typename Prec<DT>::T* tile, int ld, int nfeat, v
     if constexpr (DT == DT_F32) {
       reinterpret_cast<uint4*>(o)[0] = reinterpret_cast<const uint4*>(buf)[0];
       reinterpret_cast<uint4*>(o)[1] = reinterpret_cast<const uint4*>(buf)[1];
-    } else if constexpr (DT == DT_BF16) {
-      *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(buf);
+    } else if constexpr (DT == DT_BF16) {   // streaming store: see store4q_T
+      typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(buf), reinterpret_cast<u32x4*>(o));
     } else {
       *reinterpret_cast<uint2*>(o) = *reinterpret_cast<const uint2*>(buf);
     }
@@ -249,7 +251,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_train_kernel(MlpArgs a) {
                       layer_prefetch<DT, ROWS, NW>(pf_v, W + a.off_w[3], a.d_in[3], a.n_out[3], wave, lane, VR);
                       preset_pad<DT>(H1p, ld1p, ROWS, a.n_out[0], tid, NT);
                       preset_pad<DT>(H1v, ld1v, ROWS, a.n_out[3], tid, NT);
-                    });
+                    },
+                    (a.ablate & 16) != 0);
   __syncthreads();
   STAMP(1);
   // ---------------- forward ----------------

@@ -74,33 +74,24 @@ DEV void cvt4(const f32x4& v, typename Prec<DT>::T (&q)[4]) {
   }
 }
 
-// 4 converted values -> 4 consecutive elements of a transposed (FM) operand row
+// 4 converted values -> 4 consecutive elements of a transposed (FM) operand row.  Non-temporal
+// (streaming) stores: the wgrad operands (~200 MB per epoch) are read back only by the next
+// kernel, long after they would have left L2, and with normal stores they evict the weight
+// images every layer re-reads from L2.
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+typedef __attribute__((ext_vector_type(4))) float f32x4s;
 template <int DT>
 DEV void store4q_T(typename Prec<DT>::T* dst, const typename Prec<DT>::T (&q)[4]) {
   if constexpr (DT == DT_F32) {
-    *reinterpret_cast<float4*>(dst) = make_float4(q[0], q[1], q[2], q[3]);
+    __builtin_nontemporal_store(f32x4s{q[0], q[1], q[2], q[3]}, reinterpret_cast<f32x4s*>(dst));
   } else if constexpr (DT == DT_BF16) {
-    *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(q);
+    __builtin_nontemporal_store(*reinterpret_cast<const u32x2*>(q), reinterpret_cast<u32x2*>(dst));
   } else {
-    *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(q);
+    __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(q), reinterpret_cast<uint32_t*>(dst));
   }
 }
 
 template <int DT, int RB> struct KChunk { static constexpr int KC = 2; };
-
-template <int DT>
-DEV void store4_T(typename Prec<DT>::T* dst, float v0, float v1, float v2, float v3) {
-  using P = Prec<DT>;
-  if constexpr (DT == DT_F32) {
-    *reinterpret_cast<float4*>(dst) = make_float4(v0, v1, v2, v3);
-  } else if constexpr (DT == DT_BF16) {
-    typename P::T t[4] = {P::cvt(v0), P::cvt(v1), P::cvt(v2), P::cvt(v3)};
-    *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(t);
-  } else {
-    typename P::T t[4] = {P::cvt(v0), P::cvt(v1), P::cvt(v2), P::cvt(v3)};
-    *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(t);
-  }
-}
 
 // B fragments of a wave's FIRST (tile pair, k-chunk) step of one layer_gemm call, loaded ahead
 // of time by layer_prefetch: weights do not depend on the previous layer, so their L2 latency

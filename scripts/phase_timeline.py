@@ -52,8 +52,10 @@ def main():
         for _ in range(3):
             eng.grad(None)
         ext.set_train_tstamp(buf, EVERY)
+        ext.set_train_ablation(int(os.environ.get("TIMELINE_ABLATE", "0")))   # diagnostics
         eng.grad(None)
         torch.cuda.synchronize()
+        ext.set_train_ablation(0)
         ext.set_train_tstamp(torch.empty(0, dtype=torch.int64, device=dev), 1)
         t = buf.view(-1, nw, 16).cpu().double()
         d = t[:, :, 1:13] - t[:, :, 0:12]              # [blk][wave][phase]
@@ -64,6 +66,29 @@ def main():
                                                         for i, ph in enumerate(PHASES)},
                "phases_median_cycles(mean over waves)": {ph: float(d[:, :, i].mean(dim=1).median())
                                                          for i, ph in enumerate(PHASES)}}
+        # per dispatch round (blocks b .. b + #CUs - 1 start together): is the x load slower in
+        # the first, lockstep round than in later ones?  (s_memtime is per XCD: compare within
+        # XCD = block % 8, relative to that XCD's first stamp.)
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        blk = torch.arange(t.shape[0]) * EVERY
+        rnd = blk // ncu
+        by_round = {}
+        for r_ in sorted(set(rnd.tolist())):
+            m = rnd == r_
+            by_round[int(r_)] = {"blocks": int(m.sum()),
+                                 "load_x": float(d[m, :, 0].max(dim=1).values.median()),
+                                 "fc1": float(d[m, :, 1].max(dim=1).values.median()),
+                                 "total": float(tot[m].median())}
+        res["by_round"] = by_round
+        start = t[:, 0, 0]
+        xcd = blk % 8
+        rel = torch.zeros_like(start)
+        for x_ in range(8):
+            m = xcd == x_
+            if m.any():
+                rel[m] = start[m] - start[m].min()
+        res["start_rel_cycles_by_round"] = {int(r_): [float(v) for v in rel[rnd == r_].quantile(
+            torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64))] for r_ in sorted(set(rnd.tolist()))}
         out[f"rows{rows}"] = res
     ext.set_mlp_rows(0)
     # rollout: per-wave cycles per phase summed over the T steps, median over workgroups
