@@ -35,6 +35,8 @@ DEV float group_sum(float x) {
   return x;
 }
 
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
 // Gather ROWS rows of the [*][d] observation buffer into the LDS tile X (row stride ldx).
 // Loads go out in batches of B per thread and ALL of a batch's loads are issued before any
 // of its LDS stores; `between()` (LDS presets that do not depend on X) runs while the first
@@ -61,7 +63,9 @@ DEV void load_rows(const typename Prec<DT>::T* xb, const int* idx, int row0, int
         off[j] = r * ldx + c * E16;
         if (r < nvalid && !skip) {
           const int src = idx ? idx[m0 + r] : row0 + m0 + r;
-          v[j] = *reinterpret_cast<const uint4*>(xb + (size_t)src * d + c * E16);
+          // streaming load: each observation row is read once per kernel, keep L2 for weights
+          const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xb + (size_t)src * d + c * E16));
+          v[j] = make_uint4(t.x, t.y, t.z, t.w);
         }
       }
       r += step_r;
@@ -116,7 +120,6 @@ DEV void write_transposed(const typename Prec<DT>::T* tile, int ld, int nfeat, v
       reinterpret_cast<uint4*>(o)[0] = reinterpret_cast<const uint4*>(buf)[0];
       reinterpret_cast<uint4*>(o)[1] = reinterpret_cast<const uint4*>(buf)[1];
     } else if constexpr (DT == DT_BF16) {   // streaming store: see store4q_T
-      typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
       __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(buf), reinterpret_cast<u32x4*>(o));
     } else {
       *reinterpret_cast<uint2*>(o) = *reinterpret_cast<const uint2*>(buf);
