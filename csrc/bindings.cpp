@@ -314,21 +314,25 @@ void set_mlp_rows(int64_t rows) {
 void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor> xT, std::vector<int64_t> g_rows,
            std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab) {
   TORCH_CHECK(gT.size() == 6 && xT.size() == 6 && g_rows.size() == 6 && x_rows.size() == 6, "6 layers");
-  check(tasks, "tasks", at::kInt, 6);
-  TORCH_CHECK(tasks.numel() % 6 == 0, "tasks are 6-int records");
+  check(tasks, "tasks", at::kInt, WGRAD_TASK_INTS);
+  TORCH_CHECK(tasks.numel() % WGRAD_TASK_INTS == 0, "tasks are 8-int records");
   TORCH_CHECK(!tasks_host.is_cuda() && tasks_host.numel() == tasks.numel(), "tasks_host must mirror tasks on CPU");
-  const int ntasks = (int)(tasks.numel() / 6);
+  const int ntasks = (int)(tasks.numel() / WGRAD_TASK_INTS);
   auto th = tasks_host.contiguous();
   const int* tp = th.data_ptr<int>();
   int64_t slab_need = 0;
   for (int i = 0; i < ntasks; ++i) {
-    const int* t = tp + 6 * i;
+    const int* t = tp + WGRAD_TASK_INTS * i;
     TORCH_CHECK(t[0] >= 0 && t[0] < 6, "task layer");
-    TORCH_CHECK(t[1] + WGRAD_TILE <= g_rows[t[0]] && t[2] + WGRAD_TILE <= x_rows[t[0]], "task tile beyond operand rows");
+    const int nq = t[6], kq = t[7];
+    TORCH_CHECK(nq >= 1 && kq >= 1 && nq * kq <= 8 && nq + kq <= 6, "task quadrants: nq*kq <= 8, nq+kq <= 6");
+    TORCH_CHECK(t[1] >= 0 && t[2] >= 0 && t[1] % 16 == 0 && t[2] % 16 == 0, "task tile origin");
+    TORCH_CHECK(t[1] + 64 * nq <= g_rows[t[0]] && t[2] + 64 * kq <= x_rows[t[0]], "task tile beyond operand rows");
     // the kernel consumes 32-row k-steps in pairs: every range is a positive multiple of 64 rows
     TORCH_CHECK(t[3] >= 0 && t[4] <= ld && t[4] > t[3] && (t[4] - t[3]) % 64 == 0 && t[3] % 32 == 0,
                 "task batch range (must be a positive multiple of 64 rows)");
-    slab_need = std::max<int64_t>(slab_need, (int64_t)t[5] + WGRAD_TILE * WGRAD_TILE);
+    TORCH_CHECK(t[5] >= 0, "task slab offset");
+    slab_need = std::max<int64_t>(slab_need, (int64_t)t[5] + (int64_t)(64 * nq) * (64 * kq));
   }
   check(slab, "slab", at::kFloat, slab_need);
   WgradArgs a{};
@@ -473,6 +477,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gae", &gae);
   m.def("set_train_ablation", &set_train_ablation);
   m.def("set_wgrad_impl", &set_wgrad_impl);
+  m.def("set_wgrad_stages", [](int64_t st) { set_wgrad_stages((int)st); });
   m.def("set_adam_fused", [](int64_t on) { set_adam_fused((int)on); });
   m.def("obs_reduce", &obs_reduce);
   m.def("obs_merge", &obs_merge);

@@ -97,7 +97,8 @@ struct WgradTask {
   int layer;      // 0..5
   int n0, k0;     // output tile origin
   int m0, m1;     // reduction (batch) range
-  int slab;       // slab offset (floats) of this task's 64x64 tile
+  int slab;       // slab offset (floats) of this task's [nq*64][kq*64] tile
+  int nq, kq;     // tile extent in 64x64 quadrants (one per wave): nq*kq <= 8, nq + kq <= 6
 };
 
 struct WgradArgs {
@@ -119,6 +120,7 @@ size_t mlp_train_lds_bytes(int dt, const MlpArgs& a);
 int mlp_train_rows(int dt, const MlpArgs& a);   // row tile the launcher will use (LDS-fit)
 void set_mlp_rows_override(int rows);           // 0 auto; 16/32/64 force (A/B diagnostics)
 void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
+void set_wgrad_stages(int st);                 // bf16 wgrad DMA ring depth 3 / 4 / 6 (A/B)
 // grad[i] for i in [i_lo, i_hi) from the slabs; with_partials: also log_std grads [0, A) and the
 // 8 loss sums from the per-workgroup partials
 void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int chunk_stride,
@@ -143,5 +145,7 @@ void launch_metrics_pack(const double* ep, const float* loss8, const float* norm
                          hipStream_t s);
 }
 
-// output tile (square) of one wgrad task; operand buffers are padded to multiples of it
+// operand buffers (feature-major) are padded to multiples of 128 rows
 #define WGRAD_TILE 128
+#define WGRAD_TASK_INTS 8
+static_assert(sizeof(WgradTask) == WGRAD_TASK_INTS * sizeof(int), "WgradTask is an 8-int record");

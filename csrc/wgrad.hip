@@ -3,24 +3,33 @@
 //   dW_aug[n][k] = sum_m dY[m][n] * X[m][k]      (k == K is the bias column: X^T row K == 1)
 //
 // Both operands are feature-major (written transposed by mlp_train_kernel), so every MFMA
-// fragment is one 16-byte load along m, the reduction axis.  A task = (layer, 128x128 output
-// tile, batch chunk); each of the 4 waves owns a 64x64 quadrant = 4x4 tiles of 16x16 MFMA
-// (64 f32 accumulator registers), so one k-step issues 8 fragment loads for 16 MFMAs.
-// Results go to per-chunk fp32 slabs that grad_gather sums in a fixed order —
-// deterministic, no float atomics (SURVEY §7.4 hard part 2).
+// fragment is one 16-byte load along m, the reduction axis.  A task = (layer, output tile,
+// batch chunk).  The tile is nq x kq QUADRANTS of 64x64 (nq * kq <= 8, nq + kq <= 6), one per
+// wave of the 8-wave workgroup; each quadrant = 4x4 MFMA tiles of 16x16 (64 f32 accumulator
+// registers).  The host plan picks (nq, kq) per layer to minimise operand rows read per
+// k-step: the kernel is bound by the operand stream (HBM / MALL), and a 256x128 tile reads
+// 384 rows per step for 2x the outputs of a 128x128 tile's 256 (v_fc1: 2304 instead of 3072
+// rows per step).  Results go to per-chunk fp32 slabs ([nq*64][kq*64] per task) that
+// grad_gather sums in a fixed order — deterministic, no float atomics (SURVEY §7.4 part 2).
 #include "kernels.h"
 #include "mlp_core.h"
 
 namespace {
 
+constexpr int WG_WAVES = 8;
+
+// register-streamed variant (A/B diagnostics; the LDS-DMA kernel below is the default): each
+// active wave loads its own 4 + 4 fragments per k-step straight into registers
 template <int DT>
-__global__ __launch_bounds__(256) void wgrad_reg_kernel(WgradArgs a) {
+__global__ __launch_bounds__(WG_WAVES * 64) void wgrad_reg_kernel(WgradArgs a) {
   using P = Prec<DT>;
   using T = typename P::T;
   using Frag = typename P::Frag;
   const WgradTask tk = a.tasks[blockIdx.x];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave >> 1, wk = wave & 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (wave >= tk.nq * tk.kq) return;          // no barriers in this kernel
+  const int wn = wave / tk.kq, wk = wave - wn * tk.kq;
   const T* g = reinterpret_cast<const T*>(a.gT[tk.layer]);
   const T* x = reinterpret_cast<const T*>(a.xT[tk.layer]);
   // operands are fragment-major (FM): the fragment of (row tile, k-step) is 512 contiguous
@@ -36,9 +45,7 @@ __global__ __launch_bounds__(256) void wgrad_reg_kernel(WgradArgs a) {
   // Two register slots in ping-pong, the loop unrolled by two so each slot keeps fixed
   // registers (no copies).  Every prefetch is unconditional (clamped to the last step; its
   // data unused) and every MFMA in the loop is unconditional, so the number of loads in flight
-  // is path-independent and the compiler's waits stay partial (vmcnt(8): the next step's loads
-  // remain in flight while this step's MFMAs run).  The copy-rotation form this replaces
-  // drained vmcnt(0) at the top of every step.
+  // is path-independent and the compiler's waits stay partial.
   const int nk = (tk.m1 - tk.m0) >> 5;
   struct Slot { Frag a[4], b[4]; };
   auto fetch = [&](Slot& d, int k) {
@@ -58,8 +65,6 @@ __global__ __launch_bounds__(256) void wgrad_reg_kernel(WgradArgs a) {
   // the host plan makes every chunk a multiple of 64 rows (two steps; checked in bindings.cpp)
   Slot r0, r1;
   fetch(r0, 0);
-  // sched_barrier pins the order "issue next step's loads, then this step's MFMAs" (the
-  // scheduler otherwise sinks each load next to its first use, which serialises on latency)
   for (int k = 0; k < nk; k += 2) {
     fetch(r1, k + 1);
     __builtin_amdgcn_sched_barrier(0);
@@ -70,34 +75,37 @@ __global__ __launch_bounds__(256) void wgrad_reg_kernel(WgradArgs a) {
     mma(r1);
     __builtin_amdgcn_sched_barrier(0);
   }
-  const int lr = lane & 15;
+  const int KE = tk.kq * 64;
   float* out = a.slab + tk.slab;
-  const int col = wk * 64 + lr;
+  const int col = wk * 64 + (lane & 15);
   const int rbase = wn * 64 + (lane >> 4) * 4;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * WGRAD_TILE + col + 16 * j] = acc[i][j][q];
+      for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * KE + col + 16 * j] = acc[i][j][q];
 }
 
 // ---- LDS-DMA staged variant (default) ----------------------------------------------------
-// The register-streamed kernel above is L2->CU bandwidth bound: each of the 4 waves loads its
-// own 64-row A and B fragments, so the WG moves 32 KiB per k-step for 16 KiB of distinct data
-// (measured ~11 TB/s of L2->CU traffic, near the ~34 TB/s chip ceiling at its occupancy).
-// Here the WG stages each k-step's 16 distinct fragments (8 of dY^T, 8 of X^T, 1 KiB each at
-// bf16) ONCE into LDS with global_load_lds_dwordx4: an FM fragment is 64 lanes x 16 B in lane
-// order, exactly the lane-linear image glds writes, so each fragment is one DMA instruction and
-// the fragment reads are conflict-free ds_read_b128 at lane*16.  WG_STAGES-deep ring, counted
-// vmcnt and a raw s_barrier keep WG_STAGES-1 steps of DMA in flight across the barrier
-// (cdna_hip_programming.md 'Pipelining across barriers'): no VGPRs hold in-flight data.
-template <int DT> struct WgStages { static constexpr int S = (DT == DT_F32) ? 3 : 4; };
+// The workgroup stages each k-step's distinct fragments (4*nq of dY^T, 4*kq of X^T; 1 KiB
+// each at bf16) ONCE into LDS with global_load_lds_dwordx4: an FM fragment is 64 lanes x 16 B
+// in lane order, exactly the lane-linear image the DMA writes, so each fragment is one DMA
+// instruction and the fragment reads are conflict-free ds_read_b128 at lane*16.  Each wave
+// DMAs C fixed slots per stage (C = 2 when the task has <= 16 fragments, else 3; slots past
+// the task's fragment count re-load one of its fragments, an L2 hit, so every wave's DMA count
+// — and with it the vmcnt arithmetic — is task-independent).  S-deep ring, counted vmcnt and a
+// raw s_barrier keep S-1 steps of DMA in flight across the barrier (cdna_hip_programming.md
+// 'Pipelining across barriers'): no VGPRs hold in-flight data.
+constexpr int WG_SLOTS = 24;   // fragment slots per stage: (nq + kq) * 4 <= 24
 
 template <int DT>
 constexpr int wgrad_frag_bytes() { return 512 * Prec<DT>::BYTES; }
-template <int DT>
-constexpr size_t wgrad_lds_bytes() { return (size_t)WgStages<DT>::S * 16 * wgrad_frag_bytes<DT>(); }
+template <int DT, int S>
+constexpr size_t wgrad_lds_bytes() { return (size_t)S * WG_SLOTS * wgrad_frag_bytes<DT>(); }
+// ring depth of the bf16 kernel (A/B knob set_wgrad_stages): 3 (72 KiB, two workgroups per
+// CU), 4 (96 KiB) or 6 (144 KiB; five steps = 120 KiB of DMA in flight per CU)
+int g_wgrad_stages = 4;
 
 DEV void glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -108,42 +116,44 @@ DEV void glds16(const void* g, void* lds) {
 // lgkmcnt[11:8]=15 | vmcnt[5:4] in [15:14])
 #define WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt((((n) & 15) | (7 << 4) | (15 << 8) | ((((n) >> 4) & 3) << 14)))
 
-template <int DT>
-__global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
+template <int DT, int S, int C>
+DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   using P = Prec<DT>;
   using T = typename P::T;
   using Frag = typename P::Frag;
-  constexpr int S = WgStages<DT>::S;
   constexpr int FB = wgrad_frag_bytes<DT>();     // bytes per fragment
-  constexpr int NI = FB / 1024;                  // glds instructions per fragment (64 lanes x 16 B)
-  constexpr int SB = 16 * FB;                    // bytes per stage
-  extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
-  const WgradTask tk = a.tasks[blockIdx.x];
+  constexpr int NI = FB / 1024;                  // DMA instructions per fragment (64 lanes x 16 B)
+  constexpr int SB = WG_SLOTS * FB;              // bytes per stage
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave >> 1, wk = wave & 1;
   const char* g = reinterpret_cast<const char*>(a.gT[tk.layer]);
   const char* x = reinterpret_cast<const char*>(a.xT[tk.layer]);
   const int nk = (tk.m1 - tk.m0) >> 5;
   const int ks0 = tk.m0 >> 5;
-  // fragment f of a stage: f < 8 -> dY^T row tile n0/16 + f, else X^T row tile k0/16 + f - 8.
-  // Wave w DMAs fragments 4w .. 4w+3 of every stage.
-  const char* src[4];
+  const int NF = 4 * tk.nq, F = NF + 4 * tk.kq;
+  // slot f of a stage holds fragment f: f < NF -> dY^T row tile n0/16 + f, else X^T row tile
+  // k0/16 + f - NF.  Wave w DMAs slots C*w .. C*w + C-1 (a slot >= F re-loads fragment f - F).
+  const char* src[C];
+  int dst[C];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int f = wave * 4 + q;
-    src[q] = (f < 8) ? g + fm_frag((tk.n0 >> 4) + f, ks0, a.ld, 0) * sizeof(T)
-                     : x + fm_frag((tk.k0 >> 4) + f - 8, ks0, a.ld, 0) * sizeof(T);
+  for (int q = 0; q < C; ++q) {
+    const int f = wave * C + q;
+    const int ff = f < F ? f : f - F;
+    src[q] = (ff < NF) ? g + fm_frag((tk.n0 >> 4) + ff, ks0, a.ld, 0) * sizeof(T)
+                       : x + fm_frag((tk.k0 >> 4) + ff - NF, ks0, a.ld, 0) * sizeof(T);
+    dst[q] = f * FB;
   }
   auto issue = [&](int k) {
     const int kk = min(k, nk - 1);            // past the end: re-load valid data (count stays fixed)
     char* st = smem + (k % S) * SB;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < C; ++q)
 #pragma unroll
       for (int h = 0; h < NI; ++h)
-        glds16(src[q] + (size_t)kk * FB + h * 1024 + lane * 16, st + (wave * 4 + q) * FB + h * 1024);
+        glds16(src[q] + (size_t)kk * FB + h * 1024 + lane * 16, st + dst[q] + h * 1024);
   };
+  const bool active = wave < tk.nq * tk.kq;
+  const int wn = wave / tk.kq, wk = wave - (wave / tk.kq) * tk.kq;
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -152,22 +162,26 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 #pragma unroll
   for (int s = 0; s < S - 1; ++s) issue(s);
   for (int k = 0; k < nk; ++k) {
-    WAIT_VMCNT(4 * NI * (S - 2));             // this wave's part of stage k has landed
+    WAIT_VMCNT(C * NI * (S - 2));             // this wave's part of stage k has landed
     __builtin_amdgcn_s_barrier();              // ... everyone's; and stage k-1 is no longer read
     issue(k + S - 1);                          // refill the slot stage k-1 used
-    const char* st = smem + (k % S) * SB;
-    Frag af[4], bf[4];
+    if (active) {
+      const char* st = smem + (k % S) * SB;
+      Frag af[4], bf[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      af[i] = P::load(reinterpret_cast<const T*>(st + (wn * 4 + i) * FB) + lane * 8);
-      bf[i] = P::load(reinterpret_cast<const T*>(st + (8 + wk * 4 + i) * FB) + lane * 8);
+      for (int i = 0; i < 4; ++i) {
+        af[i] = P::load(reinterpret_cast<const T*>(st + (wn * 4 + i) * FB) + lane * 8);
+        bf[i] = P::load(reinterpret_cast<const T*>(st + (NF + wk * 4 + i) * FB) + lane * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(acc[i][j], af[i], bf[j]);
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(acc[i][j], af[i], bf[j]);
   }
   WAIT_VMCNT(0);                               // no DMA may outlive the workgroup's LDS
+  if (!active) return;
+  const int KE = tk.kq * 64;
   float* out = a.slab + tk.slab;
   const int col = wk * 64 + (lane & 15);
   const int rbase = wn * 64 + (lane >> 4) * 4;
@@ -176,7 +190,22 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * WGRAD_TILE + col + 16 * j] = acc[i][j][q];
+      for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * KE + col + 16 * j] = acc[i][j][q];
+}
+
+template <int DT, int S>
+__global__ __launch_bounds__(WG_WAVES * 64) void wgrad_kernel(WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
+  const WgradTask tk = a.tasks[blockIdx.x];
+  if (4 * (tk.nq + tk.kq) <= 2 * WG_WAVES) wgrad_lds_body<DT, S, 2>(a, tk, smem);
+  else wgrad_lds_body<DT, S, 3>(a, tk, smem);
+}
+
+template <int DT, int S>
+void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
+  const size_t lds = wgrad_lds_bytes<DT, S>();
+  set_max_lds_once<wgrad_kernel<DT, S>>(lds);
+  hipLaunchKernelGGL((wgrad_kernel<DT, S>), dim3(a.ntasks), dim3(WG_WAVES * 64), lds, s, a);
 }
 
 // With the partials pass (nred = A + 8 > 0):
@@ -222,19 +251,22 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
 
 }  // namespace
 
+extern "C" void set_wgrad_stages(int st) { g_wgrad_stages = (st == 3 || st == 6) ? st : 4; }
+
 extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
   if (a.ntasks <= 0) return;
+  const dim3 block(WG_WAVES * 64);
   if (a.impl == 1) {
-    if (dt == DT_F32) hipLaunchKernelGGL(wgrad_reg_kernel<DT_F32>, dim3(a.ntasks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(wgrad_reg_kernel<DT_BF16>, dim3(a.ntasks), dim3(256), 0, s, a);
+    if (dt == DT_F32) hipLaunchKernelGGL(wgrad_reg_kernel<DT_F32>, dim3(a.ntasks), block, 0, s, a);
+    else hipLaunchKernelGGL(wgrad_reg_kernel<DT_BF16>, dim3(a.ntasks), block, 0, s, a);
   } else if (dt == DT_F32) {
-    const size_t lds = wgrad_lds_bytes<DT_F32>();
-    set_max_lds_once<wgrad_kernel<DT_F32>>(lds);
-    hipLaunchKernelGGL(wgrad_kernel<DT_F32>, dim3(a.ntasks), dim3(256), lds, s, a);
+    launch_wgrad_lds<DT_F32, 3>(a, s);
+  } else if (g_wgrad_stages == 3) {
+    launch_wgrad_lds<DT_BF16, 3>(a, s);
+  } else if (g_wgrad_stages == 6) {
+    launch_wgrad_lds<DT_BF16, 6>(a, s);
   } else {
-    const size_t lds = wgrad_lds_bytes<DT_BF16>();
-    set_max_lds_once<wgrad_kernel<DT_BF16>>(lds);
-    hipLaunchKernelGGL(wgrad_kernel<DT_BF16>, dim3(a.ntasks), dim3(256), lds, s, a);
+    launch_wgrad_lds<DT_BF16, 4>(a, s);
   }
   HIP_CHECK_LAUNCH();
 }

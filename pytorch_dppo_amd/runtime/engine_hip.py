@@ -30,9 +30,33 @@ from ..utils.obs_stats import RunningObsStats
 
 STORAGE = {0: torch.float32, 1: torch.bfloat16, 2: torch.uint8}
 NPART_FIXED = 8
-WT = 128            # wgrad output tile (csrc/kernels.h WGRAD_TILE)
+WT = 128            # operand-buffer row padding (csrc/kernels.h WGRAD_TILE)
+
+
+def wgrad_tiles(li: int, n: int, k: int):
+    """Output tiles of one layer's weight gradient ([n][k], k including the bias column) for the
+    wgrad kernel: (layer, n0, k0, nq, kq), a tile = nq x kq quadrants of 64x64, one per wave of
+    the 8-wave workgroup (nq*kq <= 8, nq + kq <= 6).  The kernel streams (nq + kq) * 64 operand
+    rows per 32-row k-step, so the (nq, kq) minimising the layer's total rows read wins (ties:
+    fewer tasks, then wider n).  Humanoid v_fc1 (512 x 377): 4x2 tiles, 2304 rows per step
+    instead of 3072 with 128x128 tiles."""
+    N, K = -(-n // 64), -(-k // 64)
+    best = None
+    for nq in range(1, 9):
+        for kq in range(1, 9):
+            if nq * kq > 8 or nq + kq > 6 or nq > N or kq > K:
+                continue
+            tl = []
+            for a in range(0, N, nq):
+                for b in range(0, K, kq):
+                    tl.append((li, a * 64, b * 64, min(nq, N - a), min(kq, K - b)))
+            cost = sum(t[3] + t[4] for t in tl)
+            key = (cost, len(tl), -nq)
+            if best is None or key < best[0]:
+                best = (key, tl)
+    return best[1]
 ROLL_ROWS = 16
-WGRAD_TARGET_WGS = 256   # A/B (scripts/ab_kernels.py): 256 <= 512 <= 1024 us per grad step
+WGRAD_TARGET_WGS = 208   # Humanoid: 13 tiles x 16 chunks (A/B: 16 chunks beat 24-40 by ~6 %)
 
 
 def _r(x: int, m: int) -> int:
@@ -175,8 +199,9 @@ class HipEngine:
 
     # ------------------------------------------------------------------------------------------
     def _build_wgrad_plan(self, model: ActorCritic, target_wgs: Optional[int] = None,
-                          split: Optional[bool] = None) -> None:
-        """Task lists of the grouped split-K wgrad launches: (layer, 128x128 tile, batch chunk).
+                          split: Optional[bool] = None, chunks_override: Optional[int] = None) -> None:
+        """Task lists of the grouped split-K wgrad launches: (layer, output tile, batch chunk),
+        output tiles from wgrad_tiles().
 
         One *bucket* = one wgrad launch + one grad_gather launch over a contiguous flat range of
         the gradient.  Unbucketed (default): every layer in one bucket.  ``split`` (bucketed
@@ -202,30 +227,31 @@ class HipEngine:
         src = torch.full((model.num_params,), -1, dtype=torch.int64)
         self.buckets = []
         for bi, (layers, (lo, hi)) in enumerate(zip(groups, ranges)):
-            tiles = []  # (layer, n0, k0)
+            tiles = []  # (layer, n0, k0, nq, kq)
             for li in layers:
                 l = ls[li]
-                for n0 in range(0, l.fan_out, WT):
-                    for k0 in range(0, l.fan_in + 1, WT):
-                        tiles.append((li, n0, k0))
+                tiles += wgrad_tiles(li, l.fan_out, l.fan_in + 1)
             ntiles = len(tiles)
             max_chunks = max(1, self.ldT // 256)
             # the small policy bucket: half the workgroups (its gather sums every chunk's slab)
             tw = target_wgs if bi == 0 else max(64, target_wgs // 2)
             want = -(-tw // ntiles)                   # >= ~tw workgroups in flight
             want = -(-want // 8) * 8                  # whole chunks per XCD (8 XCDs)
+            if chunks_override:                       # A/B diagnostics
+                want = chunks_override
             nchunks = max(1, min(max_chunks, want))
             mc = _r(-(-self.ldT // nchunks), 64)   # even number of 32-row k-steps per task
             chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
-            chunk_stride = ntiles * WT * WT
-            tile_off = {t: i * WT * WT for i, t in enumerate(tiles)}
+            sizes = [t[3] * t[4] * 64 * 64 for t in tiles]
+            chunk_stride = sum(sizes)
+            tile_off = {t: sum(sizes[:i]) for i, t in enumerate(tiles)}
             # XCD-aware order: workgroups b, b+8, b+16, ... are dealt to the same XCD (observed
             # round-robin placement; speed only), so all tiles of a batch chunk — which share the
             # chunk's operand rows — are given consecutive slots of ONE XCD and hit its L2.
             per_xcd = [[] for _ in range(8)]
             for ci, (m0, m1) in enumerate(chunks):
                 for t in tiles:
-                    per_xcd[ci % 8].append([t[0], t[1], t[2], m0, m1, ci * chunk_stride + tile_off[t]])
+                    per_xcd[ci % 8].append([t[0], t[1], t[2], m0, m1, ci * chunk_stride + tile_off[t], t[3], t[4]])
             tasks = []
             j = 0
             while any(j < len(q) for q in per_xcd):
@@ -254,13 +280,15 @@ class HipEngine:
 
     @staticmethod
     def _slab_index(tile_off, li, n, k):
-        nt, kt = int(n.max()) // WT + 1, int(k.max()) // WT + 1
-        lut = torch.zeros(nt, kt, dtype=torch.int64)
-        for a in range(nt):
-            for b in range(kt):
-                lut[a, b] = tile_off.get((li, a * WT, b * WT), -1)
-        base = lut[n // WT, k // WT]
-        return base + (n % WT) * WT + (k % WT)
+        """slab offset of dW[n][k] of layer li: tile base + (n - n0) * (kq * 64) + (k - k0)"""
+        out = torch.full_like(n, -1)
+        for (tl, n0, k0, nq, kq), base in tile_off.items():
+            if tl != li:
+                continue
+            m = (n >= n0) & (n < n0 + 64 * nq) & (k >= k0) & (k < k0 + 64 * kq)
+            out[m] = base + (n[m] - n0) * (64 * kq) + (k[m] - k0)
+        assert bool((out >= 0).all()), "wgrad tiles do not cover the layer"
+        return out
 
     # ------------------------------------------------------------------------------------------
     def sync_tile(self) -> None:

@@ -55,7 +55,8 @@ def main():
         eng.sync_tile()
 
     def knobs(adam=1, wgrad=0, r=0):   # every arm sets every knob (no state leaks between arms)
-        return lambda: (ext.set_adam_fused(adam), ext.set_wgrad_impl(wgrad), rows(r))
+        return lambda: (ext.set_adam_fused(adam), ext.set_wgrad_impl(wgrad), rows(r), ext.set_wgrad_stages(4),
+                        eng._build_wgrad_plan(model))
 
     arms = {
         "adam_fused": (knobs(adam=1), eng.apply),
@@ -72,6 +73,16 @@ def main():
     for t in (1024, 512, 256, 100):
         arms[f"grad_wgrad_wgs{t}"] = ((lambda t=t: (knobs()(), eng._build_wgrad_plan(model, t))),
                                       lambda: eng.grad(None))
+    # wgrad DMA ring depth x batch chunks (tasks = chunks x tiles per chunk)
+    for st in (3, 4, 6):
+        for ch in (16, 24, 32, 40):
+            arms[f"grad_wgrad_s{st}_c{ch}"] = (
+                (lambda st=st, ch=ch: (knobs()(), ext.set_wgrad_stages(st),
+                                       eng._build_wgrad_plan(model, chunks_override=ch))),
+                lambda: eng.grad(None))
+    if os.environ.get("AB_ARMS"):   # regex filter on arm names
+        import re
+        arms = {k: v for k, v in arms.items() if re.search(os.environ["AB_ARMS"], k)}
     res = {k: [] for k in arms}
     for _ in range(5):
         for k, (setup, fn) in arms.items():
@@ -81,6 +92,7 @@ def main():
     ext.set_wgrad_impl(0)
     rows(0)
     ext.set_rollout_waves(8)
+    ext.set_wgrad_stages(4)
     eng._build_wgrad_plan(model)
     print(json.dumps({k: {"median_us": sorted(v)[len(v) // 2], "min_us": min(v)} for k, v in res.items()}, indent=1))
 
