@@ -353,7 +353,7 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
 
 // i_lo/i_hi: flat parameter range gathered from the slabs (-1, -1: [A, n)); with_partials: also
 // the log_std gradients and the loss sums (the range must then start at or after A)
-void grad_gather(torch::Tensor slab, torch::Tensor src_off, int64_t nchunks, int64_t stride, torch::Tensor part,
+void grad_gather(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_meta, torch::Tensor part,
                  int64_t nblk, int64_t npart, int64_t A, double scale, torch::Tensor grad, torch::Tensor loss_out,
                  int64_t i_lo, int64_t i_hi, bool with_partials) {
   const int64_t n = grad.numel();
@@ -362,11 +362,14 @@ void grad_gather(torch::Tensor slab, torch::Tensor src_off, int64_t nchunks, int
   TORCH_CHECK(A <= i_lo && i_lo <= i_hi && i_hi <= n, "gather range must lie in [A, n)");
   check(grad, "grad", at::kFloat, n);
   check(src_off, "src_off", at::kInt, n);
-  check(slab, "slab", at::kFloat, nchunks * stride);
+  check(src_meta, "src_meta", at::kInt, n);
+  check(slab, "slab", at::kFloat, 1);
   check(part, "part", at::kFloat, nblk * npart);
   check(loss_out, "loss_out", at::kFloat, 8);
   TORCH_CHECK(npart >= 8 + A, "npart");
-  launch_grad_gather(slab.data_ptr<float>(), src_off.data_ptr<int>(), (int)nchunks, (int)stride,
+  // the (offset, chunks x stride) of every element lies inside its bucket's slab by
+  // construction (HipEngine._build_wgrad_plan asserts it once; no per-epoch device sync here)
+  launch_grad_gather(slab.data_ptr<float>(), src_off.data_ptr<int>(), src_meta.data_ptr<int>(),
                      part.data_ptr<float>(), (int)nblk, (int)npart, (int)A, (float)scale, grad.data_ptr<float>(),
                      (int)i_lo, (int)i_hi, with_partials ? 1 : 0, loss_out.data_ptr<float>(), cur_stream());
 }

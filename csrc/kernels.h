@@ -121,11 +121,11 @@ int mlp_train_rows(int dt, const MlpArgs& a);   // row tile the launcher will us
 void set_mlp_rows_override(int rows);           // 0 auto; 16/32/64 force (A/B diagnostics)
 void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
 void set_wgrad_stages(int st);                 // bf16 wgrad DMA ring depth 3 / 4 / 6 (A/B)
-// grad[i] for i in [i_lo, i_hi) from the slabs; with_partials: also log_std grads [0, A) and the
-// 8 loss sums from the per-workgroup partials
-void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int chunk_stride,
-                        const float* part, int nblk, int npart, int A, float scale, float* grad,
-                        int i_lo, int i_hi, int with_partials, float* loss_out, hipStream_t s);
+// grad[i] for i in [i_lo, i_hi) from the slabs (src_off / src_meta: see grad_gather_kernel);
+// with_partials: also log_std grads [0, A) and the 8 loss sums from the per-workgroup partials
+void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part, int nblk,
+                        int npart, int A, float scale, float* grad, int i_lo, int i_hi, int with_partials,
+                        float* loss_out, hipStream_t s);
 void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
                 int T, int E, float gamma, float lam, int mode, hipStream_t s);
 void set_adam_fused(int on);

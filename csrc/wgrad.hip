@@ -212,13 +212,16 @@ void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
 //   Workgroups [0, A): grad[j] = scale * sum_b part[b*npart + 8 + j]  (log_std, one WG per dim,
 //                      strided partial sums + LDS tree: fixed order, deterministic)
 //   Workgroups [A, A+8): loss_out[q] = sum_b part[b*npart + q] (loss-term sums for logging).
-// Workgroups [nred, grid): grad[i] = scale * sum_c slab[c*stride + src_off[i]], i in [i_lo, i_hi)
-//                    (fixed chunk order: deterministic; no float atomics anywhere).  A bucketed
-//                    gradient (all-reduce of one flat range overlapping the next range's wgrad)
-//                    gathers each range with its own launch.
+// Workgroups [nred, grid): grad[i] = scale * sum_{c < nch} slab[src_off[i] + c * stride],
+//                    i in [i_lo, i_hi), with (nch, stride) of i's output tile packed in
+//                    src_meta[i] = nch * 16 + stride / 4096 (each tile has its own batch-chunk
+//                    count).  Fixed chunk order: deterministic; no float atomics anywhere.  A
+//                    bucketed gradient (all-reduce of one flat range overlapping the next
+//                    range's wgrad) gathers each range with its own launch.
 __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restrict__ slab,
-                                                          const int* __restrict__ src_off, int nchunks,
-                                                          int stride, const float* __restrict__ part,
+                                                          const int* __restrict__ src_off,
+                                                          const int* __restrict__ src_meta,
+                                                          const float* __restrict__ part,
                                                           int nblk, int npart, int A, float scale,
                                                           float* __restrict__ grad, int i_lo, int i_hi,
                                                           int nred, float* __restrict__ loss_out) {
@@ -243,8 +246,11 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
   const int nb = gridDim.x - nred;
   for (int i = i_lo + (blockIdx.x - nred) * 256 + threadIdx.x; i < i_hi; i += nb * 256) {
     const int o = src_off[i];
+    const int mt = src_meta[i];
+    const int nch = mt >> 4;
+    const size_t st = (size_t)(mt & 15) << 12;
     float s = 0.f;
-    for (int c = 0; c < nchunks; ++c) s += slab[(size_t)c * stride + o];
+    for (int c = 0; c < nch; ++c) s += slab[o + c * st];
     grad[i] = s * scale;
   }
 }
@@ -271,15 +277,15 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
-extern "C" void launch_grad_gather(const float* slab, const int* src_off, int nchunks, int chunk_stride,
-                                   const float* part, int nblk, int npart, int A, float scale, float* grad,
-                                   int i_lo, int i_hi, int with_partials, float* loss_out, hipStream_t s) {
+extern "C" void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part,
+                                   int nblk, int npart, int A, float scale, float* grad, int i_lo, int i_hi,
+                                   int with_partials, float* loss_out, hipStream_t s) {
   int grid = (i_hi - i_lo + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
   const int nred = with_partials ? A + 8 : 0;
   grid += nred;
-  hipLaunchKernelGGL(grad_gather_kernel, dim3(grid), dim3(256), 0, s, slab, src_off, nchunks, chunk_stride,
-                     part, nblk, npart, A, scale, grad, i_lo, i_hi, nred, loss_out);
+  hipLaunchKernelGGL(grad_gather_kernel, dim3(grid), dim3(256), 0, s, slab, src_off, src_meta, part, nblk, npart,
+                     A, scale, grad, i_lo, i_hi, nred, loss_out);
   HIP_CHECK_LAUNCH();
 }

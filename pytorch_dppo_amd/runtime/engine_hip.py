@@ -56,7 +56,7 @@ def wgrad_tiles(li: int, n: int, k: int):
                 best = (key, tl)
     return best[1]
 ROLL_ROWS = 16
-WGRAD_TARGET_WGS = 208   # Humanoid: 13 tiles x 16 chunks (A/B: 16 chunks beat 24-40 by ~6 %)
+WGRAD_TARGET_WGS = 0     # wgrad tasks per launch; 0: one per CU of the device (256 on MI355X)
 
 
 def _r(x: int, m: int) -> int:
@@ -212,6 +212,9 @@ class HipEngine:
         WGRAD_TARGET_WGS (env DPPO_WGRAD_WGS)."""
         if target_wgs is None:
             target_wgs = int(os.environ.get("DPPO_WGRAD_WGS", WGRAD_TARGET_WGS))
+        if target_wgs <= 0:
+            target_wgs = (torch.cuda.get_device_properties(self.device).multi_processor_count
+                          if self.device.type == "cuda" else 256)
         if split is None:
             split = self.split_grad
         ls = self.L.layers
@@ -225,70 +228,91 @@ class HipEngine:
             groups = [list(range(len(ls)))]
             ranges = [(self.A, model.num_params)]
         src = torch.full((model.num_params,), -1, dtype=torch.int64)
+        meta = torch.zeros(model.num_params, dtype=torch.int64)
         self.buckets = []
+        max_chunks = max(1, self.ldT // 64)            # a task covers >= 64 batch rows
         for bi, (layers, (lo, hi)) in enumerate(zip(groups, ranges)):
             tiles = []  # (layer, n0, k0, nq, kq)
             for li in layers:
                 l = ls[li]
                 tiles += wgrad_tiles(li, l.fan_out, l.fan_in + 1)
-            ntiles = len(tiles)
-            max_chunks = max(1, self.ldT // 256)
-            # the small policy bucket: half the workgroups (its gather sums every chunk's slab)
-            tw = target_wgs if bi == 0 else max(64, target_wgs // 2)
-            want = -(-tw // ntiles)                   # >= ~tw workgroups in flight
-            want = -(-want // 8) * 8                  # whole chunks per XCD (8 XCDs)
-            if chunks_override:                       # A/B diagnostics
-                want = chunks_override
-            nchunks = max(1, min(max_chunks, want))
-            mc = _r(-(-self.ldT // nchunks), 64)   # even number of 32-row k-steps per task
-            chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
-            sizes = [t[3] * t[4] * 64 * 64 for t in tiles]
-            chunk_stride = sum(sizes)
-            tile_off = {t: sum(sizes[:i]) for i, t in enumerate(tiles)}
+            # Batch chunks PER TILE, in proportion to the tile's operand stream ((nq + kq) * 64
+            # rows per k-step): every task then streams about the same bytes, and the task count
+            # is ~target_wgs = one workgroup per CU (the kernel is bound by each CU's operand
+            # stream, so every CU gets one equal share; largest-remainder rounding).
+            costs = [t[3] + t[4] for t in tiles]
+            if chunks_override:                       # A/B diagnostics: uniform chunk count
+                nch = [chunks_override] * len(tiles)
+            else:
+                raw = [target_wgs * c / sum(costs) for c in costs]
+                nch = [max(1, int(r)) for r in raw]
+                rest = sorted(range(len(tiles)), key=lambda t: raw[t] - int(raw[t]), reverse=True)
+                for t in rest[:max(0, target_wgs - sum(nch))]:
+                    nch[t] += 1
+            nch = [min(max_chunks, n) for n in nch]
+            tasks, tile_off, base = [], {}, 0
+            for t, n in zip(tiles, nch):
+                size = t[3] * t[4] * 64 * 64
+                mc = _r(-(-self.ldT // n), 64)        # even number of 32-row k-steps per task
+                chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
+                tile_off[t] = (base, len(chunks), size)
+                for ci, (m0, m1) in enumerate(chunks):
+                    tasks.append([t[0], t[1], t[2], m0, m1, base + ci * size, t[3], t[4]])
+                base += len(chunks) * size
             # XCD-aware order: workgroups b, b+8, b+16, ... are dealt to the same XCD (observed
-            # round-robin placement; speed only), so all tiles of a batch chunk — which share the
-            # chunk's operand rows — are given consecutive slots of ONE XCD and hit its L2.
+            # round-robin placement; speed only).  Tasks sorted by batch-row position are cut
+            # into 8 runs, one per XCD, so the tasks that share operand rows (all tiles of one
+            # row range) run on one XCD and share its L2.
+            tasks.sort(key=lambda r: (r[3] + r[4], r[0], r[1], r[2]))
             per_xcd = [[] for _ in range(8)]
-            for ci, (m0, m1) in enumerate(chunks):
-                for t in tiles:
-                    per_xcd[ci % 8].append([t[0], t[1], t[2], m0, m1, ci * chunk_stride + tile_off[t], t[3], t[4]])
-            tasks = []
+            for rank, r in enumerate(tasks):
+                per_xcd[rank * 8 // len(tasks)].append(r)
+            order = []
             j = 0
             while any(j < len(q) for q in per_xcd):
                 for q in per_xcd:
                     if j < len(q):
-                        tasks.append(q[j])
+                        order.append(q[j])
                 j += 1
-            tasks_host = torch.tensor(tasks, dtype=torch.int32).reshape(-1).contiguous()
-            # flat index -> offset of its element in this bucket's chunk-0 slab
+            tasks_host = torch.tensor(order, dtype=torch.int32).reshape(-1).contiguous()
+            # flat index -> (offset of its element in its tile's chunk-0 slab, chunk count and
+            # slab stride of that tile packed as nch * 16 + size / 4096)
             for li in layers:
                 l = ls[li]
                 woff, wn = model.offsets[f"{l.name}.weight"]
                 nn_ = torch.arange(l.fan_out).repeat_interleave(l.fan_in)
                 kk = torch.arange(l.fan_in).repeat(l.fan_out)
-                src[woff:woff + wn] = self._slab_index(tile_off, li, nn_, kk)
+                src[woff:woff + wn], meta[woff:woff + wn] = self._slab_index(tile_off, li, nn_, kk)
                 boff, bn = model.offsets[f"{l.name}.bias"]
                 nb = torch.arange(l.fan_out)
-                src[boff:boff + bn] = self._slab_index(tile_off, li, nb, torch.full_like(nb, l.fan_in))
+                src[boff:boff + bn], meta[boff:boff + bn] = self._slab_index(tile_off, li, nb,
+                                                                             torch.full_like(nb, l.fan_in))
+            # every element this bucket gathers stays inside its slab (grad_gather relies on it)
+            so, sm = src[lo:hi], meta[lo:hi]
+            reach = so + ((sm >> 4) - 1).clamp(min=0) * ((sm & 15) << 12)
+            assert bool((so >= 0).all()) and int(reach.max()) < base, "wgrad gather plan exceeds its slab"
             self.buckets.append({
                 "tasks_host": tasks_host, "tasks": tasks_host.to(self.device),
-                "slab": torch.zeros(len(chunks) * chunk_stride, device=self.device, dtype=torch.float32),
-                "nchunks": len(chunks), "chunk_stride": chunk_stride, "lo": lo, "hi": hi,
-                "partials": bi == len(groups) - 1})
+                "slab": torch.zeros(base, device=self.device, dtype=torch.float32),
+                "lo": lo, "hi": hi, "partials": bi == len(groups) - 1})
         src[src < 0] = 0  # log_std entries (handled from the partials)
         self.src_off = src.to(torch.int32).to(self.device)
+        self.src_meta = meta.to(torch.int32).to(self.device)
 
     @staticmethod
     def _slab_index(tile_off, li, n, k):
-        """slab offset of dW[n][k] of layer li: tile base + (n - n0) * (kq * 64) + (k - k0)"""
+        """dW[n][k] of layer li -> (slab offset in its tile's chunk-0 slab: tile base +
+        (n - n0) * (kq * 64) + (k - k0); packed chunk count / stride of the tile)"""
         out = torch.full_like(n, -1)
-        for (tl, n0, k0, nq, kq), base in tile_off.items():
+        meta = torch.zeros_like(n)
+        for (tl, n0, k0, nq, kq), (base, nch, size) in tile_off.items():
             if tl != li:
                 continue
             m = (n >= n0) & (n < n0 + 64 * nq) & (k >= k0) & (k < k0 + 64 * kq)
             out[m] = base + (n[m] - n0) * (64 * kq) + (k[m] - k0)
+            meta[m] = nch * 16 + size // 4096
         assert bool((out >= 0).all()), "wgrad tiles do not cover the layer"
-        return out
+        return out, meta
 
     # ------------------------------------------------------------------------------------------
     def sync_tile(self) -> None:
@@ -465,7 +489,7 @@ class HipEngine:
         for bi, b in enumerate(self.buckets):
             self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
                            b["tasks_host"], b["slab"])
-            self.ext.grad_gather(b["slab"], self.src_off, b["nchunks"], b["chunk_stride"], self.part,
+            self.ext.grad_gather(b["slab"], self.src_off, self.src_meta, self.part,
                                  self.ntrain_blk, self.npart, self.A, 1.0 / M, self.grad_flat, self.loss_sums,
                                  b["lo"], b["hi"], b["partials"])
             if reducer is not None and bi < len(self.buckets) - 1:

@@ -40,3 +40,41 @@ def test_humanoid_value_fc1_streams_fewer_rows_than_square_tiles():
     rows_per_step = sum(64 * (nq + kq) for (_, _, _, nq, kq) in tiles)
     square = (_r(500, 128) // 128) * (_r(377, 128) // 128) * 256   # 128x128 tiles
     assert rows_per_step == 2304 and rows_per_step < square
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("env", ["Humanoid-v2", "HalfCheetah-v2"])
+def test_plan_tasks_cover_tiles_and_batch_once(env, split):
+    """The full task list (HipEngine._build_wgrad_plan run on a CPU stand-in): each output tile's
+    tasks cover the batch rows [0, ldT) exactly once with 64-row-aligned chunks, every task owns
+    a disjoint slab region, the task count is ~one per CU, and every parameter's gather entry
+    (offset, chunk count, stride) matches its tile."""
+    from types import SimpleNamespace
+    from pytorch_dppo_amd.envs import get_spec
+    from pytorch_dppo_amd.models.actor_critic import ActorCritic
+    from pytorch_dppo_amd.runtime.engine_hip import HipEngine
+
+    spec = get_spec(env)
+    model = ActorCritic(spec.obs_dim, spec.act_dim)
+    stub = SimpleNamespace(L=model.packed_layout(), ldT=65536, A=spec.act_dim, device=torch.device("cpu"),
+                           split_grad=split, _slab_index=HipEngine._slab_index)
+    HipEngine._build_wgrad_plan(stub, model, target_wgs=256)
+    total = 0
+    for b in stub.buckets:
+        t = b["tasks_host"].view(-1, 8).tolist()
+        total += len(t)
+        assert len(t) <= 256 + 16
+        used = torch.zeros(b["slab"].numel(), dtype=torch.int32)
+        rows = {}
+        for (li, n0, k0, m0, m1, off, nq, kq) in t:
+            assert m0 % 64 == 0 and (m1 - m0) % 64 == 0 and 0 <= m0 < m1 <= stub.ldT
+            used[off:off + 64 * nq * 64 * kq] += 1
+            rows.setdefault((li, n0, k0), []).append((m0, m1))
+        assert bool((used == 1).all())
+        for key, rs in rows.items():
+            rs.sort()
+            assert rs[0][0] == 0 and rs[-1][1] == stub.ldT and all(a[1] == b_[0] for a, b_ in zip(rs, rs[1:]))
+    lo = min(b["lo"] for b in stub.buckets)
+    meta = stub.src_meta[lo:]
+    assert bool(((meta >> 4) >= 1).all()) and bool(((meta & 15) >= 1).all())
+    assert total >= 200
