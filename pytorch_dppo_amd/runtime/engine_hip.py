@@ -57,6 +57,7 @@ def wgrad_tiles(li: int, n: int, k: int):
     return best[1]
 ROLL_ROWS = 16
 WGRAD_TARGET_WGS = 0     # wgrad tasks per launch; 0: one per CU of the device (256 on MI355X)
+WGRAD_ALIGNED = False    # one batch-row grid for all tiles (A/B: HipEngine.wgrad_aligned)
 
 
 def _r(x: int, m: int) -> int:
@@ -241,8 +242,21 @@ class HipEngine:
             # is ~target_wgs = one workgroup per CU (the kernel is bound by each CU's operand
             # stream, so every CU gets one equal share; largest-remainder rounding).
             costs = [t[3] + t[4] for t in tiles]
+            aligned = self.wgrad_aligned if hasattr(self, "wgrad_aligned") else WGRAD_ALIGNED
             if chunks_override:                       # A/B diagnostics: uniform chunk count
                 nch = [chunks_override] * len(tiles)
+            elif aligned:
+                # one row grid for every tile (tiles sharing an operand read the same rows at the
+                # same time, on the same XCD); cheap tiles take runs of r grid chunks so every
+                # task streams about the same bytes; the finest grid within target_wgs tasks
+                cmax = max(costs)
+                run = [max(1, int(round(cmax / c))) for c in costs]
+                g = 1
+                for cand in range(1, max_chunks + 1):
+                    if sum(-(-cand // r) for r in run) <= target_wgs:
+                        g = cand
+                nch = [-(-g // r) for r in run]
+                grid = _r(-(-self.ldT // g), 64)
             else:
                 raw = [target_wgs * c / sum(costs) for c in costs]
                 nch = [max(1, int(r)) for r in raw]
@@ -251,9 +265,11 @@ class HipEngine:
                     nch[t] += 1
             nch = [min(max_chunks, n) for n in nch]
             tasks, tile_off, base = [], {}, 0
-            for t, n in zip(tiles, nch):
+            for ti, (t, n) in enumerate(zip(tiles, nch)):
                 size = t[3] * t[4] * 64 * 64
                 mc = _r(-(-self.ldT // n), 64)        # even number of 32-row k-steps per task
+                if aligned and not chunks_override:
+                    mc = grid * run[ti]
                 chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
                 tile_off[t] = (base, len(chunks), size)
                 for ci, (m0, m1) in enumerate(chunks):

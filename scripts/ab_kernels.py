@@ -73,6 +73,11 @@ def main():
     for t in (1024, 512, 256, 100):
         arms[f"grad_wgrad_wgs{t}"] = ((lambda t=t: (knobs()(), eng._build_wgrad_plan(model, t))),
                                       lambda: eng.grad(None))
+    def aligned(on):
+        eng.wgrad_aligned = on
+        eng._build_wgrad_plan(model)
+    arms["grad_wgrad_prop"] = (lambda: (knobs()(), aligned(False)), lambda: eng.grad(None))
+    arms["grad_wgrad_aligned"] = (lambda: (knobs()(), aligned(True)), lambda: eng.grad(None))
     # wgrad DMA ring depth x batch chunks (tasks = chunks x tiles per chunk)
     for st in (3, 4, 6):
         for ch in (16, 24, 32, 40):
@@ -93,6 +98,7 @@ def main():
     rows(0)
     ext.set_rollout_waves(8)
     ext.set_wgrad_stages(4)
+    eng.wgrad_aligned = False
     eng._build_wgrad_plan(model)
     print(json.dumps({k: {"median_us": sorted(v)[len(v) // 2], "min_us": min(v)} for k, v in res.items()}, indent=1))
 

@@ -42,9 +42,10 @@ def test_humanoid_value_fc1_streams_fewer_rows_than_square_tiles():
     assert rows_per_step == 2304 and rows_per_step < square
 
 
+@pytest.mark.parametrize("aligned", [False, True])
 @pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("env", ["Humanoid-v2", "HalfCheetah-v2"])
-def test_plan_tasks_cover_tiles_and_batch_once(env, split):
+def test_plan_tasks_cover_tiles_and_batch_once(env, split, aligned):
     """The full task list (HipEngine._build_wgrad_plan run on a CPU stand-in): each output tile's
     tasks cover the batch rows [0, ldT) exactly once with 64-row-aligned chunks, every task owns
     a disjoint slab region, the task count is ~one per CU, and every parameter's gather entry
@@ -57,7 +58,7 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, split):
     spec = get_spec(env)
     model = ActorCritic(spec.obs_dim, spec.act_dim)
     stub = SimpleNamespace(L=model.packed_layout(), ldT=65536, A=spec.act_dim, device=torch.device("cpu"),
-                           split_grad=split, _slab_index=HipEngine._slab_index)
+                           split_grad=split, _slab_index=HipEngine._slab_index, wgrad_aligned=aligned)
     HipEngine._build_wgrad_plan(stub, model, target_wgs=256)
     total = 0
     for b in stub.buckets:
