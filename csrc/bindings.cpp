@@ -312,7 +312,11 @@ void set_mlp_rows(int64_t rows) {
 }
 
 void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor> xT, std::vector<int64_t> g_rows,
-           std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab) {
+           std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab,
+           int64_t waves) {
+  TORCH_CHECK(waves == 8 || (waves == 16 && dt == 1 && g_wgrad_impl == 0),
+              "wgrad workgroup waves: 8, or 16 for the bf16 LDS-DMA kernel");
+  const int wmax = (int)waves, smax = waves == 16 ? 8 : 6;
   TORCH_CHECK(gT.size() == 6 && xT.size() == 6 && g_rows.size() == 6 && x_rows.size() == 6, "6 layers");
   check(tasks, "tasks", at::kInt, WGRAD_TASK_INTS);
   TORCH_CHECK(tasks.numel() % WGRAD_TASK_INTS == 0, "tasks are 8-int records");
@@ -325,7 +329,7 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
     const int* t = tp + WGRAD_TASK_INTS * i;
     TORCH_CHECK(t[0] >= 0 && t[0] < 6, "task layer");
     const int nq = t[6], kq = t[7];
-    TORCH_CHECK(nq >= 1 && kq >= 1 && nq * kq <= 8 && nq + kq <= 6, "task quadrants: nq*kq <= 8, nq+kq <= 6");
+    TORCH_CHECK(nq >= 1 && kq >= 1 && nq * kq <= wmax && nq + kq <= smax, "task quadrants beyond the workgroup");
     TORCH_CHECK(t[1] >= 0 && t[2] >= 0 && t[1] % 16 == 0 && t[2] % 16 == 0, "task tile origin");
     TORCH_CHECK(t[1] + 64 * nq <= g_rows[t[0]] && t[2] + 64 * kq <= x_rows[t[0]], "task tile beyond operand rows");
     // the kernel consumes 32-row k-steps in pairs: every range is a positive multiple of 64 rows
@@ -347,6 +351,7 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
   a.ntasks = ntasks;
   a.slab = slab.data_ptr<float>();
   a.impl = g_wgrad_impl;
+  a.waves = (int)waves;
   TORCH_CHECK(dt == 0 || dt == 1, "wgrad runs in fp32 or bf16 (the fp8 mode's update is bf16)");
   launch_wgrad((int)dt, a, cur_stream());
 }

@@ -98,7 +98,7 @@ struct WgradTask {
   int n0, k0;     // output tile origin
   int m0, m1;     // reduction (batch) range
   int slab;       // slab offset (floats) of this task's [nq*64][kq*64] tile
-  int nq, kq;     // tile extent in 64x64 quadrants (one per wave): nq*kq <= 8, nq + kq <= 6
+  int nq, kq;     // tile extent in 64x64 quadrants (one per wave): nq*kq <= W, nq + kq <= 6 (W 8) / 8 (W 16)
 };
 
 struct WgradArgs {
@@ -109,6 +109,7 @@ struct WgradArgs {
   int ntasks;
   float* slab;
   int impl;            // 0: LDS-DMA staged (default), 1: register-streamed (A/B diagnostics)
+  int waves;           // workgroup size of the LDS-DMA kernel: 8, or 16 (bf16; tiles up to 16 quadrants)
 };
 
 extern "C" {

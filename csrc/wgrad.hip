@@ -97,12 +97,14 @@ __global__ __launch_bounds__(WG_WAVES * 64) void wgrad_reg_kernel(WgradArgs a) {
 // — and with it the vmcnt arithmetic — is task-independent).  S-deep ring, counted vmcnt and a
 // raw s_barrier keep S-1 steps of DMA in flight across the barrier (cdna_hip_programming.md
 // 'Pipelining across barriers'): no VGPRs hold in-flight data.
-constexpr int WG_SLOTS = 24;   // fragment slots per stage: (nq + kq) * 4 <= 24
+// fragment slots per stage: (nq + kq) * 4 <= 24 at 8 waves (nq + kq <= 6), <= 32 at 16 waves
+// (nq + kq <= 8: e.g. 4x4 tiles, 256x256 outputs per workgroup)
+template <int W> struct WgSlots { static constexpr int N = W == 16 ? 32 : 24; };
 
 template <int DT>
 constexpr int wgrad_frag_bytes() { return 512 * Prec<DT>::BYTES; }
-template <int DT, int S>
-constexpr size_t wgrad_lds_bytes() { return (size_t)S * WG_SLOTS * wgrad_frag_bytes<DT>(); }
+template <int DT, int S, int W = 8>
+constexpr size_t wgrad_lds_bytes() { return (size_t)S * WgSlots<W>::N * wgrad_frag_bytes<DT>(); }
 // ring depth of the bf16 kernel (A/B knob set_wgrad_stages): 3 (72 KiB, two workgroups per
 // CU), 4 (96 KiB) or 6 (144 KiB; five steps = 120 KiB of DMA in flight per CU)
 int g_wgrad_stages = 4;
@@ -116,14 +118,14 @@ DEV void glds16(const void* g, void* lds) {
 // lgkmcnt[11:8]=15 | vmcnt[5:4] in [15:14])
 #define WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt((((n) & 15) | (7 << 4) | (15 << 8) | ((((n) >> 4) & 3) << 14)))
 
-template <int DT, int S, int C>
+template <int DT, int S, int C, int W>
 DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   using P = Prec<DT>;
   using T = typename P::T;
   using Frag = typename P::Frag;
   constexpr int FB = wgrad_frag_bytes<DT>();     // bytes per fragment
   constexpr int NI = FB / 1024;                  // DMA instructions per fragment (64 lanes x 16 B)
-  constexpr int SB = WG_SLOTS * FB;              // bytes per stage
+  constexpr int SB = WgSlots<W>::N * FB;         // bytes per stage
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const char* g = reinterpret_cast<const char*>(a.gT[tk.layer]);
@@ -132,13 +134,13 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   const int ks0 = tk.m0 >> 5;
   const int NF = 4 * tk.nq, F = NF + 4 * tk.kq;
   // slot f of a stage holds fragment f: f < NF -> dY^T row tile n0/16 + f, else X^T row tile
-  // k0/16 + f - NF.  Wave w DMAs slots C*w .. C*w + C-1 (a slot >= F re-loads fragment f - F).
+  // k0/16 + f - NF.  Wave w DMAs slots C*w .. C*w + C-1 (a slot >= F re-loads fragment f mod F).
   const char* src[C];
   int dst[C];
 #pragma unroll
   for (int q = 0; q < C; ++q) {
     const int f = wave * C + q;
-    const int ff = f < F ? f : f - F;
+    const int ff = f < F ? f : f % F;   // dummy slot: re-load one of the task's fragments
     src[q] = (ff < NF) ? g + fm_frag((tk.n0 >> 4) + ff, ks0, a.ld, 0) * sizeof(T)
                        : x + fm_frag((tk.k0 >> 4) + ff - NF, ks0, a.ld, 0) * sizeof(T);
     dst[q] = f * FB;
@@ -193,19 +195,23 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
       for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * KE + col + 16 * j] = acc[i][j][q];
 }
 
-template <int DT, int S>
-__global__ __launch_bounds__(WG_WAVES * 64) void wgrad_kernel(WgradArgs a) {
+template <int DT, int S, int W>
+__global__ __launch_bounds__(W * 64) void wgrad_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const WgradTask tk = a.tasks[blockIdx.x];
-  if (4 * (tk.nq + tk.kq) <= 2 * WG_WAVES) wgrad_lds_body<DT, S, 2>(a, tk, smem);
-  else wgrad_lds_body<DT, S, 3>(a, tk, smem);
+  if constexpr (W == 16) {
+    wgrad_lds_body<DT, S, 2, W>(a, tk, smem);    // 32 slots = 2 per wave
+  } else {
+    if (4 * (tk.nq + tk.kq) <= 2 * W) wgrad_lds_body<DT, S, 2, W>(a, tk, smem);
+    else wgrad_lds_body<DT, S, 3, W>(a, tk, smem);
+  }
 }
 
-template <int DT, int S>
+template <int DT, int S, int W = 8>
 void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
-  const size_t lds = wgrad_lds_bytes<DT, S>();
-  set_max_lds_once<wgrad_kernel<DT, S>>(lds);
-  hipLaunchKernelGGL((wgrad_kernel<DT, S>), dim3(a.ntasks), dim3(WG_WAVES * 64), lds, s, a);
+  const size_t lds = wgrad_lds_bytes<DT, S, W>();
+  set_max_lds_once<wgrad_kernel<DT, S, W>>(lds);
+  hipLaunchKernelGGL((wgrad_kernel<DT, S, W>), dim3(a.ntasks), dim3(W * 64), lds, s, a);
 }
 
 // With the partials pass (nred = A + 8 > 0):
@@ -267,6 +273,8 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
     else hipLaunchKernelGGL(wgrad_reg_kernel<DT_BF16>, dim3(a.ntasks), block, 0, s, a);
   } else if (dt == DT_F32) {
     launch_wgrad_lds<DT_F32, 3>(a, s);
+  } else if (a.waves == 16) {
+    launch_wgrad_lds<DT_BF16, 4, 16>(a, s);
   } else if (g_wgrad_stages == 3) {
     launch_wgrad_lds<DT_BF16, 3>(a, s);
   } else if (g_wgrad_stages == 6) {

@@ -33,18 +33,19 @@ NPART_FIXED = 8
 WT = 128            # operand-buffer row padding (csrc/kernels.h WGRAD_TILE)
 
 
-def wgrad_tiles(li: int, n: int, k: int):
+def wgrad_tiles(li: int, n: int, k: int, waves: int = 8):
     """Output tiles of one layer's weight gradient ([n][k], k including the bias column) for the
     wgrad kernel: (layer, n0, k0, nq, kq), a tile = nq x kq quadrants of 64x64, one per wave of
-    the 8-wave workgroup (nq*kq <= 8, nq + kq <= 6).  The kernel streams (nq + kq) * 64 operand
+    the workgroup (8 waves: nq*kq <= 8, nq + kq <= 6; 16 waves: nq*kq <= 16, nq + kq <= 8).  The kernel streams (nq + kq) * 64 operand
     rows per 32-row k-step, so the (nq, kq) minimising the layer's total rows read wins (ties:
     fewer tasks, then wider n).  Humanoid v_fc1 (512 x 377): 4x2 tiles, 2304 rows per step
     instead of 3072 with 128x128 tiles."""
     N, K = -(-n // 64), -(-k // 64)
     best = None
-    for nq in range(1, 9):
-        for kq in range(1, 9):
-            if nq * kq > 8 or nq + kq > 6 or nq > N or kq > K:
+    smax = 8 if waves == 16 else 6
+    for nq in range(1, 17):
+        for kq in range(1, 17):
+            if nq * kq > waves or nq + kq > smax or nq > N or kq > K:
                 continue
             tl = []
             for a in range(0, N, nq):
@@ -163,6 +164,12 @@ class HipEngine:
                        (self.h2vT, lv2.fan_out)):
             buf.view(-1)[fm_index(torch.full_like(cols, r), cols, self.ldT)] = 1.0
         self.split_grad = False          # bucketed gradient (enable_bucketed_grad, multi-rank)
+        # wgrad workgroup waves: 8 (A/B: 16-wave workgroups with up to 16-quadrant tiles stream
+        # fewer operand rows — 1,792 vs 2,304 per step for v_fc1 — but took 243 vs 226 us per
+        # grad call; bf16 only, env DPPO_WGRAD_WAVES=16)
+        self.wgrad_waves = int(os.environ.get("DPPO_WGRAD_WAVES", 8))
+        if self.dt != 1:
+            self.wgrad_waves = 8
         self._pending_reduce = []        # async all-reduce works of the current step's buckets
         self._reduce_stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None
         self._build_wgrad_plan(model)
@@ -236,7 +243,7 @@ class HipEngine:
             tiles = []  # (layer, n0, k0, nq, kq)
             for li in layers:
                 l = ls[li]
-                tiles += wgrad_tiles(li, l.fan_out, l.fan_in + 1)
+                tiles += wgrad_tiles(li, l.fan_out, l.fan_in + 1, self.wgrad_waves)
             # Batch chunks PER TILE, in proportion to the tile's operand stream ((nq + kq) * 64
             # rows per k-step): every task then streams about the same bytes, and the task count
             # is ~target_wgs = one workgroup per CU (the kernel is bound by each CU's operand
@@ -504,7 +511,7 @@ class HipEngine:
         ready = []
         for bi, b in enumerate(self.buckets):
             self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                           b["tasks_host"], b["slab"])
+                           b["tasks_host"], b["slab"], self.wgrad_waves)
             self.ext.grad_gather(b["slab"], self.src_off, self.src_meta, self.part,
                                  self.ntrain_blk, self.npart, self.A, 1.0 / M, self.grad_flat, self.loss_sums,
                                  b["lo"], b["hi"], b["partials"])

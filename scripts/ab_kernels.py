@@ -54,9 +54,16 @@ def main():
         ext.set_mlp_rows(n)
         eng.sync_tile()
 
+    waves0 = eng.wgrad_waves
+
+    def plan(waves=None, aligned=False):
+        eng.wgrad_waves = waves or waves0
+        eng.wgrad_aligned = aligned
+        eng._build_wgrad_plan(model)
+
     def knobs(adam=1, wgrad=0, r=0):   # every arm sets every knob (no state leaks between arms)
         return lambda: (ext.set_adam_fused(adam), ext.set_wgrad_impl(wgrad), rows(r), ext.set_wgrad_stages(4),
-                        eng._build_wgrad_plan(model))
+                        plan(8 if wgrad == 1 else None))
 
     arms = {
         "adam_fused": (knobs(adam=1), eng.apply),
@@ -73,16 +80,15 @@ def main():
     for t in (1024, 512, 256, 100):
         arms[f"grad_wgrad_wgs{t}"] = ((lambda t=t: (knobs()(), eng._build_wgrad_plan(model, t))),
                                       lambda: eng.grad(None))
-    def aligned(on):
-        eng.wgrad_aligned = on
-        eng._build_wgrad_plan(model)
-    arms["grad_wgrad_prop"] = (lambda: (knobs()(), aligned(False)), lambda: eng.grad(None))
-    arms["grad_wgrad_aligned"] = (lambda: (knobs()(), aligned(True)), lambda: eng.grad(None))
+    arms["grad_wgrad_prop"] = (lambda: (knobs()(), plan()), lambda: eng.grad(None))
+    arms["grad_wgrad_aligned"] = (lambda: (knobs()(), plan(aligned=True)), lambda: eng.grad(None))
+    arms["grad_wgrad_w8"] = (lambda: (knobs()(), plan(8)), lambda: eng.grad(None))
+    arms["grad_wgrad_w16"] = (lambda: (knobs()(), plan(16)), lambda: eng.grad(None))
     # wgrad DMA ring depth x batch chunks (tasks = chunks x tiles per chunk)
-    for st in (3, 4, 6):
+    for st in (3, 4, 6):   # ring depth of the 8-wave kernel
         for ch in (16, 24, 32, 40):
             arms[f"grad_wgrad_s{st}_c{ch}"] = (
-                (lambda st=st, ch=ch: (knobs()(), ext.set_wgrad_stages(st),
+                (lambda st=st, ch=ch: (knobs()(), ext.set_wgrad_stages(st), setattr(eng, "wgrad_waves", 8),
                                        eng._build_wgrad_plan(model, chunks_override=ch))),
                 lambda: eng.grad(None))
     if os.environ.get("AB_ARMS"):   # regex filter on arm names
@@ -98,8 +104,7 @@ def main():
     rows(0)
     ext.set_rollout_waves(8)
     ext.set_wgrad_stages(4)
-    eng.wgrad_aligned = False
-    eng._build_wgrad_plan(model)
+    plan()
     print(json.dumps({k: {"median_us": sorted(v)[len(v) // 2], "min_us": min(v)} for k, v in res.items()}, indent=1))
 
 

@@ -42,6 +42,7 @@ def main():
     eng.begin_update()
     ext = eng.ext
     rows_list = [int(r) for r in os.environ.get("ABLATE_ROWS", "64,32").split(",")]
+    waves0 = eng.wgrad_waves
     res = {f"{k}@{r}": [] for r in rows_list for k in VARIANTS}
     for rnd in range(6):
         for key in res:
@@ -51,6 +52,8 @@ def main():
             eng.sync_tile()
             ext.set_train_ablation(mask)
             ext.set_wgrad_impl(impl)
+            eng.wgrad_waves = 8 if impl == 1 else waves0   # the register kernel takes 8-wave tiles
+            eng._build_wgrad_plan(model)
             for _ in range(2):
                 eng.grad(None)   # warm
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

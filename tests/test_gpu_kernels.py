@@ -474,6 +474,8 @@ def test_wgrad_lds_dma_matches_register_path_bitwise():
         eng.gae()
         eng.begin_update()
         ext = eng.ext
+        eng.wgrad_waves = 8          # the register-streamed kernel takes 8-wave tiles
+        eng._build_wgrad_plan(model)
         outs = []
         for impl in (0, 1):
             ext.set_wgrad_impl(impl)
