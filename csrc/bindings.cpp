@@ -13,6 +13,18 @@ namespace {
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// Debug mode (DPPO_DEBUG_SYNC=1 / set_debug_sync, SURVEY §5.2 "HIP_LAUNCH_BLOCKING mode"): every
+// binding synchronises its stream after its launch and raises on a launch or execution error,
+// naming the binding — a kernel fault surfaces at the op that caused it, not at a later sync.
+bool g_debug_sync = false;
+void set_debug_sync(bool on) { g_debug_sync = on; }
+void after_launch(const char* what) {
+  if (!g_debug_sync) return;
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(cur_stream());
+  TORCH_CHECK(e == hipSuccess, "debug-sync: ", what, " failed: ", hipGetErrorString(e));
+}
+
 // diagnostics only: phase-ablation mask for mlp_train (scripts/ablate_train.py); always 0 in
 // training runs (the results of an ablated call are not a gradient)
 int g_train_ablate = 0;
@@ -165,6 +177,7 @@ void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len
     a.tstamp = g_roll_tstamp;
   }
   launch_rollout((int)dt, a, (int)rows, cur_stream());
+  after_launch(__func__);
 }
 
 // idx_limit: exclusive upper bound every gathered row index must respect (rows of x_buf and of
@@ -226,6 +239,7 @@ void mlp_value(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   a.v_out = v_out.data_ptr<float>();
   a.qscale = opt_scales(qscale);
   launch_mlp_value((int)dt, a, cur_stream());
+  after_launch(__func__);
 }
 
 void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0, int64_t M, torch::Tensor wimg,
@@ -292,6 +306,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   }
   a.part = part.data_ptr<float>();
   launch_mlp_train((int)dt, a, cur_stream());
+  after_launch(__func__);
 }
 
 int64_t train_lds_bytes(int64_t dt, std::vector<int64_t> layout, int64_t A) {
@@ -354,6 +369,7 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
   a.waves = (int)waves;
   TORCH_CHECK(dt == 0 || dt == 1, "wgrad runs in fp32 or bf16 (the fp8 mode's update is bf16)");
   launch_wgrad((int)dt, a, cur_stream());
+  after_launch(__func__);
 }
 
 // i_lo/i_hi: flat parameter range gathered from the slabs (-1, -1: [A, n)); with_partials: also
@@ -377,6 +393,7 @@ void grad_gather(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
   launch_grad_gather(slab.data_ptr<float>(), src_off.data_ptr<int>(), src_meta.data_ptr<int>(),
                      part.data_ptr<float>(), (int)nblk, (int)npart, (int)A, (float)scale, grad.data_ptr<float>(),
                      (int)i_lo, (int)i_hi, with_partials ? 1 : 0, loss_out.data_ptr<float>(), cur_stream());
+  after_launch(__func__);
 }
 
 void obs_reduce(torch::Tensor part, int64_t nblk, int64_t O, torch::Tensor s12, torch::Tensor epstat,
@@ -387,6 +404,7 @@ void obs_reduce(torch::Tensor part, int64_t nblk, int64_t O, torch::Tensor s12, 
   check(ep, "ep", at::kDouble, 2);
   launch_obs_reduce(part.data_ptr<float>(), (int)nblk, (int)O, s12.data_ptr<double>(), epstat.data_ptr<float>(),
                     ep.data_ptr<double>(), cur_stream());
+  after_launch(__func__);
 }
 
 void obs_merge(torch::Tensor s12, double count, double n_a, torch::Tensor shift, torch::Tensor mean, torch::Tensor m2,
@@ -402,6 +420,7 @@ void obs_merge(torch::Tensor s12, double count, double n_a, torch::Tensor shift,
   launch_obs_merge(s12.data_ptr<double>(), (int)O, count, n_a, shift.data_ptr<float>(), mean.data_ptr<double>(),
                    m2.data_ptr<double>(), mean_f32.data_ptr<float>(), inv_std.data_ptr<float>(), var_floor,
                    cur_stream());
+  after_launch(__func__);
 }
 
 void gae(torch::Tensor rewards, torch::Tensor values, torch::Tensor dones, torch::Tensor adv, torch::Tensor ret,
@@ -416,6 +435,7 @@ void gae(torch::Tensor rewards, torch::Tensor values, torch::Tensor dones, torch
   check(ret, "ret", at::kFloat, T * E);
   launch_gae(rewards.data_ptr<float>(), values.data_ptr<float>(), dones.data_ptr<float>(), adv.data_ptr<float>(),
              ret.data_ptr<float>(), (int)T, (int)E, (float)gamma, (float)lam, (int)mode, cur_stream());
+  after_launch(__func__);
 }
 
 void metrics_pack(torch::Tensor ep, torch::Tensor loss8, torch::Tensor norm_part, torch::Tensor out) {
@@ -425,6 +445,7 @@ void metrics_pack(torch::Tensor ep, torch::Tensor loss8, torch::Tensor norm_part
   check(out, "out", at::kDouble, 11);
   launch_metrics_pack(ep.data_ptr<double>(), loss8.data_ptr<float>(), norm_part.data_ptr<float>(),
                       (int)norm_part.numel(), out.data_ptr<double>(), cur_stream());
+  after_launch(__func__);
 }
 
 void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, double lr, double b1, double b2,
@@ -450,6 +471,7 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, do
               (float)b1, (float)b2, (float)eps, (float)max_norm, state.data_ptr<float>(), norm_part.data_ptr<float>(),
               nblk, wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q, (int)host_step,
               cur_stream());
+  after_launch(__func__);
 }
 
 void pack(torch::Tensor p, torch::Tensor wimg, torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul) {
@@ -462,6 +484,7 @@ void pack(torch::Tensor p, torch::Tensor wimg, torch::Tensor w_map, torch::Tenso
   if (qmul.defined() && qmul.numel() > 0) { check(qmul, "qmul", at::kFloat, n); q = qmul.data_ptr<float>(); }
   launch_pack(p.data_ptr<float>(), (int)n, wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q,
               cur_stream());
+  after_launch(__func__);
 }
 
 }  // namespace
@@ -474,6 +497,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("train_lds_bytes", &train_lds_bytes);
   m.def("train_rows", &train_rows);
   m.def("set_mlp_rows", &set_mlp_rows);
+  m.def("set_debug_sync", &set_debug_sync);
   m.def("set_rollout_waves", [](int64_t nw) {
     TORCH_CHECK(nw == 4 || nw == 8, "rollout waves: 4 or 8");
     set_rollout_waves((int)nw);

@@ -30,6 +30,10 @@ def load(build_if_missing: bool = False):
         _MOD = importlib.import_module("pytorch_dppo_amd.ops._dppo_hip")
     if getattr(_MOD, "arch", None) != "gfx950":
         raise RuntimeError(f"extension built for {getattr(_MOD, 'arch', '?')}, need gfx950")
+    if os.environ.get("DPPO_DEBUG_SYNC", "0") == "1":
+        # debug mode: every op synchronises after its launch and raises naming the op (HIP
+        # kernels are asynchronous: without this a fault surfaces at some later sync point)
+        _MOD.set_debug_sync(True)
     return _MOD
 
 

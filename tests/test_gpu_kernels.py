@@ -545,3 +545,23 @@ def test_two_ranks_on_one_gpu_stay_in_sync(extra):
     assert r.returncode == 0, r.stderr[-3000:]
     assert "replicas_in_sync True" in r.stderr, r.stderr[-2000:]
     assert '"n_gpus": 2' in r.stdout
+
+
+def test_debug_sync_mode_runs_an_iteration_bit_identical():
+    """DPPO_DEBUG_SYNC mode (every op synchronises + checks after its launch) changes no result."""
+    from pytorch_dppo_amd.parallel.dist import DistContext
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    common = dict(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 4,
+                  batch_size=64 * 4, num_epoch=1, dtype="bf16")
+    ext = _ext()
+    out = []
+    for on in (False, True):
+        ext.set_debug_sync(on)
+        try:
+            w = DPPOWorker(dppo_preset(**common), DistContext(device=DEV))
+            w.iteration_step()
+            torch.cuda.synchronize()
+            out.append(w.model.flat.data.clone())
+        finally:
+            ext.set_debug_sync(False)
+    assert torch.equal(out[0], out[1])
