@@ -474,6 +474,43 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, do
   after_launch(__func__);
 }
 
+// grad_gather (partials pass + [A, n)) and the no-clip Adam step in one launch (world size 1:
+// nothing runs between them).  Bit-identical parameters to grad_gather -> adam(host_step).
+void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_meta, torch::Tensor part,
+                 int64_t npblk, int64_t npart, int64_t A, double scale, torch::Tensor loss_out, torch::Tensor g,
+                 torch::Tensor p, torch::Tensor m, torch::Tensor v, double lr, double b1, double b2, double eps,
+                 int64_t step, torch::Tensor state, torch::Tensor norm_part, torch::Tensor wimg, torch::Tensor w_map,
+                 torch::Tensor wt_map, int64_t dt, torch::Tensor qmul) {
+  const int64_t n = p.numel();
+  check(p, "p", at::kFloat, n);
+  check(g, "g", at::kFloat, n);
+  check(m, "m", at::kFloat, n);
+  check(v, "v", at::kFloat, n);
+  check(src_off, "src_off", at::kInt, n);
+  check(src_meta, "src_meta", at::kInt, n);
+  check(slab, "slab", at::kFloat, 1);
+  check(part, "part", at::kFloat, npblk * npart);
+  check(loss_out, "loss_out", at::kFloat, 8);
+  check(state, "state", at::kFloat, 4);
+  check(w_map, "w_map", at::kInt, n);
+  check(wt_map, "wt_map", at::kInt, n);
+  check(wimg, "wimg", storage_type((int)dt), 1);
+  TORCH_CHECK(npart >= 8 + A && A < n, "npart / A");
+  TORCH_CHECK(step >= 1, "gather_adam needs the host step number (eager launches only)");
+  const int nblk = (int)norm_part.numel();
+  check(norm_part, "norm_part", at::kFloat, nblk);
+  TORCH_CHECK(nblk > A + 8 && nblk <= 4096, "norm_part must hold more than A + 8 blocks");
+  const float* q = nullptr;
+  if (qmul.defined() && qmul.numel() > 0) { check(qmul, "qmul", at::kFloat, n); q = qmul.data_ptr<float>(); }
+  launch_gather_adam(slab.data_ptr<float>(), src_off.data_ptr<int>(), src_meta.data_ptr<int>(),
+                     part.data_ptr<float>(), (int)npblk, (int)npart, (int)A, (float)scale, loss_out.data_ptr<float>(),
+                     g.data_ptr<float>(), p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (int)n,
+                     (float)lr, (float)b1, (float)b2, (float)eps, (int)step, state.data_ptr<float>(),
+                     norm_part.data_ptr<float>(), nblk, wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(),
+                     (int)dt, q, cur_stream());
+  after_launch(__func__);
+}
+
 void pack(torch::Tensor p, torch::Tensor wimg, torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul) {
   const int64_t n = p.numel();
   check(p, "p", at::kFloat, n);
@@ -514,6 +551,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("obs_reduce", &obs_reduce);
   m.def("obs_merge", &obs_merge);
   m.def("adam", &adam);
+  m.def("gather_adam", &gather_adam);
   m.def("pack", &pack);
   m.def("metrics_pack", &metrics_pack);
   m.attr("arch") = "gfx950";

@@ -163,3 +163,19 @@ inline void set_max_lds_once(size_t bytes) {
               __FILE__, __LINE__);                                               \
     }                                                                            \
   } while (0)
+
+// sum_{c < nch} p[c * st] in that fixed order (the split-K slab reduction of the weight gradient):
+// the loads of 16 chunks are issued before the first add, instead of one load -> wait -> add
+// round trip per chunk that a variable trip count otherwise compiles to.
+__device__ __forceinline__ float slab_sum(const float* __restrict__ p, int nch, size_t st) {
+  float s = 0.f;
+  for (int c0 = 0; c0 < nch; c0 += 16) {
+    float x[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[c] = (c0 + c < nch) ? p[(size_t)(c0 + c) * st] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (c0 + c < nch) s += x[c];
+  }
+  return s;
+}

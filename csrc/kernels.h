@@ -134,6 +134,13 @@ void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, 
                  float eps, float max_norm, float* state, float* norm_part, int nblk,
                  void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale, int host_step,
                  hipStream_t s);
+// grad_gather (with the partials pass, range [A, n)) + no-clip Adam fused: world size 1 only
+// (no all-reduce between them); nblk = norm_part size, must exceed A + 8
+void launch_gather_adam(const float* slab, const int* src_off, const int* src_meta, const float* part, int npblk,
+                        int npart, int A, float scale, float* loss_out, float* g, float* p, float* m, float* v,
+                        int n, float lr, float b1, float b2, float eps, int step, float* state, float* norm_part,
+                        int nblk, void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale,
+                        hipStream_t s);
 void launch_pack(const float* p, int n, void* wimg, const int* w_map, const int* wt_map, int dt,
                  const float* img_scale, hipStream_t s);
 void launch_obs_reduce(const float* part, int nblk, int O, double* s12, const float* epstat, double* ep,

@@ -205,6 +205,92 @@ __global__ __launch_bounds__(256) void adam_noclip_kernel(float* __restrict__ p,
   }
 }
 
+// Gradient gather + no-clip Adam in ONE launch (world size 1: no all-reduce sits between the
+// two, SURVEY K11+K12).  Element i's gradient is formed exactly as grad_gather_kernel forms it
+// (same fixed chunk order, same scale) and handed straight to adam_elem, so the parameters are
+// bit-identical to the grad_gather -> adam_noclip pair; the gradient is still written to g (the
+// metrics fallback reads it).  Grid = norm_part size: blocks [0, A) reduce the log_std partials
+// and update parameter j; blocks [A, A+8) reduce the loss sums; the rest grid-stride over
+// [A, n).  Every block leaves its sum of squares in norm_part (0 for the loss blocks).
+template <int DT>
+__global__ __launch_bounds__(256) void gather_adam_kernel(
+    const float* __restrict__ slab, const int* __restrict__ src_off, const int* __restrict__ src_meta,
+    const float* __restrict__ part, int npblk, int npart, int A, float scale, float* __restrict__ loss_out,
+    float* __restrict__ g, float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, int n, float lr,
+    float b1, float b2, float eps, float step, float* __restrict__ state, float* __restrict__ norm_part,
+    typename Prec<DT>::T* __restrict__ wimg, const int* __restrict__ w_map, const int* __restrict__ wt_map,
+    const float* __restrict__ qmul) {
+  using P = Prec<DT>;
+  __shared__ float red[256];
+  const float bc1 = 1.f - powf(b1, step);
+  const float bc2 = 1.f - powf(b2, step);
+  const float step_size = lr / bc1;
+  const float rbc2 = 1.f / sqrtf(bc2);
+  const int nred = A + 8;
+  float ss = 0.f;
+  // the optimizer-state loads are issued before the gradient is formed (they do not depend on
+  // it), so their latency overlaps the slab loads'
+  auto update = [&](int i, float gi, float mi, float vi, float pv, int wi) {
+    g[i] = gi;
+    const float pi = adam_elem(mi, vi, pv, gi, b1, b2, step_size, rbc2, eps);
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+    if (wi >= 0) {
+      const typename P::T q = P::cvt(qmul ? pi * qmul[i] : pi);
+      wimg[wi] = q;
+      wimg[wt_map[i]] = q;
+    }
+  };
+  if ((int)blockIdx.x < nred) {
+    const int j = blockIdx.x;
+    const int col = j < A ? 8 + j : j - A;
+    float s = 0.f;
+    for (int b = threadIdx.x; b < npblk; b += 256) s += part[(size_t)b * npart + col];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      if (j < A) {
+        const float gi = red[0] * scale;
+        update(j, gi, m[j], v[j], p[j], w_map[j]);
+        norm_part[j] = gi * gi;
+      } else {
+        loss_out[j - A] = red[0];
+        norm_part[j] = 0.f;
+      }
+      if (j == 0) {
+        state[0] = step;
+        state[1] = step;
+      }
+    }
+    return;
+  }
+  const int nb = gridDim.x - nred;
+  for (int i = A + (blockIdx.x - nred) * 256 + threadIdx.x; i < n; i += nb * 256) {
+    const int o = src_off[i];
+    const int mt = src_meta[i];
+    const float mi = m[i], vi = v[i], pv = p[i];
+    const int wi = w_map[i];
+    const int nch = mt >> 4;
+    const size_t st = (size_t)(mt & 15) << 12;
+    const float s = slab_sum(slab + o, nch, st);
+    const float gi = s * scale;
+    ss = fmaf(gi, gi, ss);
+    update(i, gi, mi, vi, pv, wi);
+  }
+  red[threadIdx.x] = ss;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) norm_part[blockIdx.x] = red[0];
+}
+
 template <int DT>
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ p, int n,
                                                    typename Prec<DT>::T* __restrict__ wimg,
@@ -296,6 +382,26 @@ extern "C" void launch_adam(float* p, const float* g, float* m, float* v, int n,
   else
     hipLaunchKernelGGL(adam_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
                        state, norm_part, nblk, (uint8_t*)wimg, w_map, wt_map, img_scale);
+  HIP_CHECK_LAUNCH();
+}
+
+extern "C" void launch_gather_adam(const float* slab, const int* src_off, const int* src_meta, const float* part,
+                                   int npblk, int npart, int A, float scale, float* loss_out, float* g, float* p,
+                                   float* m, float* v, int n, float lr, float b1, float b2, float eps, int step,
+                                   float* state, float* norm_part, int nblk, void* wimg, const int* w_map,
+                                   const int* wt_map, int dt, const float* img_scale, hipStream_t s) {
+#define GA_ARGS slab, src_off, src_meta, part, npblk, npart, A, scale, loss_out, g, p, m, v, n, lr, b1, b2, eps, \
+                (float)step, state, norm_part
+  if (dt == DT_F32)
+    hipLaunchKernelGGL(gather_adam_kernel<DT_F32>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (float*)wimg, w_map, wt_map,
+                       img_scale);
+  else if (dt == DT_BF16)
+    hipLaunchKernelGGL(gather_adam_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (__bf16*)wimg, w_map,
+                       wt_map, img_scale);
+  else
+    hipLaunchKernelGGL(gather_adam_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (uint8_t*)wimg, w_map,
+                       wt_map, img_scale);
+#undef GA_ARGS
   HIP_CHECK_LAUNCH();
 }
 

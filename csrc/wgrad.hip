@@ -255,8 +255,7 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
     const int mt = src_meta[i];
     const int nch = mt >> 4;
     const size_t st = (size_t)(mt & 15) << 12;
-    float s = 0.f;
-    for (int c = 0; c < nch; ++c) s += slab[o + c * st];
+    const float s = slab_sum(slab + o, nch, st);
     grad[i] = s * scale;
   }
 }

@@ -180,7 +180,13 @@ class HipEngine:
         self.adam_v = torch.zeros(n, **f32)
         self.adam_state = torch.zeros(4, **f32)
         self.adam_step = 0
-        self.norm_part = torch.zeros(min(1024, (n + 255) // 256), **f32)
+        # per-block gradient sums of squares of whichever Adam path ran; the fused gather+Adam
+        # launch uses one block per entry: A + 8 reduction blocks plus one per 256 elements
+        # launch (one element per thread: a grid-stride second pass would double the load latency
+        # chain of the blocks that take it) needs A + 8 reduction blocks plus one per 256 elements
+        self.norm_part = torch.zeros(min(4096, (n - self.A + 255) // 256 + self.A + 8), **f32)
+        # world-size-1 fast path: grad_gather + no-clip Adam in one launch (DPPO_FUSED_APPLY=0: off)
+        self.fused_apply = os.environ.get("DPPO_FUSED_APPLY", "1") != "0"
         self.idx_dev = torch.zeros(self.ldT, dtype=torch.int32, **dev)
         self.key_action = rng.base_key(params.seed, rng.STREAM_ACTION, action_rank)
         self.empty = torch.empty(0, dtype=torch.int32, **dev)
@@ -470,10 +476,20 @@ class HipEngine:
                 w.wait()
         self._pending_reduce = []
 
-    def grad(self, idx: Optional[torch.Tensor], reducer=None) -> None:
+    def can_fuse_apply(self, extra_grad: float = 0.0) -> bool:
+        """grad(idx, apply=True) is available: one gradient range, no clipping (the Adam step
+        needs no global norm first), eager launches (the host knows the step number), and no
+        all-reduce between the gradient and the update (the caller checks that: world size 1)."""
+        p = self.p
+        clip = p.max_grad_norm is not None and p.max_grad_norm > 0
+        return (self.fused_apply and not self.use_graphs and not extra_grad and not clip
+                and len(self.buckets) == 1 and self.buckets[0]["partials"])
+
+    def grad(self, idx: Optional[torch.Tensor], reducer=None, apply: bool = False) -> None:
         """one minibatch gradient into grad_flat.  ``reducer(t) -> work`` (bucketed mode): called
         on each bucket's flat range as soon as it is gathered (async all-reduce); finish with
-        wait_reduce() before apply()."""
+        wait_reduce() before apply().  ``apply=True`` (only when can_fuse_apply()): the gather
+        and the Adam step run as ONE launch — the same update as grad() then apply()."""
         p = self.p
         M = self.mb
         if idx is None:
@@ -489,7 +505,11 @@ class HipEngine:
             self.idx_dev[:M].copy_(idx.to(torch.int32), non_blocking=True)
             idx_t, row0 = self.idx_dev, 0
         first, xt_ready = bool(self._first_step), bool(idx is None and self._xT_valid)
-        if reducer is not None:
+        if apply:
+            assert reducer is None and self.can_fuse_apply(), "fused gather + Adam is not available here"
+            self._launch_grad(idx_t, row0, first, xt_ready, fused_apply=True)
+            self.adam_step += 1
+        elif reducer is not None:
             assert not self.use_graphs, "bucketed all-reduce cannot run inside a captured graph"
             self._launch_grad(idx_t, row0, first, xt_ready, reducer)
         else:
@@ -499,7 +519,8 @@ class HipEngine:
         self._loss_dev = self.loss_sums
         return None
 
-    def _launch_grad(self, idx_t: torch.Tensor, row0: int, first: bool, xt_ready: bool, reducer=None) -> None:
+    def _launch_grad(self, idx_t: torch.Tensor, row0: int, first: bool, xt_ready: bool, reducer=None,
+                     fused_apply: bool = False) -> None:
         p, M = self.p, self.mb
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
                 1 if p.std_convention == "var" else 0, 1 if first else 0, self.npart]
@@ -512,6 +533,16 @@ class HipEngine:
         for bi, b in enumerate(self.buckets):
             self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
                            b["tasks_host"], b["slab"], self.wgrad_waves)
+            if fused_apply:
+                if p.loss == "dppo_ref":   # train.py:164: the pre-update log_std, before Adam moves it
+                    self.log_std_old.copy_(self.model.flat.data[:self.A])
+                b1, b2 = p.adam_betas
+                self.ext.gather_adam(b["slab"], self.src_off, self.src_meta, self.part, self.ntrain_blk,
+                                     self.npart, self.A, 1.0 / M, self.loss_sums, self.grad_flat,
+                                     self.model.flat.data, self.adam_m, self.adam_v, float(p.lr), float(b1),
+                                     float(b2), float(p.adam_eps), self.adam_step + 1, self.adam_state,
+                                     self.norm_part, self.wimg, self.w_map, self.wt_map, self.dt, self.no_q)
+                return
             self.ext.grad_gather(b["slab"], self.src_off, self.src_meta, self.part,
                                  self.ntrain_blk, self.npart, self.A, 1.0 / M, self.grad_flat, self.loss_sums,
                                  b["lo"], b["hi"], b["partials"])

@@ -157,6 +157,11 @@ class DPPOWorker:
                     eng.apply(extra)
                     self.updates += 1
                     continue
+                if (not self.ctx.collective and hasattr(eng, "can_fuse_apply")
+                        and eng.can_fuse_apply(extra)):
+                    eng.grad(idx, apply=True)           # world size 1: gather + Adam, one launch
+                    self.updates += 1
+                    continue
                 eng.grad(idx)
                 if deferred:
                     work = self.ctx.allreduce_grads(eng.grad_flat, async_op=True)

@@ -565,3 +565,30 @@ def test_debug_sync_mode_runs_an_iteration_bit_identical():
         finally:
             ext.set_debug_sync(False)
     assert torch.equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("dtype,loss", [("bf16", "ppo"), ("fp32", "ppo"), ("bf16", "dppo_ref")])
+def test_fused_gather_adam_bit_identical_to_gather_then_adam(dtype, loss, monkeypatch):
+    """World size 1 runs grad_gather + no-clip Adam as ONE launch (gather_adam): parameters, Adam
+    moments and weight images after a full iteration equal the two-launch path's bit for bit."""
+    from pytorch_dppo_amd.parallel.dist import DistContext
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    common = dict(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 4,
+                  batch_size=64 * 4, num_epoch=3, dtype=dtype, loss=loss)
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DPPO_FUSED_APPLY", fused)
+        w = DPPOWorker(dppo_preset(**common), DistContext(device=DEV))
+        assert w.engine.fused_apply == (fused == "1")
+        assert w.engine.can_fuse_apply() == (fused == "1")
+        m = w.iteration_step()
+        torch.cuda.synchronize()
+        e = w.engine
+        out.append((w.model.flat.data.clone(), e.adam_m.clone(), e.adam_v.clone(), e.wimg.clone(),
+                    e.grad_flat.clone(), m))
+    (p0, m0, v0, i0, g0, mt0), (p1, m1, v1, i1, g1, mt1) = out
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+    assert torch.equal(i0.view(torch.uint8), i1.view(torch.uint8))
+    assert torch.equal(g0, g1)
+    assert abs(mt0["grad_norm"] - mt1["grad_norm"]) <= 1e-5 * (1 + mt1["grad_norm"])
+    assert mt0["loss"] == mt1["loss"]
