@@ -405,7 +405,11 @@ class HipEngine:
                          float(self.p.reward_clip), self.qscale, xt, self.x_rows[0])
 
     @torch.no_grad()
-    def rollout(self) -> Dict:
+    def rollout(self, stats_stream: Optional[torch.cuda.Stream] = None) -> Dict:
+        """T env steps for every env.  ``stats_stream`` (rollout-mode obs stats only): the
+        one-launch moment/episode-stat reduce runs there, ordered after the rollout kernel, so
+        it (and the caller's merge, issued on the same stream) overlaps the value forward and
+        the update; the caller orders its stream after that work before reading the stats."""
         p = self.p
         self.refresh_fwd_image()   # fp8: weights changed during the previous update
         shift = self.stats.shift().clone()
@@ -417,7 +421,13 @@ class HipEngine:
             self._xT_valid = self.xT_from_rollout
             self.env.t += self.T
             # one launch: moments [nblk][2][O] -> s12, episode stats [nblk][2] -> ep_sum
-            self.ext.obs_reduce(self.mom, self.mom.shape[0], self.O, self.s12, self.epstat, self.ep_sum)
+            if stats_stream is not None:
+                stats_stream.wait_stream(torch.cuda.current_stream(self.device))
+                shift.record_stream(stats_stream)
+                with torch.cuda.stream(stats_stream):
+                    self.ext.obs_reduce(self.mom, self.mom.shape[0], self.O, self.s12, self.epstat, self.ep_sum)
+            else:
+                self.ext.obs_reduce(self.mom, self.mom.shape[0], self.O, self.s12, self.epstat, self.ep_sum)
             s1, s2 = self.s12[0], self.s12[1]
             ep = self.ep_sum
         else:

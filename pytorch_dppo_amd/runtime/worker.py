@@ -71,6 +71,17 @@ class DPPOWorker:
         self._perm_gen = torch.Generator(device="cpu")
         self._pending = None          # (async all-reduce work, extra) under --overlap-rollout
         self._staged = None           # metrics of the last deferred iteration (iteration_step(defer=True))
+        # GPU engine: optional side stream for the observation-statistics reduce + all-reduce +
+        # merge (DPPO_STATS_STREAM=1 on, auto: when an RCCL all-reduce sits in that chain, 0 off =
+        # default).  Measured slower on the 1-GPU box: 26.06-26.35 vs 26.43-26.55 M env steps/s
+        # plain, 24.55-24.79 vs 24.85-25.17 M with the RCCL calls forced — the reduce/merge
+        # kernels take CU slots from the LDS-bound value forward and the hand-offs cost more
+        # than the ~15 us (+ all-reduce latency) they hide.
+        mode = os.environ.get("DPPO_STATS_STREAM", "0")
+        want = {"1": True, "0": False}.get(mode, bool(ctx.collective))
+        self._stats_stream = None
+        if want and self.device.type == "cuda" and hasattr(self.engine, "s12"):
+            self._stats_stream = torch.cuda.Stream(device=self.device)
 
     # ---------------------------------------------------------------------------------------
     def _merge_stats(self, count, s1, s2, shift, count_uniform: bool = False) -> None:
@@ -110,7 +121,8 @@ class DPPOWorker:
         t0 = time.perf_counter()
         tm.start("iteration")
         tm.start("rollout")
-        ro = eng.rollout()
+        side = self._stats_stream if p.obs_norm_update == "rollout" else None
+        ro = eng.rollout(stats_stream=side) if side is not None else eng.rollout()
         # --overlap-rollout (SURVEY §5.8 option b): the previous iteration's final gradient
         # all-reduce ran on RCCL's stream concurrently with the rollout kernel just enqueued
         # (which acts with the pre-update weights: a 1-update policy lag, safe for PPO because
@@ -119,7 +131,16 @@ class DPPOWorker:
         tm.stop("rollout")
         tm.start("obs_stats")
         # every rank collects exactly T*E steps -> the global count is host-known (no sync)
-        self._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"], count_uniform=True)
+        stats_done = None
+        if side is not None:
+            # rollout-mode stats feed only the NEXT rollout's normalisation: the reduce, the RCCL
+            # all-reduce and the Chan merge run on a side stream, overlapping values/GAE/update
+            with torch.cuda.stream(side):
+                self._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"], count_uniform=True)
+                stats_done = torch.cuda.Event()
+                stats_done.record(side)
+        else:
+            self._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"], count_uniform=True)
         if p.obs_norm_update == "step" and hasattr(eng, "after_stats_merge"):
             eng.after_stats_merge()
         tm.stop("obs_stats")
@@ -170,6 +191,10 @@ class DPPOWorker:
                     self.ctx.allreduce_grads(eng.grad_flat, mean=mean)
                     eng.apply(extra)
                 self.updates += 1
+        if stats_done is not None:
+            # order the compute stream after the merge: the metrics read the episode stats, and
+            # everything after this iteration (next rollout, snapshots, checkpoints) the stats
+            torch.cuda.current_stream(self.device).wait_event(stats_done)
         tm.stop("update")
         tm.stop("iteration")
         steps_local = eng.T * eng.E

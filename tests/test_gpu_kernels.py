@@ -592,3 +592,25 @@ def test_fused_gather_adam_bit_identical_to_gather_then_adam(dtype, loss, monkey
     assert torch.equal(g0, g1)
     assert abs(mt0["grad_norm"] - mt1["grad_norm"]) <= 1e-5 * (1 + mt1["grad_norm"])
     assert mt0["loss"] == mt1["loss"]
+
+
+def test_side_stream_obs_stats_bit_identical(monkeypatch):
+    """The rollout-mode obs-stat reduce + merge on a side stream (overlapping values/GAE/update)
+    leaves parameters, normaliser state and metrics exactly as the inline path does."""
+    from pytorch_dppo_amd.parallel.dist import DistContext
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    common = dict(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 4,
+                  batch_size=64 * 4, num_epoch=2, dtype="bf16")
+    out = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("DPPO_STATS_STREAM", on)
+        w = DPPOWorker(dppo_preset(**common), DistContext(device=DEV))
+        assert (w._stats_stream is not None) == (on == "1")
+        ms = [w.iteration_step(), w.iteration_step(defer=True), w.iteration_step(defer=True)]
+        ms.append(w.finish_metrics())
+        torch.cuda.synchronize()
+        out.append((w.model.flat.data.clone(), w.stats.mean.clone(), w.stats.mean_diff.clone(), w.stats.n,
+                    repr([(m["mean_ep_return"], m["ep_count"], m["loss"]) for m in ms if m])))
+    a, b = out
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    assert a[3] == b[3] and a[4] == b[4]
