@@ -56,10 +56,12 @@ __global__ __launch_bounds__(256) void obs_reduce_kernel(const float* __restrict
 }
 
 __global__ __launch_bounds__(256) void obs_merge_kernel(const double* __restrict__ s12, int O, double count,
-                                                        double n_a, const float* __restrict__ shift,
+                                                        double n_a, const float* shift,
                                                         double* __restrict__ mean, double* __restrict__ m2,
-                                                        float* __restrict__ mean_f32, float* __restrict__ inv_std,
+                                                        float* mean_f32, float* __restrict__ inv_std,
                                                         double var_floor) {
+  // shift may alias mean_f32 (the rollout takes its moments about the current fp32 mean):
+  // each thread reads shift[d] before it writes mean_f32[d], so neither is __restrict__
   const int d = blockIdx.x * 256 + threadIdx.x;
   if (d >= O) return;
   const double s1 = s12[d], s2 = s12[O + d];

@@ -412,8 +412,10 @@ class HipEngine:
         the update; the caller orders its stream after that work before reading the stats."""
         p = self.p
         self.refresh_fwd_image()   # fp8: weights changed during the previous update
-        shift = self.stats.shift().clone()
         if p.obs_norm_update == "rollout":
+            # the shift IS the fp32 mean, no snapshot copy: its readers are the rollout kernel
+            # and obs_merge, which reads shift[d] before writing mean_f32[d] in the same thread
+            shift = self.stats.shift()
             # full-batch update: the rollout also writes the fragment-major x^T wgrad operand once,
             # so the 10 epochs' fused kernels skip re-transposing X (xT_ready)
             self._launch_rollout(self.T, 0, self.env.t, self.stats, shift,
@@ -431,6 +433,7 @@ class HipEngine:
             s1, s2 = self.s12[0], self.s12[1]
             ep = self.ep_sum
         else:
+            shift = self.stats.shift().clone()
             self.local_stats = RunningObsStats(self.O, self.device)
             self.local_stats.copy_from(self.stats)
             s1 = torch.zeros(self.O, dtype=torch.float64, device=self.device)
