@@ -13,13 +13,17 @@
 namespace {
 
 // One workgroup per 64 consecutive (q, d) columns: lane = column (coalesced 256-B rows), the
-// 4 waves split the blocks (b = wave, wave + 4, ...), then a fixed-order LDS combine —
-// deterministic, and 64x more loads in flight than one thread per column walking all blocks.
+// OR_WAVES waves split the blocks (b = wave, wave + OR_WAVES, ...) with 4 rows' loads in flight
+// per lane, then a fixed-order LDS combine — deterministic.  Only ~13 workgroups exist (2*O/64),
+// so the per-lane chain of dependent loads is the kernel's time: 16 waves x 4 loads in flight
+// walk 256 blocks in 4 round trips (4 waves x 2 loads took 32: 11.6 us).
 // The last workgroup also sums the per-block episode stats [nblk][2] -> ep[2] (fp64).
-__global__ __launch_bounds__(256) void obs_reduce_kernel(const float* __restrict__ part, int nblk, int O,
-                                                         double* __restrict__ s12, const float* __restrict__ epstat,
-                                                         double* __restrict__ ep) {
-  __shared__ double red[4][64];
+constexpr int OR_WAVES = 16;
+__global__ __launch_bounds__(OR_WAVES * 64) void obs_reduce_kernel(const float* __restrict__ part, int nblk, int O,
+                                                                   double* __restrict__ s12,
+                                                                   const float* __restrict__ epstat,
+                                                                   double* __restrict__ ep) {
+  __shared__ double red[OR_WAVES][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ncol = 2 * O;
   const int ngrp = (ncol + 63) / 64;
@@ -39,20 +43,29 @@ __global__ __launch_bounds__(256) void obs_reduce_kernel(const float* __restrict
     return;
   }
   const int i = blockIdx.x * 64 + lane;       // column i = q * O + d of the [2][O] partial
-  double a0 = 0.0, a1 = 0.0;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   if (i < ncol) {
     const float* p = part + i;
     const size_t stride = (size_t)ncol;
     int b = wave;
-    for (; b + 4 < nblk; b += 8) {
-      a0 += p[(size_t)b * stride];
-      a1 += p[(size_t)(b + 4) * stride];
+    for (; b + 3 * OR_WAVES < nblk; b += 4 * OR_WAVES) {
+      const float x0 = p[(size_t)b * stride], x1 = p[(size_t)(b + OR_WAVES) * stride];
+      const float x2 = p[(size_t)(b + 2 * OR_WAVES) * stride], x3 = p[(size_t)(b + 3 * OR_WAVES) * stride];
+      a0 += x0;
+      a1 += x1;
+      a2 += x2;
+      a3 += x3;
     }
-    for (; b < nblk; b += 4) a0 += p[(size_t)b * stride];
+    for (; b < nblk; b += OR_WAVES) a0 += p[(size_t)b * stride];
   }
-  red[wave][lane] = a0 + a1;
+  red[wave][lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
-  if (wave == 0 && i < ncol) s12[i] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (wave == 0 && i < ncol) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < OR_WAVES; ++w) t += red[w][lane];
+    s12[i] = t;
+  }
 }
 
 __global__ __launch_bounds__(256) void obs_merge_kernel(const double* __restrict__ s12, int O, double count,
@@ -85,7 +98,7 @@ __global__ __launch_bounds__(256) void obs_merge_kernel(const double* __restrict
 
 extern "C" void launch_obs_reduce(const float* part, int nblk, int O, double* s12, const float* epstat, double* ep,
                                   hipStream_t s) {
-  hipLaunchKernelGGL(obs_reduce_kernel, dim3((2 * O + 63) / 64 + 1), dim3(256), 0, s, part, nblk, O, s12, epstat, ep);
+  hipLaunchKernelGGL(obs_reduce_kernel, dim3((2 * O + 63) / 64 + 1), dim3(OR_WAVES * 64), 0, s, part, nblk, O, s12, epstat, ep);
   HIP_CHECK_LAUNCH();
 }
 
