@@ -7,22 +7,40 @@ namespace {
 // One lane per env, reverse recurrence over T (train.py:117-122):
 //   delta_t = r_t + gamma*V_{t+1}*(1-d_t) - V_t ;  A_t = delta_t + gamma*lam*(1-d_t)*A_{t+1}
 // [T][E] layout: lanes of a wave read consecutive envs -> coalesced.
-__global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rew, const float* __restrict__ val,
-                                                  const float* __restrict__ done, float* __restrict__ adv,
-                                                  float* __restrict__ ret, int T, int E, float gamma, float lam) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
+// 64-thread workgroups (E/64 of them, spread over more CUs than E/256), and the loads of 8
+// steps are issued before their part of the recurrence (same arithmetic in the same order): the
+// step-at-a-time loop was a chain of T dependent load round trips per lane.
+__global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ rew, const float* __restrict__ val,
+                                                 const float* __restrict__ done, float* __restrict__ adv,
+                                                 float* __restrict__ ret, int T, int E, float gamma, float lam) {
+  const int e = blockIdx.x * 64 + threadIdx.x;
   if (e >= E) return;
   float nxt = 0.f;
   float vnext = val[(size_t)T * E + e];
-  for (int t = T - 1; t >= 0; --t) {
-    const size_t o = (size_t)t * E + e;
-    const float nt = 1.f - done[o];
-    const float v = val[o];
-    const float delta = rew[o] + gamma * vnext * nt - v;
+  auto step = [&](size_t o, float r, float v, float d) {
+    const float nt = 1.f - d;
+    const float delta = r + gamma * vnext * nt - v;
     nxt = delta + gamma * lam * nt * nxt;
     adv[o] = nxt;
     ret[o] = nxt + v;
     vnext = v;
+  };
+  int t = T - 1;
+  for (; t >= 7; t -= 8) {
+    float r[8], v[8], d[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const size_t o = (size_t)(t - k) * E + e;
+      r[k] = rew[o];
+      v[k] = val[o];
+      d[k] = done[o];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) step((size_t)(t - k) * E + e, r[k], v[k], d[k]);
+  }
+  for (; t >= 0; --t) {
+    const size_t o = (size_t)t * E + e;
+    step(o, rew[o], val[o], done[o]);
   }
 }
 
@@ -346,7 +364,7 @@ extern "C" void launch_gae(const float* rewards, const float* values, const floa
   if (scan)
     hipLaunchKernelGGL(gae_scan_kernel, dim3(E), dim3(256), 0, s, rewards, values, dones, adv, ret, T, E, gamma, lam);
   else
-    hipLaunchKernelGGL(gae_kernel, dim3((E + 255) / 256), dim3(256), 0, s, rewards, values, dones, adv, ret, T, E,
+    hipLaunchKernelGGL(gae_kernel, dim3((E + 63) / 64), dim3(64), 0, s, rewards, values, dones, adv, ret, T, E,
                        gamma, lam);
   HIP_CHECK_LAUNCH();
 }
