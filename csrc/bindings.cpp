@@ -18,7 +18,11 @@ hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 // naming the binding — a kernel fault surfaces at the op that caused it, not at a later sync.
 bool g_debug_sync = false;
 void set_debug_sync(bool on) { g_debug_sync = on; }
+// Always: a launch (or LDS attribute) error the launchers recorded raises here, naming the op.
 void after_launch(const char* what) {
+  char msg[192];
+  const int code = dppo_take_error(msg, (int)sizeof(msg));
+  TORCH_CHECK(code == 0, what, ": HIP launch failed: ", msg);
   if (!g_debug_sync) return;
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipStreamSynchronize(cur_stream());
@@ -56,8 +60,10 @@ void set_wgrad_impl(int64_t impl) {
   g_wgrad_impl = (int)impl;
 }
 
+// dt 3 (split-bf16): one 4-byte slot per logical element (hi | lo bf16 pairs in 32-byte groups,
+// csrc/common.h Prec<DT_S3>), held in int32 tensors so numel counts logical elements
 at::ScalarType storage_type(int dt) {
-  return dt == 0 ? at::kFloat : (dt == 1 ? at::kBFloat16 : at::kByte);
+  return dt == 0 ? at::kFloat : (dt == 1 ? at::kBFloat16 : (dt == 3 ? at::kInt : at::kByte));
 }
 
 void check(const torch::Tensor& t, const char* name, at::ScalarType st, int64_t min_numel) {
@@ -331,6 +337,7 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
            int64_t waves) {
   TORCH_CHECK(waves == 8 || (waves == 16 && dt == 1 && g_wgrad_impl == 0),
               "wgrad workgroup waves: 8, or 16 for the bf16 LDS-DMA kernel");
+  TORCH_CHECK(dt != 3 || g_wgrad_impl == 0, "split-bf16 wgrad runs on the LDS-DMA kernel only");
   const int wmax = (int)waves, smax = waves == 16 ? 8 : 6;
   TORCH_CHECK(gT.size() == 6 && xT.size() == 6 && g_rows.size() == 6 && x_rows.size() == 6, "6 layers");
   check(tasks, "tasks", at::kInt, WGRAD_TASK_INTS);
@@ -367,7 +374,7 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
   a.slab = slab.data_ptr<float>();
   a.impl = g_wgrad_impl;
   a.waves = (int)waves;
-  TORCH_CHECK(dt == 0 || dt == 1, "wgrad runs in fp32 or bf16 (the fp8 mode's update is bf16)");
+  TORCH_CHECK(dt == 0 || dt == 1 || dt == 3, "wgrad runs in fp32, bf16 or bf16x3 (the fp8 mode's update is bf16)");
   launch_wgrad((int)dt, a, cur_stream());
   after_launch(__func__);
 }

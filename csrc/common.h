@@ -1,6 +1,7 @@
 // Shared device helpers for the DPPO kernels (gfx950 / CDNA4, wave64).
 //
-// * Prec<DT>: one MFMA "fragment" abstraction for the three operand precisions.
+// * Prec<DT>: one MFMA "fragment" abstraction for the four operand precisions (fp32, bf16,
+//   fp8 e4m3, and split-bf16 "bf16x3" = fp32-accurate on three bf16 MFMAs).
 //   Every fragment holds 8 consecutive K-elements per lane: lane l owns rows/cols (l & 15)
 //   and k = 8*(l >> 4) + j, j = 0..7 — the native operand map of
 //   v_mfma_f32_16x16x32_{bf16,fp8} (cdna_hip_programming.md §3).  The fp32 path issues
@@ -18,7 +19,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
 #define DEV __device__ __forceinline__
 
-enum { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2 };
+enum { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2, DT_S3 = 3 };
 
 template <int DT> struct Prec;
 
@@ -43,6 +44,8 @@ template <> struct Prec<DT_F32> {
   }
   DEV static T cvt(float x) { return x; }
   DEV static float tof(T x) { return x; }
+  DEV static void put(T* b, size_t i, float x) { b[i] = x; }
+  DEV static float get(const T* b, size_t i) { return b[i]; }
 };
 
 template <> struct Prec<DT_BF16> {
@@ -55,7 +58,56 @@ template <> struct Prec<DT_BF16> {
   }
   DEV static T cvt(float x) { return (__bf16)x; }
   DEV static float tof(T x) { return (float)x; }
+  DEV static void put(T* b, size_t i, float x) { b[i] = (__bf16)x; }
+  DEV static float get(const T* b, size_t i) { return (float)b[i]; }
 };
+
+// Split-bf16 "fp32-accurate" operands (DT_S3): x = hi + lo with hi = bf16(x), lo = bf16(x - hi),
+// and a . b ~= hi_a.hi_b + hi_a.lo_b + lo_a.hi_b on three v_mfma_f32_16x16x32_bf16 with fp32
+// accumulation.  The residual (lo_a.lo_b plus each operand's lost tail) is ~2^-16 relative per
+// product; a dot product's error is ~1e-5 relative — the fp32 GEMM tolerances of the tests
+// (2e-5 value forward, 1e-4 gradients) hold at 3x the bf16 MFMA cost, where gfx950's exact
+// v_mfma_f32_16x16x4_f32 runs at 1/16 of the bf16 rate (no xf32 MFMA on CDNA4).
+// Storage: a logical element is a 4-byte slot (T), so every block-level address (row strides,
+// fragment-major fragments, LDS carving) is the fp32 one; inside each 8-aligned group of 8
+// slots (32 bytes) the 8 hi values come first (16 B), then the 8 lo values (16 B).  A fragment
+// (8 consecutive k of one lane) is therefore 32 contiguous bytes: hi | lo, two 16-byte loads.
+// Element i: hi at bf16 index 2*(i & ~7) + (i & 7), lo 8 further.  split(hi + lo) == (hi, lo)
+// exactly (hi + lo is exact in fp32 and RNE ties can only have left hi even), so re-splitting a
+// stored value is lossless.
+struct S3Slot { uint32_t raw; };
+struct S3Frag { bf16x8 h, l; };
+template <> struct Prec<DT_S3> {
+  using T = S3Slot;
+  using Frag = S3Frag;
+  static constexpr int BYTES = 4;
+  DEV static Frag load(const T* p) {
+    const bf16x8* q = reinterpret_cast<const bf16x8*>(p);
+    return Frag{q[0], q[1]};
+  }
+  DEV static f32x4 mma(f32x4 c, const Frag& a, const Frag& b) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
+  }
+  DEV static __bf16* hi_ptr(T* b, size_t i) { return reinterpret_cast<__bf16*>(b) + 2 * (i & ~size_t(7)) + (i & 7); }
+  DEV static const __bf16* hi_ptr(const T* b, size_t i) {
+    return reinterpret_cast<const __bf16*>(b) + 2 * (i & ~size_t(7)) + (i & 7);
+  }
+  DEV static void split(float x, __bf16& h, __bf16& l) {
+    h = (__bf16)x;
+    l = (__bf16)(x - (float)h);
+  }
+  DEV static void put(T* b, size_t i, float x) {
+    __bf16* p = hi_ptr(b, i);
+    split(x, p[0], p[8]);
+  }
+  DEV static float get(const T* b, size_t i) {
+    const __bf16* p = hi_ptr(b, i);
+    return (float)p[0] + (float)p[8];
+  }
+};
+template <int DT> struct IsSplit { static constexpr bool value = DT == DT_S3; };
 
 // OCP e4m3fn (gfx950 native; NOT the MI300 fnuz encoding)
 template <> struct Prec<DT_FP8> {
@@ -76,6 +128,8 @@ template <> struct Prec<DT_FP8> {
     *reinterpret_cast<uint8_t*>(&q) = x;
     return float(q);
   }
+  DEV static void put(T* b, size_t i, float x) { b[i] = cvt(x); }
+  DEV static float get(const T* b, size_t i) { return tof(b[i]); }
 };
 
 // Fragment-major ("FM") layout of a [rows][cols] matrix (rows % 16 == 0, cols % 32 == 0):
@@ -143,25 +197,28 @@ DEV float gauss(uint32_t base, uint32_t env, uint32_t step, uint32_t dim) {
   return (dim & 1u) ? g.y : g.x;
 }
 
+// Launch-error channel (optim.hip): every launcher records the first failed launch or
+// attribute call; every binding (bindings.cpp after_launch) takes it after its launch and raises
+// a Python exception naming the op — a refused launch never leaves a silently stale result.
+extern "C" void dppo_note_error(hipError_t e, const char* file, int line);
+
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) is a driver call (~µs of host time): issue it
 // once per kernel instantiation and only raise it (the attribute is a per-function maximum).
 template <auto Kernel>
 inline void set_max_lds_once(size_t bytes) {
   static size_t set = 0;   // one static per kernel (template on the function pointer itself)
   if (bytes > set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(Kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)bytes);
-    set = bytes;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(Kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) dppo_note_error(e, __FILE__, __LINE__);
+    else set = bytes;
   }
 }
 
-#define HIP_CHECK_LAUNCH()                                                       \
-  do {                                                                           \
-    hipError_t e__ = hipGetLastError();                                          \
-    if (e__ != hipSuccess) {                                                     \
-      fprintf(stderr, "HIP launch error %s at %s:%d\n", hipGetErrorString(e__), \
-              __FILE__, __LINE__);                                               \
-    }                                                                            \
+#define HIP_CHECK_LAUNCH()                                          \
+  do {                                                              \
+    hipError_t e__ = hipGetLastError();                             \
+    if (e__ != hipSuccess) dppo_note_error(e__, __FILE__, __LINE__); \
   } while (0)
 
 // sum_{c < nch} p[c * st] in that fixed order (the split-K slab reduction of the weight gradient):

@@ -110,6 +110,24 @@ DEV void write_transposed(const typename Prec<DT>::T* tile, int ld, int nfeat, v
   using T = typename Prec<DT>::T;
   constexpr int CH = ROWS / 8;
   T* dst = reinterpret_cast<T*>(dstv);
+  if constexpr (IsSplit<DT>::value) {
+    // 8 consecutive m of feature f: their 8 hi then 8 lo bf16 values are one 32-byte FM group
+    using P = Prec<DT>;
+    for (int i = tid; i < nfeat * CH; i += NT) {
+      const int f = i / CH, c = i - f * CH;
+      bf16x8 h, l;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const __bf16* p = P::hi_ptr(tile, (c * 8 + j) * ld + f);
+        h[j] = p[0];
+        l[j] = p[8];
+      }
+      u32x4* o = reinterpret_cast<u32x4*>(P::hi_ptr(dst, fm_index(f, m0 + c * 8, ldT)));
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(&h), o);
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(&l), o + 1);
+    }
+    return;
+  }
   for (int i = tid; i < nfeat * CH; i += NT) {
     const int f = i / CH, c = i - f * CH;
     T buf[8];
@@ -186,8 +204,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_value_kernel(MlpArgs a) {
   if (tid < nvalid) a.v_out[m0 + tid] = V[tid];
 }
 
+// (split-bf16 at 4 waves: the 32-row tile needs ~134 KiB of LDS at Humanoid dims, one workgroup
+// per CU, so each wave may take the whole 512-VGPR budget of its SIMD instead of spilling)
+template <int DT, int NW> struct TrainOcc { static constexpr int V = (DT == DT_S3 && NW == 4) ? 1 : 8 / NW; };
+
 template <int DT, int ROWS, int NW>
-__global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_train_kernel(MlpArgs a) {
+__global__ __launch_bounds__(NW * 64, (TrainOcc<DT, NW>::V)) void mlp_train_kernel(MlpArgs a) {
   using P = Prec<DT>;
   using T = typename P::T;
   constexpr int NT = NW * 64;
@@ -361,7 +383,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_train_kernel(MlpArgs a) {
         const float lsig = cvar * a.log_std[j];
         const float isig = __expf(-lsig);
         const float z = (act_at(q, j) - MU[r * A + j]) * isig;
-        DMU[r * ldmu + j] = P::cvt(valid ? dlogp * z * isig : 0.f);
+        P::put(DMU, r * ldmu + j, valid ? dlogp * z * isig : 0.f);
         // d/dlog_std: logp term + entropy bonus (-ent_coeff * sum_j log sigma_j)
         DLS[r * A + j] = valid ? (dlogp * (z * z - 1.f) - a.ent_coeff) * cvar : 0.f;
         lent += -a.ent_coeff * (0.5f + 0.5f * LOG_2PI_F + lsig);
@@ -389,7 +411,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_train_kernel(MlpArgs a) {
         const float lg = logf(p + 1e-5f);
         lent += -a.ent_coeff * p * lg * invA;
         dp += -a.ent_coeff * invA * (lg + p / (p + 1e-5f));
-        DMU[r * ldmu + j] = P::cvt(valid ? dp * p * (x - mu) / var : 0.f);
+        P::put(DMU, r * ldmu + j, valid ? dp * p * (x - mu) / var : 0.f);
         DLS[r * A + j] = valid ? dp * p * ((x - mu) * (x - mu) / (2.f * var) - 0.5f) : 0.f;
         cf += (fabsf(ratio - 1.f) > a.clip) ? invA : 0.f;
         if (valid) a.mu_prev[(size_t)src * A + j] = mu;   // train.py:164 model_old <- model
@@ -419,7 +441,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_train_kernel(MlpArgs a) {
         else dv = 0.5f * d1 + 0.5f * d2 * inr;
       }
       if (a.loss_kind != 0 && valid) a.v_prev[src] = v;
-      DV[r * ldv] = P::cvt(valid ? dv : 0.f);
+      P::put(DV, r * ldv, valid ? dv : 0.f);
       float* lrow = LOSS + r * NPART_FIXED;
       const float vm = valid ? 1.f : 0.f;
       lrow[0] = lclip * vm; lrow[1] = lv * vm; lrow[2] = lent * vm; lrow[3] = kl * vm; lrow[4] = cf * vm;
@@ -505,6 +527,10 @@ template <int DT>
 int train_rows_t(const MlpArgs& a) {
   if constexpr (DT == DT_F32) {
     return 16;
+  } else if constexpr (DT == DT_S3) {
+    // split-bf16 fragments are fp32-sized: the 64-row / 8-wave form spills (2 x 256 VGPRs per
+    // SIMD is not enough), and at Humanoid dims only the 32-row tile fits LDS anyway
+    return g_rows_override == 16 ? 16 : 32;
   } else {
     const int want = g_rows_override;
     if ((want == 0 || want == 64) && train_lds<DT, 64>(a) <= LDS_MAX) return 64;
@@ -577,24 +603,28 @@ size_t train_lds_any(const MlpArgs& a) {
 extern "C" void launch_mlp_train(int dt, const MlpArgs& a, hipStream_t s) {
   if (dt == DT_F32) train_t<DT_F32>(a, s);
   else if (dt == DT_BF16) train_t<DT_BF16>(a, s);
+  else if (dt == DT_S3) train_t<DT_S3>(a, s);
   else train_t<DT_FP8>(a, s);
 }
 
 extern "C" void launch_mlp_value(int dt, const MlpArgs& a, hipStream_t s) {
   if (dt == DT_F32) value_t<DT_F32>(a, s);
   else if (dt == DT_BF16) value_t<DT_BF16>(a, s);
+  else if (dt == DT_S3) value_t<DT_S3>(a, s);
   else value_t<DT_FP8>(a, s);
 }
 
 extern "C" size_t mlp_train_lds_bytes(int dt, const MlpArgs& a) {
   if (dt == DT_F32) return train_lds_any<DT_F32>(a);
   if (dt == DT_BF16) return train_lds_any<DT_BF16>(a);
+  if (dt == DT_S3) return train_lds_any<DT_S3>(a);
   return train_lds_any<DT_FP8>(a);
 }
 
 extern "C" int mlp_train_rows(int dt, const MlpArgs& a) {
   if (dt == DT_F32) return train_rows_t<DT_F32>(a);
   if (dt == DT_BF16) return train_rows_t<DT_BF16>(a);
+  if (dt == DT_S3) return train_rows_t<DT_S3>(a);
   return train_rows_t<DT_FP8>(a);
 }
 

@@ -80,6 +80,7 @@ DEV void cvt4(const f32x4& v, typename Prec<DT>::T (&q)[4]) {
 // images every layer re-reads from L2.
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __attribute__((ext_vector_type(4))) float f32x4s;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4v;
 template <int DT>
 DEV void store4q_T(typename Prec<DT>::T* dst, const typename Prec<DT>::T (&q)[4]) {
   if constexpr (DT == DT_F32) {
@@ -227,32 +228,53 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
               // out holds h = tanh(pre) of this layer's input; dpre = v * (1 - h^2)
               f32x4 h;
 #pragma unroll
-              for (int i = 0; i < 4; ++i) h[i] = P::tof(out[(r0 + i) * ldo + c]);
+              for (int i = 0; i < 4; ++i) h[i] = P::get(out, (r0 + i) * ldo + c);
               v = v * (1.0f - h * h);
             }
-            typename P::T q[4];
-            cvt4<DT>(v, q);
-            if constexpr (EPI != EPI_DTANH_GLOBAL) {
-              if constexpr (DT == DT_BF16) {
-                // 2-byte row stores straight from the two packed dwords (ds_write_b16 /
-                // ds_write_b16_d16_hi): no second per-value conversion
-                uint32_t wx = reinterpret_cast<const uint32_t*>(q)[0];
-                uint32_t wy = reinterpret_cast<const uint32_t*>(q)[1];
-                // opaque: otherwise LLVM folds trunc(cvt_pk(a, b)) back into a per-value cvt
-                asm volatile("" : "+v"(wx), "+v"(wy));
-                const uint2 w = make_uint2(wx, wy);
-                uint16_t* o16 = reinterpret_cast<uint16_t*>(out);
-                o16[(r0 + 0) * ldo + c] = (uint16_t)w.x;
-                o16[(r0 + 1) * ldo + c] = (uint16_t)(w.x >> 16);
-                o16[(r0 + 2) * ldo + c] = (uint16_t)w.y;
-                o16[(r0 + 3) * ldo + c] = (uint16_t)(w.y >> 16);
-              } else {
+            if constexpr (IsSplit<DT>::value) {
+              // split-bf16: hi = bf16(v), lo = bf16(v - hi), 4-wide (packed converts); LDS row
+              // stores per element, and the transposed operand's 4 consecutive m as one 8-byte
+              // hi store + one 8-byte lo store (the 4 slots share one 8-group: m0 + r0 % 4 == 0)
+              const bf16x4v hv = __builtin_convertvector(v, bf16x4v);
+              const bf16x4v lv = __builtin_convertvector(v - __builtin_convertvector(hv, f32x4), bf16x4v);
+              if constexpr (EPI != EPI_DTANH_GLOBAL) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) out[(r0 + i) * ldo + c] = q[i];
+                for (int i = 0; i < 4; ++i) {
+                  __bf16* p = P::hi_ptr(out, (r0 + i) * ldo + c);
+                  p[0] = hv[i];
+                  p[8] = lv[i];
+                }
               }
+              if (outT != nullptr) {
+                __bf16* p = P::hi_ptr(outT, fm_index(c, m0 + r0, ldT));
+                __builtin_nontemporal_store(*reinterpret_cast<const u32x2*>(&hv), reinterpret_cast<u32x2*>(p));
+                __builtin_nontemporal_store(*reinterpret_cast<const u32x2*>(&lv), reinterpret_cast<u32x2*>(p + 8));
+              }
+            } else {
+              typename P::T q[4];
+              cvt4<DT>(v, q);
+              if constexpr (EPI != EPI_DTANH_GLOBAL) {
+                if constexpr (DT == DT_BF16) {
+                  // 2-byte row stores straight from the two packed dwords (ds_write_b16 /
+                  // ds_write_b16_d16_hi): no second per-value conversion
+                  uint32_t wx = reinterpret_cast<const uint32_t*>(q)[0];
+                  uint32_t wy = reinterpret_cast<const uint32_t*>(q)[1];
+                  // opaque: otherwise LLVM folds trunc(cvt_pk(a, b)) back into a per-value cvt
+                  asm volatile("" : "+v"(wx), "+v"(wy));
+                  const uint2 w = make_uint2(wx, wy);
+                  uint16_t* o16 = reinterpret_cast<uint16_t*>(out);
+                  o16[(r0 + 0) * ldo + c] = (uint16_t)w.x;
+                  o16[(r0 + 1) * ldo + c] = (uint16_t)(w.x >> 16);
+                  o16[(r0 + 2) * ldo + c] = (uint16_t)w.y;
+                  o16[(r0 + 3) * ldo + c] = (uint16_t)(w.y >> 16);
+                } else {
+#pragma unroll
+                  for (int i = 0; i < 4; ++i) out[(r0 + i) * ldo + c] = q[i];
+                }
+              }
+              if (outT != nullptr)   // FM wgrad operand: 4 consecutive m of feature c are contiguous
+                store4q_T<DT>(outT + fm_index(c, m0 + r0, ldT), q);
             }
-            if (outT != nullptr)   // FM wgrad operand: 4 consecutive m of feature c are contiguous
-              store4q_T<DT>(outT + fm_index(c, m0 + r0, ldT), q);
           }
         }
       }
@@ -318,11 +340,10 @@ struct LdsCarve {
 template <int DT>
 DEV void preset_pad(typename Prec<DT>::T* H, int ld, int rows, int c0, int tid, int nthreads) {
   using P = Prec<DT>;
-  const typename P::T zero = P::cvt(0.f), one = P::cvt(1.f);
   for (int r = tid; r < rows; r += nthreads) {
     typename P::T* h = H + r * ld;
-    h[c0] = one;
-    for (int c = c0 + 1; c < ld; ++c) h[c] = zero;
+    P::put(h, c0, 1.f);
+    for (int c = c0 + 1; c < ld; ++c) P::put(h, c, 0.f);
   }
 }
 

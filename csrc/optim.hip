@@ -1,4 +1,6 @@
 // GAE scan and fused Adam + global-norm clip + weight-image refresh (K12, K16).
+#include <stdio.h>
+
 #include "kernels.h"
 #include "mlp_core.h"
 
@@ -162,9 +164,9 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     p[i] = pi;
     const int wi = w_map[i];
     if (wi >= 0) {
-      const typename P::T q = P::cvt(qmul ? pi * qmul[i] : pi);
-      wimg[wi] = q;
-      wimg[wt_map[i]] = q;
+      const float q = qmul ? pi * qmul[i] : pi;
+      P::put(wimg, wi, q);
+      P::put(wimg, wt_map[i], q);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -204,9 +206,9 @@ __global__ __launch_bounds__(256) void adam_noclip_kernel(float* __restrict__ p,
     p[i] = pi;
     const int wi = w_map[i];
     if (wi >= 0) {
-      const typename P::T q = P::cvt(qmul ? pi * qmul[i] : pi);
-      wimg[wi] = q;
-      wimg[wt_map[i]] = q;
+      const float q = qmul ? pi * qmul[i] : pi;
+      P::put(wimg, wi, q);
+      P::put(wimg, wt_map[i], q);
     }
   }
   __shared__ float red[256];
@@ -255,9 +257,9 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
     v[i] = vi;
     p[i] = pi;
     if (wi >= 0) {
-      const typename P::T q = P::cvt(qmul ? pi * qmul[i] : pi);
-      wimg[wi] = q;
-      wimg[wt_map[i]] = q;
+      const float q = qmul ? pi * qmul[i] : pi;
+      P::put(wimg, wi, q);
+      P::put(wimg, wt_map[i], q);
     }
   };
   if ((int)blockIdx.x < nred) {
@@ -318,9 +320,9 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ p, 
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const int wi = w_map[i];
     if (wi >= 0) {
-      const typename P::T q = P::cvt(qmul ? p[i] * qmul[i] : p[i]);
-      wimg[wi] = q;
-      wimg[wt_map[i]] = q;
+      const float q = qmul ? p[i] * qmul[i] : p[i];
+      P::put(wimg, wi, q);
+      P::put(wimg, wt_map[i], q);
     }
   }
 }
@@ -348,6 +350,24 @@ __global__ __launch_bounds__(256) void metrics_pack_kernel(const double* __restr
   if (t == 0) out[10] = sqrt(red[0]);
   if (t < 2) out[t] = ep[t];
   if (t < 8) out[2 + t] = (double)loss8[t];
+}
+
+namespace {
+hipError_t g_err = hipSuccess;
+char g_err_where[160];
+}  // namespace
+
+extern "C" void dppo_note_error(hipError_t e, const char* file, int line) {
+  if (g_err != hipSuccess) return;   // keep the first one
+  g_err = e;
+  snprintf(g_err_where, sizeof(g_err_where), "%s at %s:%d", hipGetErrorString(e), file, line);
+}
+
+extern "C" int dppo_take_error(char* msg, int cap) {
+  const int code = (int)g_err;
+  if (code != 0 && msg != nullptr && cap > 0) snprintf(msg, (size_t)cap, "%s", g_err_where);
+  g_err = hipSuccess;
+  return code;
 }
 
 extern "C" void launch_metrics_pack(const double* ep, const float* loss8, const float* norm_part, int nblk,
@@ -384,6 +404,9 @@ extern "C" void launch_adam(float* p, const float* g, float* m, float* v, int n,
     else if (dt == DT_BF16)
       hipLaunchKernelGGL(adam_noclip_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
                          step, state, norm_part, (__bf16*)wimg, w_map, wt_map, img_scale);
+    else if (dt == DT_S3)
+      hipLaunchKernelGGL(adam_noclip_kernel<DT_S3>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
+                         step, state, norm_part, (S3Slot*)wimg, w_map, wt_map, img_scale);
     else
       hipLaunchKernelGGL(adam_noclip_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
                          step, state, norm_part, (uint8_t*)wimg, w_map, wt_map, img_scale);
@@ -397,6 +420,9 @@ extern "C" void launch_adam(float* p, const float* g, float* m, float* v, int n,
   else if (dt == DT_BF16)
     hipLaunchKernelGGL(adam_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
                        state, norm_part, nblk, (__bf16*)wimg, w_map, wt_map, img_scale);
+  else if (dt == DT_S3)
+    hipLaunchKernelGGL(adam_kernel<DT_S3>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
+                       state, norm_part, nblk, (S3Slot*)wimg, w_map, wt_map, img_scale);
   else
     hipLaunchKernelGGL(adam_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
                        state, norm_part, nblk, (uint8_t*)wimg, w_map, wt_map, img_scale);
@@ -416,6 +442,9 @@ extern "C" void launch_gather_adam(const float* slab, const int* src_off, const 
   else if (dt == DT_BF16)
     hipLaunchKernelGGL(gather_adam_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (__bf16*)wimg, w_map,
                        wt_map, img_scale);
+  else if (dt == DT_S3)
+    hipLaunchKernelGGL(gather_adam_kernel<DT_S3>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (S3Slot*)wimg, w_map,
+                       wt_map, img_scale);
   else
     hipLaunchKernelGGL(gather_adam_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (uint8_t*)wimg, w_map,
                        wt_map, img_scale);
@@ -431,6 +460,8 @@ extern "C" void launch_pack(const float* p, int n, void* wimg, const int* w_map,
     hipLaunchKernelGGL(pack_kernel<DT_F32>, dim3(grid), dim3(256), 0, s, p, n, (float*)wimg, w_map, wt_map, img_scale);
   else if (dt == DT_BF16)
     hipLaunchKernelGGL(pack_kernel<DT_BF16>, dim3(grid), dim3(256), 0, s, p, n, (__bf16*)wimg, w_map, wt_map, img_scale);
+  else if (dt == DT_S3)
+    hipLaunchKernelGGL(pack_kernel<DT_S3>, dim3(grid), dim3(256), 0, s, p, n, (S3Slot*)wimg, w_map, wt_map, img_scale);
   else
     hipLaunchKernelGGL(pack_kernel<DT_FP8>, dim3(grid), dim3(256), 0, s, p, n, (uint8_t*)wimg, w_map, wt_map, img_scale);
   HIP_CHECK_LAUNCH();

@@ -88,11 +88,11 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   }
   for (int i = tid; i < ROWS * ld2; i += NTHR) {
     int c = i % ld2;
-    h1[i] = P::cvt(c == a.n1 ? 1.f : 0.f);
+    P::put(h1, i, c == a.n1 ? 1.f : 0.f);
   }
   for (int i = tid; i < ROWS * ld3; i += NTHR) {
     int c = i % ld3;
-    h2[i] = P::cvt(c == a.n2 ? 1.f : 0.f);
+    P::put(h2, i, c == a.n2 ? 1.f : 0.f);
   }
   for (int d = tid; d < O; d += NTHR) { s1[d] = 0.f; s2[d] = 0.f; }
   for (int d = tid; d < S; d += NTHR) {   // per-dim constants once per launch (no per-step modulo)
@@ -114,7 +114,12 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   if (tid < O) { hm = a.mean[tid]; his = a.inv_std[tid]; hsh = a.shift[tid]; }
   BPre<DT, ROWS / 16> pf;   // cross-barrier weight prefetch of each layer's first k-chunk
   // bf16 / fp32: the LDS tile and the buffer share the element type (fp8 tiles feed a bf16 buffer)
-  constexpr bool XO_FROM_LDS = sizeof(T) == sizeof(typename PX::T) && sizeof(T) == 2;
+  // (split-bf16: the LDS tile and the buffer share the 32-byte hi|lo group layout too)
+  constexpr bool SPLIT = IsSplit<DT>::value;
+  constexpr bool XO_FROM_LDS = (sizeof(T) == sizeof(typename PX::T) && sizeof(T) == 2) || SPLIT;
+  // the observe loop keeps this feature's ROWS values in the buffer type, or as fp32 for split
+  // storage (split once, at the 32-byte x^T group store)
+  using GT = std::conditional_t<SPLIT, float, typename PX::T>;
   // phase timeline (diagnostics, a.tstamp != null): per-wave shader-clock cycles summed over
   // the steps for each phase, written by lane 0 of every wave of every workgroup
   unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
         float m = hm, is = his, sh = hsh;
         if (d != tid && d < O) { m = a.mean[d]; is = a.inv_std[d]; sh = a.shift[d]; }
         float ls1 = 0.f, ls2 = 0.f;
-        typename PX::T grp[ROWS];   // this feature's ROWS consecutive buffer rows (xT groups of 8)
+        GT grp[ROWS];   // this feature's ROWS consecutive buffer rows (xT groups of 8)
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
           float xv;
@@ -148,8 +153,9 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
           } else {
             xv = (d == O) ? 1.f : 0.f;
           }
-          xs[r * ld1 + d] = P::cvt(xv);
-          grp[r] = PX::cvt(xv);
+          P::put(xs, r * ld1 + d, xv);
+          if constexpr (SPLIT) grp[r] = xv;
+          else grp[r] = PX::cvt(xv);
           if constexpr (!XO_FROM_LDS)
             if (r < nvalid) xo[((size_t)tb * a.buf_E + e0 + r) * a.d1 + d] = grp[r];
         }
@@ -162,7 +168,19 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
 #pragma unroll
           for (int g = 0; g < ROWS / 8; ++g) {
             typename PX::T* o = xT + fm_index(d, mrow + 8 * g, a.ldT);
-            if constexpr (sizeof(typename PX::T) == 2) {
+            if constexpr (SPLIT) {
+              bf16x8 hv, lv;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                __bf16 h, l;
+                Prec<DT_S3>::split(grp[8 * g + j], h, l);
+                hv[j] = h;
+                lv[j] = l;
+              }
+              uint4* o4 = reinterpret_cast<uint4*>(o);
+              o4[0] = *reinterpret_cast<const uint4*>(&hv);
+              o4[1] = *reinterpret_cast<const uint4*>(&lv);
+            } else if constexpr (sizeof(typename PX::T) == 2) {
               *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(&grp[8 * g]);
             } else {
               reinterpret_cast<uint4*>(o)[0] = reinterpret_cast<const uint4*>(&grp[8 * g])[0];
@@ -177,13 +195,15 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
     if (!last) layer_prefetch<DT, ROWS, NW>(pf, W1, a.d1, a.n1, wave, lane);
     __syncthreads();
     if constexpr (XO_FROM_LDS) {
-      // row-major buffer rows from the normalised LDS tile: one 16-byte store per 8 features
-      // instead of ROWS 2-byte stores per feature (fire-and-forget, overlaps the MFMA layers)
-      const int ch = a.d1 / 8;
+      // row-major buffer rows from the normalised LDS tile: one 16-byte store per 16 bytes of
+      // features instead of ROWS element stores per feature (fire-and-forget, overlaps the MFMA
+      // layers)
+      constexpr int EPC = 16 / sizeof(T);
+      const int ch = a.d1 / EPC;
       for (int i = tid; i < nvalid * ch; i += NTHR) {
         const int r = i / ch, c = i - r * ch;
-        *reinterpret_cast<uint4*>(xo + ((size_t)tb * a.buf_E + e0 + r) * a.d1 + c * 8) =
-            *reinterpret_cast<const uint4*>(xs + r * ld1 + c * 8);
+        *reinterpret_cast<uint4*>(xo + ((size_t)tb * a.buf_E + e0 + r) * a.d1 + c * EPC) =
+            *reinterpret_cast<const uint4*>(xs + r * ld1 + c * EPC);
       }
     }
     if (last) break;
@@ -400,7 +420,7 @@ void launch_nw(const RolloutArgs& a, hipStream_t s) {
 template <int DT, int ROWS>
 void launch_t(const RolloutArgs& a, hipStream_t s) {
   // fp32 operands and 32-env tiles: the 8-wave form spills (twice the fragment registers)
-  if (g_rollout_waves == 4 || DT == DT_F32 || ROWS > 16) launch_nw<DT, ROWS, 4>(a, s);
+  if (g_rollout_waves == 4 || DT == DT_F32 || DT == DT_S3 || ROWS > 16) launch_nw<DT, ROWS, 4>(a, s);
   else launch_nw<DT, ROWS, 8>(a, s);
 }
 
@@ -412,10 +432,12 @@ extern "C" void launch_rollout(int dt, const RolloutArgs& a, int rows, hipStream
   if (rows == 32) {
     if (dt == DT_F32) launch_t<DT_F32, 32>(a, s);
     else if (dt == DT_BF16) launch_t<DT_BF16, 32>(a, s);
+    else if (dt == DT_S3) launch_t<DT_S3, 32>(a, s);
     else launch_t<DT_FP8, 32>(a, s);
   } else {
     if (dt == DT_F32) launch_t<DT_F32, 16>(a, s);
     else if (dt == DT_BF16) launch_t<DT_BF16, 16>(a, s);
+    else if (dt == DT_S3) launch_t<DT_S3, 16>(a, s);
     else launch_t<DT_FP8, 16>(a, s);
   }
 }

@@ -151,8 +151,13 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
 #pragma unroll
     for (int q = 0; q < C; ++q)
 #pragma unroll
-      for (int h = 0; h < NI; ++h)
-        glds16(src[q] + (size_t)kk * FB + h * 1024 + lane * 16, st + dst[q] + h * 1024);
+      for (int h = 0; h < NI; ++h) {
+        // split-bf16 fragments (32 B per lane: hi | lo) are de-interleaved by the DMA itself:
+        // instruction h moves every lane's h-th 16 bytes, so LDS holds the hi block, then the
+        // lo block, each read conflict-free at lane * 16
+        const size_t go = IsSplit<DT>::value ? (size_t)lane * 32 + h * 16 : (size_t)h * 1024 + lane * 16;
+        glds16(src[q] + (size_t)kk * FB + go, st + dst[q] + h * 1024);
+      }
   };
   const bool active = wave < tk.nq * tk.kq;
   const int wn = wave / tk.kq, wk = wave - (wave / tk.kq) * tk.kq;
@@ -170,10 +175,18 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
     if (active) {
       const char* st = smem + (k % S) * SB;
       Frag af[4], bf[4];
+      auto lds_frag = [&](int f) {
+        if constexpr (IsSplit<DT>::value) {
+          const char* b = st + f * FB + lane * 16;
+          return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + 1024)};
+        } else {
+          return P::load(reinterpret_cast<const T*>(st + f * FB) + lane * 8);
+        }
+      };
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        af[i] = P::load(reinterpret_cast<const T*>(st + (wn * 4 + i) * FB) + lane * 8);
-        bf[i] = P::load(reinterpret_cast<const T*>(st + (NF + wk * 4 + i) * FB) + lane * 8);
+        af[i] = lds_frag(wn * 4 + i);
+        bf[i] = lds_frag(NF + wk * 4 + i);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -267,11 +280,13 @@ extern "C" void set_wgrad_stages(int st) { g_wgrad_stages = (st == 3 || st == 6)
 extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
   if (a.ntasks <= 0) return;
   const dim3 block(WG_WAVES * 64);
-  if (a.impl == 1) {
+  if (a.impl == 1) {   // (bindings.cpp rejects the split-bf16 operands here)
     if (dt == DT_F32) hipLaunchKernelGGL(wgrad_reg_kernel<DT_F32>, dim3(a.ntasks), block, 0, s, a);
     else hipLaunchKernelGGL(wgrad_reg_kernel<DT_BF16>, dim3(a.ntasks), block, 0, s, a);
   } else if (dt == DT_F32) {
     launch_wgrad_lds<DT_F32, 3>(a, s);
+  } else if (dt == DT_S3) {
+    launch_wgrad_lds<DT_S3, 3>(a, s);
   } else if (a.waves == 16) {
     launch_wgrad_lds<DT_BF16, 4, 16>(a, s);
   } else if (g_wgrad_stages == 3) {

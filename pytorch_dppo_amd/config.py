@@ -44,7 +44,8 @@ class Params:
     # ---- MI355X-native additions --------------------------------------
     device: str = "cpu"                  # cpu | gpu
     num_envs: int = 1                    # E vectorised envs per worker
-    dtype: str = "fp32"                  # fp32 | bf16 | fp8  (GEMM operand precision)
+    dtype: str = "fp32"                  # fp32 | bf16x3 | bf16 | fp8  (GEMM operand precision;
+                                         # bf16x3 = fp32-accurate split-bf16 on the bf16 MFMA)
     hidden: tuple = (100, 100)           # model.py:11-12
     value_mult: int = 5                  # model.py:17 (value fc1 = hidden[0]*5)
     loss: str = "ppo"                    # ppo (corrected, ppo.py:148-167) | dppo_ref (train.py:142-161)
@@ -95,8 +96,8 @@ class Params:
         self.adam_betas = tuple(float(b) for b in self.adam_betas)
         if self.device not in ("cpu", "gpu"):
             raise ValueError(f"device must be cpu|gpu, got {self.device}")
-        if self.dtype not in ("fp32", "bf16", "fp8"):
-            raise ValueError(f"dtype must be fp32|bf16|fp8, got {self.dtype}")
+        if self.dtype not in ("fp32", "bf16x3", "bf16", "fp8"):
+            raise ValueError(f"dtype must be fp32|bf16x3|bf16|fp8, got {self.dtype}")
         if self.loss not in ("ppo", "dppo_ref"):
             raise ValueError(f"loss must be ppo|dppo_ref, got {self.loss}")
         if self.value_loss not in ("mse", "clipped_half"):

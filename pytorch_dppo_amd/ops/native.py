@@ -11,7 +11,8 @@ import os
 
 _MOD = None
 
-DT_CODE = {"fp32": 0, "bf16": 1, "fp8": 2}
+# bf16x3: split-bf16 operands, fp32-accurate on three bf16 MFMAs (ops/storage.py)
+DT_CODE = {"fp32": 0, "bf16": 1, "fp8": 2, "bf16x3": 3}
 
 
 def load(build_if_missing: bool = False):

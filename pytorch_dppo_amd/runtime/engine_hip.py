@@ -24,11 +24,11 @@ import torch
 
 from ..config import Params
 from ..models.actor_critic import ActorCritic, PackedLayout, fm_index
-from ..ops import native
+from ..ops import native, storage
 from ..utils import rng
 from ..utils.obs_stats import RunningObsStats
 
-STORAGE = {0: torch.float32, 1: torch.bfloat16, 2: torch.uint8}
+STORAGE = storage.STORAGE
 NPART_FIXED = 8
 WT = 128            # operand-buffer row padding (csrc/kernels.h WGRAD_TILE)
 
@@ -162,7 +162,7 @@ class HipEngine:
         cols = torch.arange(self.ldT, device=device)
         for buf, r in ((self.h1pT, lp1.fan_out), (self.h2pT, lp2.fan_out), (self.h1vT, lv1.fan_out),
                        (self.h2vT, lv2.fan_out)):
-            buf.view(-1)[fm_index(torch.full_like(cols, r), cols, self.ldT)] = 1.0
+            storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), 1.0, self.dt)
         self.split_grad = False          # bucketed gradient (enable_bucketed_grad, multi-rank)
         # wgrad workgroup waves: 8 (A/B: 16-wave workgroups with up to 16-quadrant tiles stream
         # fewer operand rows — 1,792 vs 2,304 per step for v_fc1 — but took 243 vs 226 us per
@@ -370,6 +370,13 @@ class HipEngine:
         self.qscale.copy_(s)
         qmul = torch.where(self.layer_id >= 0, (1.0 / s)[self.layer_id.clamp(min=0)], torch.zeros_like(flat))
         self.ext.pack(flat, self.wimg_fwd, self.w_map, self.wt_map, self.dt_fwd, qmul)
+
+    def decode(self, t: torch.Tensor) -> torch.Tensor:
+        """a storage-precision buffer of this engine (x_buf, an operand buffer) as fp32"""
+        return storage.decode(t, self.dt)
+
+    def encode(self, x: torch.Tensor) -> torch.Tensor:
+        return storage.encode(x, self.dt)
 
     def current_obs(self) -> torch.Tensor:
         return self.env.observe()

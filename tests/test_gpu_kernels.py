@@ -1,6 +1,7 @@
 """HIP kernel numerics vs the plain-PyTorch fp32 oracle (SURVEY §4 'Unit: HIP kernels').
 
-fp32 operands run the exact-f32 MFMA path (v_mfma_f32_16x16x4_f32) -> tight tolerances;
+fp32 operands run the exact-f32 MFMA path (v_mfma_f32_16x16x4_f32) and bf16x3 (split-bf16 hi/lo
+operands on three bf16 MFMAs, the fp32-accurate fast mode) -> the same tight tolerances;
 bf16 operands -> loose, relative budgets.  Shapes cover Pendulum (3/1), HalfCheetah (17/6)
 and Humanoid (376/17) dims with odd E and padded tails.
 """
@@ -12,7 +13,7 @@ import torch
 from pytorch_dppo_amd.config import Params, dppo_preset, ppo_preset
 from pytorch_dppo_amd.envs import get_spec, make_vec_env
 from pytorch_dppo_amd.models.actor_critic import ActorCritic
-from pytorch_dppo_amd.ops import oracle
+from pytorch_dppo_amd.ops import oracle, storage
 from pytorch_dppo_amd.utils.obs_stats import RunningObsStats
 
 pytestmark = pytest.mark.gpu
@@ -49,17 +50,22 @@ def test_extension_loads_for_gfx950():
     assert ext.__file__.endswith(".so")
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3"])
 def test_pack_matches_reference_layout(dtype):
     p = dppo_preset(device="gpu", env_name="HalfCheetah-v2", num_envs=64, exploration_size=256,
                     batch_size=256, dtype=dtype)
     eng, model, _, _ = _engine(p)
-    ref = model.packed_layout().pack(model.flat.data, eng.sdtype)
-    assert torch.equal(eng.wimg.float(), ref.float())
+    ref = storage.encode(model.packed_layout().pack(model.flat.data), eng.dt)
+    assert torch.equal(eng.wimg, ref)       # bit-exact, incl. the device hi/lo split (RNE both)
+    if dtype == "bf16x3":
+        err = (eng.decode(eng.wimg) - model.packed_layout().pack(model.flat.data)).abs().max().item()
+        assert err <= 2 ** -16 * model.flat.data.abs().max().item()
 
 
 @pytest.mark.parametrize("env_name,dtype,tol", [("Pendulum-v0", "fp32", 2e-5), ("HalfCheetah-v2", "fp32", 2e-5),
-                                                ("Humanoid-v2", "fp32", 5e-5), ("Humanoid-v2", "bf16", 3e-2),
+                                                ("Humanoid-v2", "fp32", 5e-5), ("Pendulum-v0", "bf16x3", 2e-5),
+                                                ("HalfCheetah-v2", "bf16x3", 2e-5), ("Humanoid-v2", "bf16x3", 5e-5),
+                                                ("Humanoid-v2", "bf16", 3e-2),
                                                 ("Humanoid-v2", "fp8", 1.5e-1), ("HalfCheetah-v2", "fp8", 1.5e-1)])
 def test_value_forward(env_name, dtype, tol):
     p = dppo_preset(device="gpu", env_name=env_name, num_envs=37, exploration_size=37 * 5,
@@ -71,10 +77,10 @@ def test_value_forward(env_name, dtype, tol):
     xb = torch.zeros(M, eng.d0, device=DEV)
     xb[:, :O] = x
     xb[:, O] = 1.0
-    eng.x_buf.copy_(xb.to(eng.sdtype))
+    eng.x_buf.copy_(eng.encode(xb))
     eng.values()
     with torch.no_grad():
-        _, _, v = model(eng.x_buf[:, :O].float())
+        _, _, v = model(eng.decode(eng.x_buf)[:, :O])
     err = (eng.values_buf - v.reshape(-1)).abs().max().item()
     scale = v.abs().max().item() + 1e-3
     assert err / scale < tol, (err, scale)
@@ -90,10 +96,12 @@ def _torch_rollout(params, model, seed_state_from):
     return eng
 
 
-@pytest.mark.parametrize("env_name", ["Pendulum-v0", "HalfCheetah-v2", "Humanoid-v2"])
-def test_rollout_matches_torch_engine(env_name):
+@pytest.mark.parametrize("env_name,dtype", [("Pendulum-v0", "fp32"), ("HalfCheetah-v2", "fp32"), ("Humanoid-v2", "fp32"),
+                                            ("Pendulum-v0", "bf16x3"), ("HalfCheetah-v2", "bf16x3"),
+                                            ("Humanoid-v2", "bf16x3")])
+def test_rollout_matches_torch_engine(env_name, dtype):
     p = dppo_preset(device="gpu", env_name=env_name, num_envs=45, exploration_size=45 * 8,
-                    batch_size=45 * 8, dtype="fp32")
+                    batch_size=45 * 8, dtype=dtype)
     eng, model, env, stats = _engine(p)
     stats.observes(env.observe())
     with torch.no_grad():
@@ -109,16 +117,23 @@ def test_rollout_matches_torch_engine(env_name):
     assert torch.allclose(eng.logp.view(T, E), ref.logp, atol=1e-4, rtol=1e-5)
     assert torch.allclose(eng.rewards.view(T, E), ref.rewards, atol=2e-4, rtol=1e-4)
     assert torch.equal(eng.dones.view(T, E), ref.dones)
-    xk = eng.x_buf.float().view(T + 1, E, -1)[..., :O]
+    xk = eng.decode(eng.x_buf).view(T + 1, E, -1)[..., :O]
     assert torch.allclose(xk, ref.x, atol=2e-4, rtol=1e-4)
     assert torch.allclose(env.state, ref.env.state, atol=2e-4, rtol=1e-4)
     assert torch.allclose(ro_h["s1"], ro_t["s1"], rtol=1e-4, atol=1e-2)
+    # sum of squares of the moment partials too (a bug there only shows via the variance)
+    s2_scale = ro_t["s2"].abs().max().item() + 1.0
+    assert torch.allclose(ro_h["s2"], ro_t["s2"], rtol=1e-4, atol=1e-4 * s2_scale)
     assert abs(ro_h["ep_count"] - ro_t["ep_count"]) < 0.5
 
 
-def test_obs_reduce_and_merge_kernels_match_torch_welford():
+@pytest.mark.parametrize("O,nblk,alias", [(37, 19, False), (376, 259, True)])
+def test_obs_reduce_and_merge_kernels_match_torch_welford(O, nblk, alias):
+    """O=37/19 blocks: two column groups, one ragged, tail loop only.  O=376/259 blocks:
+    the 4-rows-in-flight loop of obs_reduce plus an uneven remainder and the episode-stat block's
+    strided loop past 64 blocks; and obs_merge with shift ALIASING mean_f32, as the engine calls it
+    (the kernel must read shift[d] before it writes mean_f32[d])."""
     ext = _ext()
-    O, nblk = 37, 19     # 2*O = 74 columns: two column groups, one ragged
     g = torch.Generator(device="cpu").manual_seed(4)
     ref = RunningObsStats(O, DEV)
     dev_st = RunningObsStats(O, DEV)
@@ -137,7 +152,10 @@ def test_obs_reduce_and_merge_kernels_match_torch_welford():
         assert torch.allclose(s12[0], s1, rtol=1e-5, atol=1e-3)
         assert torch.allclose(s12[1], s2, rtol=1e-5, atol=1e-2)
         assert torch.allclose(ep, epstat.double().sum(0), rtol=1e-12)
-        ext.obs_merge(s12, float(nblk * 8), float(dev_st.n), dev_st.shift().clone(), dev_st.mean, dev_st.mean_diff,
+        sh = dev_st.shift() if alias else dev_st.shift().clone()
+        if alias:
+            assert sh.data_ptr() == dev_st.mean_f32.data_ptr()
+        ext.obs_merge(s12, float(nblk * 8), float(dev_st.n), sh, dev_st.mean, dev_st.mean_diff,
                       dev_st.mean_f32, dev_st.inv_std_f32, 1e-2)
         dev_st.n += nblk * 8
     assert torch.allclose(dev_st.mean, ref.mean, rtol=1e-5, atol=1e-4)
@@ -169,8 +187,8 @@ def _fill_buffer(eng, model, gen_seed=3):
     xb = torch.zeros(N + eng.E, eng.d0, device=DEV)
     xb[:, :O] = x
     xb[:, O] = 1.0
-    eng.x_buf.copy_(xb.to(eng.sdtype))
-    xq = eng.x_buf.float()[:N, :O]
+    eng.x_buf.copy_(eng.encode(xb))
+    xq = eng.decode(eng.x_buf)[:N, :O]
     with torch.no_grad():
         mu, ls, v = model(xq)
     a = (mu + 0.6 * torch.randn(N, A, generator=g).to(DEV))
@@ -201,6 +219,10 @@ def _torch_grad(model, p, xq, eng, idx):
     ("Humanoid-v2", "fp32", "clipped_half", "std", 512, 2e-4),
     ("Humanoid-v2", "bf16", "mse", "std", 512, 6e-2),
     ("Pendulum-v0", "fp32", "mse", "std", 64, 1e-4),
+    ("HalfCheetah-v2", "bf16x3", "mse", "std", 256, 1e-4),
+    ("HalfCheetah-v2", "bf16x3", "clipped_half", "var", 200, 1e-4),
+    ("Humanoid-v2", "bf16x3", "clipped_half", "std", 512, 2e-4),
+    ("Pendulum-v0", "bf16x3", "mse", "std", 64, 1e-4),
 ])
 def test_fused_loss_backward_matches_autograd(env_name, dtype, value_loss, conv, mb, tol):
     p = ppo_preset(device="gpu", env_name=env_name, num_envs=64, exploration_size=64 * 8,
@@ -243,17 +265,18 @@ def test_fused_loss_backward_row_tiles(rows, env_name, mb):
         assert rel < 6e-2, rel
         eng.values()
         with torch.no_grad():
-            _, _, v = model(eng.x_buf[:, :model.num_inputs].float())
+            _, _, v = model(eng.decode(eng.x_buf)[:, :model.num_inputs])
         err = (eng.values_buf - v.reshape(-1)).abs().max().item()
         assert err / (v.abs().max().item() + 1e-3) < 3e-2, err
     finally:
         ext.set_mlp_rows(0)
 
 
-def test_rollout_written_xT_equals_kernel_written_xT():
+@pytest.mark.parametrize("dtype", ["bf16", "bf16x3"])
+def test_rollout_written_xT_equals_kernel_written_xT(dtype):
     """full-batch: the x^T operand the rollout emits == the one mlp_train would transpose."""
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 4,
-                    batch_size=64 * 4, dtype="bf16")
+                    batch_size=64 * 4, dtype=dtype)
     eng, model, env, stats = _engine(p)
     stats.observes(env.observe())
     assert eng.xT_from_rollout
@@ -326,7 +349,7 @@ def test_adam_kernel_matches_oracle(max_norm):
             oracle.clip_grad_norm_(gr, max_norm)
         oracle.adam_step_(p_ref, gr, m_ref, v_ref, step, p.lr, p.adam_betas, p.adam_eps)
     assert torch.allclose(model.flat.data, p_ref, atol=1e-6, rtol=1e-5)
-    ref_img = model.packed_layout().pack(model.flat.data, eng.sdtype)
+    ref_img = storage.encode(model.packed_layout().pack(model.flat.data), eng.dt)
     assert torch.equal(eng.wimg, ref_img)
 
 
@@ -567,7 +590,7 @@ def test_debug_sync_mode_runs_an_iteration_bit_identical():
     assert torch.equal(out[0], out[1])
 
 
-@pytest.mark.parametrize("dtype,loss", [("bf16", "ppo"), ("fp32", "ppo"), ("bf16", "dppo_ref")])
+@pytest.mark.parametrize("dtype,loss", [("bf16", "ppo"), ("fp32", "ppo"), ("bf16", "dppo_ref"), ("bf16x3", "ppo")])
 def test_fused_gather_adam_bit_identical_to_gather_then_adam(dtype, loss, monkeypatch):
     """World size 1 runs grad_gather + no-clip Adam as ONE launch (gather_adam): parameters, Adam
     moments and weight images after a full iteration equal the two-launch path's bit for bit."""
@@ -614,3 +637,89 @@ def test_side_stream_obs_stats_bit_identical(monkeypatch):
     a, b = out
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
     assert a[3] == b[3] and a[4] == b[4]
+
+
+@pytest.mark.parametrize("dtype,tol", [("bf16x3", 2e-4), ("bf16", 6e-2)])
+def test_bench_geometry_full_batch_gradient_matches_autograd(dtype, tol):
+    """The benchmarked geometry exactly (bench.py defaults): Humanoid-v2, E=4096, T=16, one
+    full-batch step of 65,536 rows, x^T written by the rollout kernel (xT_ready), the 256-task
+    wgrad plan with up to 1,024 batch chunks — vs fp32 autograd on the same decoded buffer."""
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=4096 * 16,
+                    batch_size=4096 * 16, dtype=dtype, num_epoch=1)
+    eng, model, env, stats = _engine(p)
+    stats.observes(env.observe())
+    assert eng.xT_from_rollout and eng.N == 65536
+    assert sum(b["tasks_host"].numel() // 8 for b in eng.buckets) >= 200
+    eng.rollout()
+    eng.values()
+    eng.gae()
+    eng.begin_update()
+    assert eng._xT_valid
+    eng.grad(None)
+    xq = eng.decode(eng.x_buf)[:eng.N, :model.num_inputs]
+    model.flat.grad = None
+    mu, ls, v = model(xq)
+    out = oracle.ppo_loss(mu, ls, v, eng.actions, eng.logp, eng.adv, eng.ret, eng.values_buf[:eng.N],
+                          clip=p.clip, ent_coeff=p.ent_coeff, value_loss=p.value_loss, convention=p.std_convention)
+    out["loss"].backward()
+    g_ref = model.flat.grad.detach()
+    rel = (eng.grad_flat - g_ref).norm().item() / (g_ref.norm().item() + 1e-12)
+    assert rel < tol, rel
+    # per-layer too: no layer may hide behind the others' norm
+    for name in ("p_fc1", "p_fc2", "mu", "v_fc1", "v_fc2", "v"):
+        o, n = model.offsets[f"{name}.weight"]
+        gr, gk = g_ref[o:o + n], eng.grad_flat[o:o + n]
+        assert (gk - gr).norm().item() <= 3 * tol * (gr.norm().item() + 1e-8), name
+
+
+@pytest.mark.parametrize("env_name", ["Humanoid-v2"])
+def test_rollout_bf16_eight_wave_kernel_tracks_torch_engine(env_name):
+    """The benchmarked bf16 rollout variant (rollout_kernel<bf16, 16 envs, 8 waves>) vs the torch
+    engine with the same noise: log-probs depend only on the noise (tight), actions/obs carry the
+    bf16 policy error (loose), done flags are action-independent (exact)."""
+    p = dppo_preset(device="gpu", env_name=env_name, num_envs=64, exploration_size=64 * 8,
+                    batch_size=64 * 8, dtype="bf16")
+    eng, model, env, stats = _engine(p)
+    stats.observes(env.observe())
+    eng.params_changed()
+    p_cpu = Params.from_dict({**p.to_dict(), "device": "cpu"})
+    ref = _torch_rollout(p_cpu, model, stats)
+    eng.rollout()
+    ref.rollout()
+    T, E = eng.T, eng.E
+    assert torch.allclose(eng.logp.view(T, E), ref.logp, atol=1e-4, rtol=1e-5)
+    assert torch.equal(eng.dones.view(T, E), ref.dones)
+    da = (eng.actions.view(T, E, -1) - ref.actions).abs()
+    assert da.max().item() < 5e-2 and da.mean().item() < 5e-3, (da.max().item(), da.mean().item())
+    xk = eng.decode(eng.x_buf).view(T + 1, E, -1)[..., :model.num_inputs]
+    dx = (xk - ref.x).abs()
+    assert dx.max().item() < 5e-2 and dx.mean().item() < 5e-3, (dx.max().item(), dx.mean().item())
+
+
+def test_learning_reduced_precision_tracks_fp32_accurate():
+    """GPU learning check: 24 DPPO iterations of synthetic Humanoid at each
+    precision from the same seed.  Each run must learn (late return well above the first
+    iterations'), and the bf16 / fp8 curves must end within a band of the fp32-accurate
+    (bf16x3) curve."""
+    from pytorch_dppo_amd.parallel.dist import DistContext
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    curves = {}
+    for dt in ("bf16x3", "bf16", "fp8"):
+        p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=1024, exploration_size=1024 * 16,
+                        batch_size=1024 * 16, num_epoch=10, dtype=dt, seed=11)
+        w = DPPOWorker(p, DistContext(device=DEV))
+        r = []
+        for _ in range(24):
+            w.iteration_step()
+            # mean per-step (clipped) reward of the iteration's rollout: episode returns would
+            # also grow with episode length alone
+            r.append(w.engine.rewards.mean().item())
+        curves[dt] = r
+    import statistics
+    late = {k: statistics.fmean(v[-6:]) for k, v in curves.items()}
+    early = {k: statistics.fmean(v[:3]) for k, v in curves.items()}
+    print("learning curves (mean step reward)", {k: [round(x, 4) for x in v] for k, v in curves.items()})
+    for k in curves:
+        assert late[k] > early[k] + 0.02, (k, early[k], late[k])
+    for k in ("bf16", "fp8"):
+        assert abs(late[k] - late["bf16x3"]) <= 0.25 * abs(late["bf16x3"] - early["bf16x3"]) + 0.01, (k, late)
