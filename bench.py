@@ -11,8 +11,13 @@ rollout of T x E = 16 x 4096 = 65,536 env steps (Humanoid-v2 dims: obs 376, act 
 dynamics), value forward, GAE, then 10 epochs, each ONE synchronous global step on the full
 65,536-row batch (reference: batch_size == exploration_size, main.py:20,28), each with the
 RCCL all-reduce of the flat gradient and the fused Adam step.  Per-GPU work is fixed as N
-grows (weak scaling).  Model: the reference actor-critic (model.py), random init, bf16 MFMA
-operands with fp32 master weights/accumulation.
+grows (weak scaling).  Model: the reference actor-critic (model.py), random init.
+
+Precision: the headline runs at the reference's precision, fp32 (model.py / train.py are fp32
+end to end): ``--dtype bf16x3`` = every GEMM on split-bf16 operands (x = hi + lo, three bf16
+MFMAs per product, fp32 accumulate; fp32 tolerances in tests/test_gpu_kernels.py), fp32 master
+weights, fp32 loss/GAE/Adam.  The reduced-precision modes (bf16, fp8 forward) are timed in the
+same invocation on the same config and reported as separately labelled ``variants``.
 
 Timing: W untimed warmup iterations; barrier + device sync; K timed iterations; barrier +
 device sync; the max over ranks of the elapsed time.  Rank 0 prints ONE JSON line.  The
@@ -38,6 +43,8 @@ METRIC = "env steps/sec (whole node), MuJoCo Humanoid-v2, 8 DPPO workers"
 # BASELINE.md derived estimate for the reference on this metric: 0.8-1.6e3 steps/s per node
 # (8 workers).  We divide by the UPPER end (conservative).
 BASELINE_VALUE = 1.6e3
+# JSON "dtype" labels: bf16x3 IS fp32-accurate compute (split-bf16 operands, fp32 accumulate)
+DTYPE_LABEL = {"bf16x3": "fp32_3xbf16", "fp32": "fp32", "bf16": "bf16", "fp8": "fp8_e4m3_fwd+bf16_update"}
 
 
 def main():
@@ -49,7 +56,12 @@ def main():
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--rollout-len", type=int, default=16)
     ap.add_argument("--num-epoch", type=int, default=10)
-    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--dtype", default="bf16x3",
+                    help="headline operand precision: bf16x3 (fp32-accurate, default), fp32 (exact f32 MFMA), "
+                         "bf16, fp8")
+    ap.add_argument("--variants", default="bf16,fp8",
+                    help="comma list of extra dtypes timed after the headline on the same config "
+                         "(reported under 'variants'; '' = none)")
     ap.add_argument("--batch-size", type=int, default=0, help="0 = full buffer (reference DPPO)")
     ap.add_argument("--overlap-rollout", action="store_true",
                     help="overlap the final gradient all-reduce with the next rollout (1-update lag)")
@@ -77,56 +89,75 @@ def main():
     ctx.force_collectives = args.force_collectives
     E, T = args.num_envs, args.rollout_len
     rows = E * T
-    p = dppo_preset(device="gpu", env_name=args.env_name, num_envs=E, exploration_size=rows,
-                    batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=args.dtype,
-                    num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
-                    use_graphs=args.graphs, grad_buckets=args.grad_buckets,
-                    phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
-    w = DPPOWorker(p, ctx)
-    for i in range(args.warmup):
-        m = w.iteration_step()
-        if args.verbose and ctx.rank == 0:
-            print("warmup", i, json.dumps({k: round(v, 4) if isinstance(v, float) else v for k, v in m.items()}),
-                  file=sys.stderr, flush=True)
-    ctx.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    # the production loop (run_worker): each iteration's metrics are read one iteration later,
-    # so the host enqueues the next rollout while the device still runs this update.  Every
-    # kernel of all K iterations is inside the timed region (closing synchronize below).
-    for i in range(args.steps):
-        mi = w.iteration_step(defer=True)
-        if args.verbose and ctx.rank == 0 and mi:
-            print("step", i, json.dumps({k: round(v, 4) if isinstance(v, float) else v for k, v in mi.items()}),
-                  file=sys.stderr, flush=True)
-    ctx.barrier()
-    torch.cuda.synchronize()
-    el = torch.tensor([time.perf_counter() - t0], device=ctx.device, dtype=torch.float64)
-    m = w.finish_metrics() or m
-    if args.verify_sync:
-        in_sync = ctx.verify_replicas(w.model.flat.data)
-        if ctx.rank == 0:
-            print(f"replicas_in_sync {in_sync}", file=sys.stderr, flush=True)
-        if not in_sync:
-            raise SystemExit("replicas diverged")
-    el = el.to(ctx.device)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+
+    def run(dtype: str):
+        """W untimed + K timed iterations at ``dtype``: (elapsed max over ranks, params, worker, metrics)"""
+        p = dppo_preset(device="gpu", env_name=args.env_name, num_envs=E, exploration_size=rows,
+                        batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=dtype,
+                        num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
+                        use_graphs=args.graphs, grad_buckets=args.grad_buckets,
+                        phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
+        w = DPPOWorker(p, ctx)
+        m = {}
+        for i in range(args.warmup):
+            m = w.iteration_step()
+            if args.verbose and ctx.rank == 0:
+                print(dtype, "warmup", i, json.dumps({k: round(v, 4) if isinstance(v, float) else v
+                                                      for k, v in m.items()}), file=sys.stderr, flush=True)
+        ctx.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        # the production loop (run_worker): each iteration's metrics are read one iteration later,
+        # so the host enqueues the next rollout while the device still runs this update.  Every
+        # kernel of all K iterations is inside the timed region (closing synchronize below).
+        for i in range(args.steps):
+            mi = w.iteration_step(defer=True)
+            if args.verbose and ctx.rank == 0 and mi:
+                print(dtype, "step", i, json.dumps({k: round(v, 4) if isinstance(v, float) else v
+                                                    for k, v in mi.items()}), file=sys.stderr, flush=True)
+        ctx.barrier()
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], device=ctx.device, dtype=torch.float64)
+        m = w.finish_metrics() or m
+        if args.verify_sync:
+            in_sync = ctx.verify_replicas(w.model.flat.data)
+            if ctx.rank == 0:
+                print(f"{dtype} replicas_in_sync {in_sync}", file=sys.stderr, flush=True)
+            if not in_sync:
+                raise SystemExit("replicas diverged")
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item()), p, w, m
+
+    elapsed, p, w, m = run(args.dtype)
     total_steps = rows * ctx.world_size * args.steps
     value = total_steps / elapsed
+    bucketed = bool(w.bucketed)
+    del w
+    variants = {}
+    for dt in [d for d in args.variants.split(",") if d and d != args.dtype]:
+        el_v, _, wv, _ = run(dt)
+        variants[dt] = {"value": total_steps / el_v, "ms_per_step": el_v / args.steps * 1e3,
+                        "dtype": DTYPE_LABEL[dt], "vs_headline": (total_steps / el_v) / value}
+        del wv
+        torch.cuda.empty_cache()
     if ctx.rank == 0:
         out = {"metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": ctx.world_size,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": value / BASELINE_VALUE,
-               "dtype": args.dtype, "data": "synthetic (Humanoid-v2 obs/act dims, random-init weights)",
+               "dtype": DTYPE_LABEL[args.dtype], "data": "synthetic (Humanoid-v2 obs/act dims, random-init weights)",
                "config": {"model": "reference actor-critic MLP (policy 376-100-100-17, value 376-500-100-1)",
                           "global_batch": rows * ctx.world_size, "seq_len": T,
-                          "parallelism": f"dp{ctx.world_size}", "env": args.env_name, "num_envs_per_gpu": E,
+                          "parallelism": f"dp{ctx.world_size}", "env": args.env_name,
+                          "dppo_workers": ctx.world_size, "workers_per_gpu": 1, "num_envs_per_gpu": E,
                           "rollout_len": T, "num_epoch": args.num_epoch,
                           "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout, "graphs": args.graphs,
-                          "grad_buckets": bool(w.bucketed),
+                          "grad_buckets": bucketed,
+                          "note": ("value = total env steps/s of all n_gpus workers (one DPPO worker per GPU); "
+                                   "the 8-worker node figure of the metric is the n_gpus=8 run; vs_baseline "
+                                   "divides by the reference's derived 8-worker CPU node estimate (BASELINE.md)"),
                           "last_iter": {k: m[k] for k in ("loss", "mean_ep_return", "ms_rollout", "ms_values_gae",
-                                                          "ms_update", "ms_obs_stats") if k in m}}}
+                                                          "ms_update", "ms_obs_stats") if k in m}},
+               "variants": variants}
         print(json.dumps(out), flush=True)
     ctx.destroy()
 

@@ -305,7 +305,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   a.xT_ready = xT_ready ? 1 : 0;
   a.ablate = g_train_ablate;
   if (g_tstamp != nullptr) {
-    const int64_t nw = ROWS == 64 ? 8 : 4;
+    const int64_t nw = mlp_train_waves((int)dt, a);
     TORCH_CHECK(g_tstamp_numel >= ((nblk + g_tstamp_every - 1) / g_tstamp_every) * nw * 16, "tstamp buffer too small");
     a.tstamp = g_tstamp;
     a.tstamp_every = g_tstamp_every;
@@ -541,6 +541,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("train_lds_bytes", &train_lds_bytes);
   m.def("train_rows", &train_rows);
   m.def("set_mlp_rows", &set_mlp_rows);
+  m.def("set_s3_train_waves", [](int64_t nw) {
+    TORCH_CHECK(nw == 4 || nw == 8, "split-bf16 train waves: 4 or 8");
+    set_s3_train_waves((int)nw);
+  });
   m.def("set_debug_sync", &set_debug_sync);
   m.def("set_rollout_waves", [](int64_t nw) {
     TORCH_CHECK(nw == 4 || nw == 8, "rollout waves: 4 or 8");

@@ -570,12 +570,31 @@ void value_launch(const MlpArgs& a, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+// waves of the 32-row split-bf16 workgroup: 4 (one wave per SIMD, 512 VGPRs each) or 8 (two
+// per SIMD at <= 256 VGPRs: the second wave hides the first's L2 / LDS latency).  Measured
+// (scripts/ab_train.py, bench geometry): 8 waves 290 us vs 4 waves 361 us per call.
+int g_s3_train_waves = 8;
+
+template <int DT>
+int train_waves_t(const MlpArgs& a) {
+  const int rows = train_rows_t<DT>(a);
+  if (rows == 64) return 8;
+  if (DT == DT_S3 && rows == 32 && g_s3_train_waves == 8) return 8;
+  return 4;
+}
+
 template <int DT>
 void train_t(const MlpArgs& a, hipStream_t s) {
   if constexpr (DT == DT_F32) {
     train_launch<DT, 16, 4>(a, s);
   } else {
     const int rows = train_rows_t<DT>(a);
+    if constexpr (DT == DT_S3) {
+      if (rows == 32 && train_waves_t<DT>(a) == 8) {
+        train_launch<DT, 32, 8>(a, s);
+        return;
+      }
+    }
     if (rows == 64) train_launch<DT, 64, 8>(a, s);
     else if (rows == 16) train_launch<DT, 16, 4>(a, s);
     else train_launch<DT, 32, 4>(a, s);
@@ -629,3 +648,10 @@ extern "C" int mlp_train_rows(int dt, const MlpArgs& a) {
 }
 
 extern "C" void set_mlp_rows_override(int rows) { g_rows_override = rows; }
+extern "C" void set_s3_train_waves(int nw) { g_s3_train_waves = nw == 8 ? 8 : 4; }
+extern "C" int mlp_train_waves(int dt, const MlpArgs& a) {
+  if (dt == DT_F32) return 4;
+  if (dt == DT_BF16) return train_waves_t<DT_BF16>(a);
+  if (dt == DT_S3) return train_waves_t<DT_S3>(a);
+  return train_waves_t<DT_FP8>(a);
+}

@@ -92,7 +92,9 @@ DEV void store4q_T(typename Prec<DT>::T* dst, const typename Prec<DT>::T (&q)[4]
   }
 }
 
-template <int DT, int RB> struct KChunk { static constexpr int KC = 2; };
+// (split-bf16 fragments are twice the registers: one k-step per chunk keeps the 8-wave, 2-waves-
+// per-SIMD form inside 256 VGPRs; the second wave per SIMD hides the latency instead)
+template <int DT, int RB> struct KChunk { static constexpr int KC = IsSplit<DT>::value ? 1 : 2; };
 
 // B fragments of a wave's FIRST (tile pair, k-chunk) step of one layer_gemm call, loaded ahead
 // of time by layer_prefetch: weights do not depend on the previous layer, so their L2 latency
@@ -227,8 +229,16 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
             } else if constexpr (EPI == EPI_DTANH_INPLACE || EPI == EPI_DTANH_GLOBAL) {
               // out holds h = tanh(pre) of this layer's input; dpre = v * (1 - h^2)
               f32x4 h;
+              if constexpr (IsSplit<DT>::value) {
+                // rows r0..r0+3 of column c: one per-lane base, then a fixed row stride (ldo is
+                // a multiple of 8, so the hi|lo group arithmetic is per column only)
+                const __bf16* hp = P::hi_ptr(out, (size_t)r0 * ldo + c);
 #pragma unroll
-              for (int i = 0; i < 4; ++i) h[i] = P::get(out, (r0 + i) * ldo + c);
+                for (int i = 0; i < 4; ++i) h[i] = (float)hp[2 * i * ldo] + (float)hp[2 * i * ldo + 8];
+              } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) h[i] = P::get(out, (r0 + i) * ldo + c);
+              }
               v = v * (1.0f - h * h);
             }
             if constexpr (IsSplit<DT>::value) {
@@ -238,11 +248,11 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
               const bf16x4v hv = __builtin_convertvector(v, bf16x4v);
               const bf16x4v lv = __builtin_convertvector(v - __builtin_convertvector(hv, f32x4), bf16x4v);
               if constexpr (EPI != EPI_DTANH_GLOBAL) {
+                __bf16* p = P::hi_ptr(out, (size_t)r0 * ldo + c);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                  __bf16* p = P::hi_ptr(out, (r0 + i) * ldo + c);
-                  p[0] = hv[i];
-                  p[8] = lv[i];
+                  p[2 * i * ldo] = hv[i];
+                  p[2 * i * ldo + 8] = lv[i];
                 }
               }
               if (outT != nullptr) {
@@ -335,15 +345,31 @@ struct LdsCarve {
 };
 
 // Columns [c0, ld) of a rows x ld activation tile: column c0 = 1 (the constant bias input of
-// the next layer), the rest 0.  Columns < c0 are NOT touched: the producing layer's epilogue
-// writes every row of them (layer_gemm stores all ROWS rows of each column c < n_real).
+// the next layer), the rest 0.  Written as whole 16-byte chunks (split-bf16: 32-byte hi|lo
+// groups) from the chunk holding c0 on, so the columns of that chunk below c0 are zeroed too:
+// callers preset BEFORE the producing layer's epilogue writes every row of the columns
+// c < n_real (layer_gemm stores all ROWS rows of each of them), behind a barrier.
 template <int DT>
 DEV void preset_pad(typename Prec<DT>::T* H, int ld, int rows, int c0, int tid, int nthreads) {
   using P = Prec<DT>;
-  for (int r = tid; r < rows; r += nthreads) {
-    typename P::T* h = H + r * ld;
-    P::put(h, c0, 1.f);
-    for (int c = c0 + 1; c < ld; ++c) P::put(h, c, 0.f);
+  constexpr bool SPLIT = IsSplit<DT>::value;
+  constexpr int G = SPLIT ? 8 : 16 / P::BYTES;   // logical elements per chunk (ld % G == 0)
+  const int g0 = c0 / G, ng = ld / G - g0;
+  for (int i = tid; i < rows * ng; i += nthreads) {
+    const int r = i / ng, g = g0 + (i - r * ng);
+    const int one = c0 - g * G;                   // column c0 inside this chunk, if it is here
+    // the 1.0 bit pattern of the storage type, placed in dword `wi` at bit `sh` (register
+    // selects only: a dynamically indexed local array would live in scratch)
+    constexpr int EPW = 4 / (SPLIT ? 2 : P::BYTES);   // elements per dword
+    constexpr uint32_t ONE = (SPLIT || DT == DT_BF16) ? 0x3F80u : (DT == DT_F32 ? 0x3F800000u : 0x38u);
+    const bool here = one >= 0 && one < G;
+    const int wi = one / EPW, sh = (one - wi * EPW) * (32 / EPW);
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = (here && wi == k) ? (ONE << sh) : 0u;
+    uint4* dst = reinterpret_cast<uint4*>(H + (size_t)r * ld + (size_t)g * G);
+    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    if constexpr (SPLIT) dst[1] = make_uint4(0, 0, 0, 0);             // lo of the group
   }
 }
 

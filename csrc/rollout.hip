@@ -86,14 +86,8 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
     int r = i / S, d = i - r * S;
     st[i] = (r < nvalid) ? a.state[(size_t)(e0 + r) * S + d] : 0.f;
   }
-  for (int i = tid; i < ROWS * ld2; i += NTHR) {
-    int c = i % ld2;
-    P::put(h1, i, c == a.n1 ? 1.f : 0.f);
-  }
-  for (int i = tid; i < ROWS * ld3; i += NTHR) {
-    int c = i % ld3;
-    P::put(h2, i, c == a.n2 ? 1.f : 0.f);
-  }
+  preset_pad<DT>(h1, ld2, ROWS, a.n1, tid, NTHR);   // the layers' epilogues write columns < n
+  preset_pad<DT>(h2, ld3, ROWS, a.n2, tid, NTHR);
   for (int d = tid; d < O; d += NTHR) { s1[d] = 0.f; s2[d] = 0.f; }
   for (int d = tid; d < S; d += NTHR) {   // per-dim constants once per launch (no per-step modulo)
     wdrv[d] = 0.5f + (float)(d % 7) / 7.0f;
@@ -420,7 +414,7 @@ void launch_nw(const RolloutArgs& a, hipStream_t s) {
 template <int DT, int ROWS>
 void launch_t(const RolloutArgs& a, hipStream_t s) {
   // fp32 operands and 32-env tiles: the 8-wave form spills (twice the fragment registers)
-  if (g_rollout_waves == 4 || DT == DT_F32 || DT == DT_S3 || ROWS > 16) launch_nw<DT, ROWS, 4>(a, s);
+  if (g_rollout_waves == 4 || DT == DT_F32 || ROWS > 16) launch_nw<DT, ROWS, 4>(a, s);
   else launch_nw<DT, ROWS, 8>(a, s);
 }
 

@@ -16,7 +16,7 @@ for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
   i=$((i+1))
   echo "== pass $i: $P"
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $P --kernel-include-regex "$REGEX" -d "$OUT/pmc/p$i" -o run \
-      --output-format csv -- python3 bench.py --steps 1 --warmup 1 > "$OUT/pmc/p$i.log" 2>&1
+      --output-format csv -- python3 bench.py --steps 1 --warmup 1 --variants "" ${BENCH_ARGS:-} > "$OUT/pmc/p$i.log" 2>&1
   rc=$?
   echo "rc=$rc"
   [ $rc -eq 0 ] || { tail -20 "$OUT/pmc/p$i.log"; [ $rc -ge 124 ] && exit $rc; }

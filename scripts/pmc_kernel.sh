@@ -14,7 +14,7 @@ for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT
          "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -k 10 120 rocprofv3 --kernel-trace --pmc $P --kernel-include-regex "$REGEX" -d "$OUT/p$i" -o run \
-      --output-format csv -- python3 bench.py --steps 1 --warmup 1 > "$OUT/p$i.log" 2>&1
+      --output-format csv -- python3 bench.py --steps 1 --warmup 1 --variants "" ${BENCH_ARGS:-} > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.log"; exit $rc; }
