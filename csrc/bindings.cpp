@@ -431,7 +431,8 @@ void obs_merge(torch::Tensor s12, double count, double n_a, torch::Tensor shift,
 }
 
 void gae(torch::Tensor rewards, torch::Tensor values, torch::Tensor dones, torch::Tensor adv, torch::Tensor ret,
-         double gamma, double lam, int64_t mode) {
+         double gamma, double lam, int64_t mode, int64_t seg) {
+  TORCH_CHECK(seg >= 0, "segment length must be >= 0 (0: no segment cut)");
   TORCH_CHECK(rewards.dim() == 2, "rewards [T,E]");
   TORCH_CHECK(mode >= 0 && mode <= 2, "gae mode: 0 auto, 1 per-env lanes, 2 parallel-in-time scan");
   const int64_t T = rewards.size(0), E = rewards.size(1);
@@ -441,7 +442,7 @@ void gae(torch::Tensor rewards, torch::Tensor values, torch::Tensor dones, torch
   check(adv, "adv", at::kFloat, T * E);
   check(ret, "ret", at::kFloat, T * E);
   launch_gae(rewards.data_ptr<float>(), values.data_ptr<float>(), dones.data_ptr<float>(), adv.data_ptr<float>(),
-             ret.data_ptr<float>(), (int)T, (int)E, (float)gamma, (float)lam, (int)mode, cur_stream());
+             ret.data_ptr<float>(), (int)T, (int)E, (float)gamma, (float)lam, (int)mode, (int)seg, cur_stream());
   after_launch(__func__);
 }
 

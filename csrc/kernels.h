@@ -133,7 +133,7 @@ void launch_grad_gather(const float* slab, const int* src_off, const int* src_me
                         int npart, int A, float scale, float* grad, int i_lo, int i_hi, int with_partials,
                         float* loss_out, hipStream_t s);
 void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
-                int T, int E, float gamma, float lam, int mode, hipStream_t s);
+                int T, int E, float gamma, float lam, int mode, int seg, hipStream_t s);
 void set_adam_fused(int on);
 void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, float b1, float b2,
                  float eps, float max_norm, float* state, float* norm_part, int nblk,

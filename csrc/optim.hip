@@ -12,17 +12,21 @@ namespace {
 // 64-thread workgroups (E/64 of them, spread over more CUs than E/256), and the loads of 8
 // steps are issued before their part of the recurrence (same arithmetic in the same order): the
 // step-at-a-time loop was a chain of T dependent load round trips per lane.
+// seg > 0: the reference's segment length num_steps (train.py:82) — after every seg steps the
+// recursion restarts (A_{t+1} masked) while the not-done bootstrap V_{t+1} stays in delta.
 __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ rew, const float* __restrict__ val,
                                                  const float* __restrict__ done, float* __restrict__ adv,
-                                                 float* __restrict__ ret, int T, int E, float gamma, float lam) {
+                                                 float* __restrict__ ret, int T, int E, float gamma, float lam,
+                                                 int seg) {
   const int e = blockIdx.x * 64 + threadIdx.x;
   if (e >= E) return;
   float nxt = 0.f;
   float vnext = val[(size_t)T * E + e];
-  auto step = [&](size_t o, float r, float v, float d) {
+  auto step = [&](int t, size_t o, float r, float v, float d) {
     const float nt = 1.f - d;
     const float delta = r + gamma * vnext * nt - v;
-    nxt = delta + gamma * lam * nt * nxt;
+    const float cont = (seg > 0 && (t + 1) % seg == 0) ? 0.f : 1.f;
+    nxt = delta + gamma * lam * nt * cont * nxt;
     adv[o] = nxt;
     ret[o] = nxt + v;
     vnext = v;
@@ -38,11 +42,11 @@ __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ rew, 
       d[k] = done[o];
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) step((size_t)(t - k) * E + e, r[k], v[k], d[k]);
+    for (int k = 0; k < 8; ++k) step(t - k, (size_t)(t - k) * E + e, r[k], v[k], d[k]);
   }
   for (; t >= 0; --t) {
     const size_t o = (size_t)t * E + e;
-    step(o, rew[o], val[o], done[o]);
+    step(t, o, rew[o], val[o], done[o]);
   }
 }
 
@@ -57,7 +61,7 @@ __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ rew, 
 __global__ __launch_bounds__(256) void gae_scan_kernel(const float* __restrict__ rew, const float* __restrict__ val,
                                                        const float* __restrict__ done, float* __restrict__ adv,
                                                        float* __restrict__ ret, int T, int E, float gamma,
-                                                       float lam) {
+                                                       float lam, int seg) {
   __shared__ float sD[256], sC[256];
   const int e = blockIdx.x, j = threadIdx.x;
   const int chunk = (T + 255) / 256;
@@ -66,7 +70,7 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float* __restrict__
     const size_t o = (size_t)t * E + e;
     const float nt = 1.f - done[o];
     delta = rew[o] + gamma * val[o + E] * nt - val[o];
-    c = gamma * lam * nt;
+    c = (seg > 0 && (t + 1) % seg == 0) ? 0.f : gamma * lam * nt;
   };
   float D = 0.f, C = 1.f;
   for (int t = t1 - 1; t >= t0; --t) {
@@ -377,15 +381,16 @@ extern "C" void launch_metrics_pack(const double* ep, const float* loss8, const 
 }
 
 extern "C" void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
-                           int T, int E, float gamma, float lam, int mode, hipStream_t s) {
+                           int T, int E, float gamma, float lam, int mode, int seg, hipStream_t s) {
   // mode 0 = auto: the per-env lane scan keeps >= 1 full wave busy per env batch; with few envs
   // and a long horizon its single dependent chain per lane is the latency, so scan in time.
   const bool scan = mode == 2 || (mode == 0 && E <= 64 && T >= 512);
   if (scan)
-    hipLaunchKernelGGL(gae_scan_kernel, dim3(E), dim3(256), 0, s, rewards, values, dones, adv, ret, T, E, gamma, lam);
+    hipLaunchKernelGGL(gae_scan_kernel, dim3(E), dim3(256), 0, s, rewards, values, dones, adv, ret, T, E, gamma, lam,
+                       seg);
   else
     hipLaunchKernelGGL(gae_kernel, dim3((E + 63) / 64), dim3(64), 0, s, rewards, values, dones, adv, ret, T, E,
-                       gamma, lam);
+                       gamma, lam, seg);
   HIP_CHECK_LAUNCH();
 }
 

@@ -17,6 +17,7 @@ from __future__ import annotations
 import argparse
 import dataclasses
 import json
+import warnings
 from dataclasses import dataclass, field, fields
 from typing import Any, Dict, Optional
 
@@ -43,6 +44,7 @@ class Params:
 
     # ---- MI355X-native additions --------------------------------------
     device: str = "cpu"                  # cpu | gpu
+    env_backend: str = "builtin"         # builtin (tensor envs, in-kernel on GPU) | gym (gym.make, host-stepped)
     num_envs: int = 1                    # E vectorised envs per worker
     dtype: str = "fp32"                  # fp32 | bf16x3 | bf16 | fp8  (GEMM operand precision;
                                          # bf16x3 = fp32-accurate split-bf16 on the bf16 MFMA)
@@ -92,10 +94,19 @@ class Params:
     def __post_init__(self):
         if self.update_treshold is None:
             self.update_treshold = self.num_processes - 1
+        elif self.update_treshold != self.num_processes - 1:
+            # chief.py:13 fires when counter > threshold, i.e. with threshold+1 of N workers'
+            # gradients.  The synchronous RCCL all-reduce always combines all N ranks, so a
+            # smaller threshold (straggler tolerance) cannot be honoured: say so, do not no-op.
+            warnings.warn(f"update_treshold={self.update_treshold} is inert: the gradient all-reduce is "
+                          f"synchronous over all num_processes={self.num_processes} ranks (reference "
+                          f"default N-1 = {self.num_processes - 1})", UserWarning, stacklevel=3)
         self.hidden = tuple(int(h) for h in self.hidden)
         self.adam_betas = tuple(float(b) for b in self.adam_betas)
         if self.device not in ("cpu", "gpu"):
             raise ValueError(f"device must be cpu|gpu, got {self.device}")
+        if self.env_backend not in ("builtin", "gym"):
+            raise ValueError(f"env_backend must be builtin|gym, got {self.env_backend}")
         if self.dtype not in ("fp32", "bf16x3", "bf16", "fp8"):
             raise ValueError(f"dtype must be fp32|bf16x3|bf16|fp8, got {self.dtype}")
         if self.loss not in ("ppo", "dppo_ref"):
@@ -132,6 +143,12 @@ class Params:
     @property
     def buffer_rows(self) -> int:
         return self.rollout_len * self.num_envs
+
+    def gae_segment(self) -> int:
+        """the reference's segment length num_steps (train.py:82, ppo.py:87) when it cuts the
+        T-step rollout (0 otherwise): GAE restarts after every num_steps steps, bootstrapping
+        the not-done state (ops/oracle.gae, csrc/optim.hip gae kernels)"""
+        return self.num_steps if 0 < self.num_steps < self.rollout_len else 0
 
     def minibatch_rows(self) -> int:
         return max(1, min(self.batch_size, self.buffer_rows))

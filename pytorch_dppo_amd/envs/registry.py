@@ -7,8 +7,9 @@ env name resolves to
 * ``pendulum`` — a faithful vectorised Pendulum-v0 (gym's dynamics; CPU torch + HIP), or
 * ``synthetic`` — an obs/act-dim-faithful synthetic locomotion task (CPU torch + HIP),
   used for every MuJoCo/Bullet name, or
-* ``gym`` — the real env through :mod:`pytorch_dppo_amd.envs.gym_adapter` when ``gym`` is
-  importable and ``--env-backend gym`` is asked for.
+* ``gym`` — the real env through :mod:`pytorch_dppo_amd.envs.gym_adapter` with
+  ``--env-backend gym`` (``gym.make``, or a factory installed with ``register_env``); its dims
+  come from the env's spaces (:func:`host_spec`).
 
 Dims are gym facts (SURVEY.md §2.6 [ext]).
 """
@@ -18,6 +19,7 @@ from dataclasses import dataclass
 
 KIND_SYNTHETIC = 0
 KIND_PENDULUM = 1
+KIND_HOST = 2          # a host-stepped env (gym backend): dims come from the env itself
 
 
 @dataclass(frozen=True)
@@ -49,6 +51,11 @@ _reg(["Humanoid-v1", "Humanoid-v2"], 376, 17, KIND_SYNTHETIC, 1000)
 _reg(["HalfCheetahBulletEnv-v0"], 26, 6, KIND_SYNTHETIC, 1000)
 _reg(["HopperBulletEnv-v0"], 15, 3, KIND_SYNTHETIC, 1000)
 _reg(["AntBulletEnv-v0"], 28, 8, KIND_SYNTHETIC, 1000)
+
+
+def host_spec(name: str, obs_dim: int, act_dim: int, limit: int) -> EnvSpec:
+    """spec of a host-stepped env (``--env-backend gym``) built from the env's own spaces"""
+    return EnvSpec(name, int(obs_dim), int(act_dim), KIND_HOST, int(limit))
 
 
 def get_spec(name: str) -> EnvSpec:

@@ -184,7 +184,15 @@ class PendulumEnv(VecEnv):
 
 
 def make_vec_env(spec: EnvSpec, num_envs: int, seed: int = 1, rank: int = 0, device="cpu",
-                 max_episode_length: int = 10000) -> VecEnv:
+                 max_episode_length: int = 10000, backend: str = "builtin", name: str = ""):
+    """``builtin``: the tensor envs above (stepped in-kernel on the GPU engine); ``gym``: real
+    gym envs stepped on the host (envs/gym_adapter.py, ``gym.make`` as main.py:45; ``name`` or
+    ``spec.name``)."""
+    if backend == "gym":
+        from .gym_adapter import GymVecEnv
+        return GymVecEnv(name or spec.name, num_envs, seed=seed, rank=rank, max_episode_length=max_episode_length)
+    if backend != "builtin":
+        raise ValueError(f"env backend must be builtin|gym, got {backend!r}")
     cls = PendulumEnv if spec.kind == KIND_PENDULUM else SyntheticEnv
     return cls(spec, num_envs, seed=seed, rank=rank, device=device,
                max_episode_length=max_episode_length)

@@ -38,11 +38,14 @@ def normal_pdf_var(x: torch.Tensor, mu: torch.Tensor, var: torch.Tensor) -> torc
 
 
 def gae(rewards: torch.Tensor, values: torch.Tensor, dones: torch.Tensor, gamma: float,
-        lam: float) -> Tuple[torch.Tensor, torch.Tensor]:
+        lam: float, segment: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """GAE(lambda) over a [T,E] rollout (train.py:109-122, ppo.py:119-133, vectorised).
 
     ``values`` is [T+1,E] (row T = bootstrap V(s_T)); ``dones[t]`` = episode ended at step t
     (so V_{t+1} and A_{t+1} are masked, which is the reference's segment break + R=0).
+    ``segment`` > 0 (the reference's ``num_steps``, train.py:82 / ppo.py:87): a segment also
+    ends after every ``segment`` steps — there the recursion restarts (A_{t+1} masked) while
+    the bootstrap V_{t+1} of the not-done state is kept (train.py:109-112 per segment).
     Returns (advantages [T,E], returns [T,E]) with returns = A + V.
     """
     T = rewards.shape[0]
@@ -51,7 +54,8 @@ def gae(rewards: torch.Tensor, values: torch.Tensor, dones: torch.Tensor, gamma:
     for t in range(T - 1, -1, -1):
         nonterm = 1.0 - dones[t].to(rewards.dtype)
         delta = rewards[t] + gamma * values[t + 1] * nonterm - values[t]
-        nxt = delta + gamma * lam * nonterm * nxt
+        cont = 0.0 if (segment > 0 and (t + 1) % segment == 0) else 1.0
+        nxt = delta + gamma * lam * nonterm * cont * nxt
         adv[t] = nxt
     return adv, adv + values[:T]
 

@@ -197,6 +197,7 @@ class HipEngine:
         self.loss_sums = torch.zeros(NPART_FIXED, **f32)
         self.metrics_buf = torch.zeros(2 + NPART_FIXED + 1, dtype=torch.float64, **dev)
         self.empty_x = torch.empty(0, dtype=self.sdtype, **dev)
+        self.x_raw: Optional[torch.Tensor] = None   # compat Q8: raw bootstrap rows (values())
         # the rollout can emit the full-batch x^T operand when the update is one full-batch step
         self.xT_from_rollout = (self.mb == self.N and self.ldT == self.N and E % 16 == 0 and self.N % 32 == 0
                                 and params.obs_norm_update == "rollout")
@@ -208,7 +209,11 @@ class HipEngine:
         self._graph_warm: set = set()
         self._capture_stream = torch.cuda.Stream(device=device) if self.use_graphs else None
         stats.device_merge = self._device_merge
-        env.reset()
+        # host-stepped env (--env-backend gym): no in-kernel dynamics; rollout() takes the host
+        # path (_rollout_host) and the update runs on the HIP kernels as usual
+        self.host_env = bool(getattr(env, "host_stepped", False))
+        obs0 = env.reset()
+        self._host_obs = obs0.to(device) if self.host_env else None
         self.params_changed()
 
     # ------------------------------------------------------------------------------------------
@@ -379,7 +384,7 @@ class HipEngine:
         return storage.encode(x, self.dt)
 
     def current_obs(self) -> torch.Tensor:
-        return self.env.observe()
+        return self._host_obs if self.host_env else self.env.observe()
 
     def _device_merge(self, s1, s2, count, n_a, shift) -> None:
         """RunningObsStats merge on the device (csrc/obs.hip): one launch instead of ~15 ops."""
@@ -412,11 +417,72 @@ class HipEngine:
                          float(self.p.reward_clip), self.qscale, xt, self.x_rows[0])
 
     @torch.no_grad()
+    def _rollout_host(self) -> Dict:
+        """T steps of a host-stepped env (gym backend, train.py:82-106 vectorised): the env runs
+        on the host, so the fused rollout kernel (which steps the builtin dynamics in-kernel)
+        cannot; per step the E observations are normalised and the policy head evaluated as
+        device tensor ops (E rows; the env's host loop is the bottleneck here), the action noise
+        and log-prob use the same keyed RNG as the kernel, and the buffer rows are written in
+        the storage precision.  The rollout-time x^T operand is not emitted (the update kernel
+        transposes X itself)."""
+        from ..ops import oracle
+        p, T, E, O = self.p, self.T, self.E, self.O
+        shift = self.stats.shift().clone()
+        s1 = torch.zeros(O, dtype=torch.float64, device=self.device)
+        s2 = torch.zeros_like(s1)
+        ep = torch.zeros(2, dtype=torch.float64, device=self.device)
+        norm = self.stats
+        if p.obs_norm_update == "step":
+            self.local_stats = RunningObsStats(O, self.device)
+            self.local_stats.copy_from(self.stats)
+            norm = self.local_stats
+        log_std = self.model.view("log_std")
+        log_sigma = log_std if p.std_convention == "std" else 0.5 * log_std
+        sigma = torch.exp(log_sigma)
+        eidx = torch.arange(E, device=self.device, dtype=torch.int64)
+        dims = torch.arange(self.A, device=self.device, dtype=torch.int64)
+        X = torch.zeros(T + 1, E, self.d0, device=self.device)
+        X[..., O] = 1.0
+        obs = self._host_obs
+        for t in range(T):
+            _, a1, a2 = RunningObsStats.moments(obs, shift)
+            s1 += a1
+            s2 += a2
+            if p.obs_norm_update == "step":
+                norm.observes(obs)
+            x = norm.normalize(obs)
+            mu, _, _ = self.model(x)
+            eps = rng.gauss(self.key_action, eidx[:, None], self.env.t, dims[None, :])
+            a = mu + sigma * eps
+            logp = (-0.5 * eps * eps - 0.5 * oracle.LOG_2PI - log_sigma).sum(-1)
+            nobs, r, done, info = self.env.step(a)
+            r = r.to(self.device)
+            if p.reward_clip > 0:
+                r = r.clamp(-p.reward_clip, p.reward_clip)
+            X[t, :, :O] = x
+            rows = slice(t * E, (t + 1) * E)
+            self.actions[rows] = a
+            self.logp[rows] = logp
+            self.rewards[rows] = r
+            self.dones[rows] = done.to(self.device, torch.float32)
+            ep[0] += float(info["ep_return_sum"])
+            ep[1] += float(info["ep_count"])
+            obs = nobs.to(self.device, torch.float32)
+        X[T, :, :O] = norm.normalize(obs)
+        self._host_obs = obs
+        self.x_buf.copy_(self.encode(X.view(-1, self.d0)))
+        self._xT_valid = False
+        return {"count": float(self.N), "s1": s1, "s2": s2, "shift": shift,
+                "ep_return_sum": ep[0], "ep_count": ep[1], "ep2": ep}
+
+    @torch.no_grad()
     def rollout(self, stats_stream: Optional[torch.cuda.Stream] = None) -> Dict:
         """T env steps for every env.  ``stats_stream`` (rollout-mode obs stats only): the
         one-launch moment/episode-stat reduce runs there, ordered after the rollout kernel, so
         it (and the caller's merge, issued on the same stream) overlaps the value forward and
         the update; the caller orders its stream after that work before reading the stats."""
+        if self.host_env:
+            return self._rollout_host()
         p = self.p
         self.refresh_fwd_image()   # fp8: weights changed during the previous update
         if p.obs_norm_update == "rollout":
@@ -462,12 +528,27 @@ class HipEngine:
         M = (self.T + 1) * self.E
         self.ext.mlp_value(self.dt_fwd, self.x_buf, self.empty, 0, M, self.wimg_fwd, self.layout, self.scales,
                            self.model.flat.data, self.A, self.values_buf, False, self.qscale)
+        if self.p.compat:
+            # Q8 (train.py:109-112, ppo.py:119-122): the reference bootstraps R = V(s_T) from the
+            # RAW, un-normalised last state.  Rows [T*E, (T+1)*E) of values_buf get V of the env's
+            # current raw observation (the rollout left the env after its last step).
+            raw = self.env.observe().to(self.device, torch.float32)
+            xr = torch.zeros(self.E, self.d0, device=self.device)
+            xr[:, :self.O] = raw
+            xr[:, self.O] = 1.0
+            if self.x_raw is None:
+                self.x_raw = torch.empty(self.E, self.d0, dtype=self.sdtype, device=self.device)
+            self.x_raw.copy_(self.encode(xr))
+            self.ext.mlp_value(self.dt_fwd, self.x_raw, self.empty, 0, self.E, self.wimg_fwd, self.layout,
+                               self.scales, self.model.flat.data, self.A, self.values_buf[self.N:], False,
+                               self.qscale)
 
     @torch.no_grad()
     def gae(self) -> None:
         T, E = self.T, self.E
         self.ext.gae(self.rewards.view(T, E), self.values_buf.view(T + 1, E), self.dones.view(T, E),
-                     self.adv.view(T, E), self.ret.view(T, E), float(self.p.gamma), float(self.p.gae_param), 0)
+                     self.adv.view(T, E), self.ret.view(T, E), float(self.p.gamma), float(self.p.gae_param), 0,
+                     self.p.gae_segment())
         if self.p.normalize_adv:
             m, s = self.adv.mean(), self.adv.std()
             self.adv.sub_(m).div_(s + 1e-8)

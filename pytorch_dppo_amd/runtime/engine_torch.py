@@ -117,7 +117,8 @@ class TorchEngine:
 
     @torch.no_grad()
     def gae(self) -> None:
-        adv, ret = oracle.gae(self.rewards, self.values_buf, self.dones, self.p.gamma, self.p.gae_param)
+        adv, ret = oracle.gae(self.rewards, self.values_buf, self.dones, self.p.gamma, self.p.gae_param,
+                              segment=self.p.gae_segment())
         if self.p.normalize_adv:
             adv = (adv - adv.mean()) / (adv.std() + 1e-8)
         self.adv.copy_(adv)

@@ -18,7 +18,7 @@ from typing import Dict, Optional
 
 import torch
 
-from ..envs import get_spec, make_vec_env
+from ..envs import get_spec, host_spec, make_vec_env
 from ..models.actor_critic import ActorCritic
 from ..utils import rng
 from ..utils.obs_stats import RunningObsStats
@@ -51,11 +51,16 @@ def evaluator_main(params_dict: Dict, q, stop_event=None, out_q=None) -> None:
     from ..config import Params
     p = Params.from_dict(params_dict)
     torch.set_num_threads(1)
-    spec = get_spec(p.env_name)
+    if p.env_backend == "gym":   # test.py:28 gym.make
+        env = make_vec_env(None, 1, seed=p.seed + 7777, rank=0, max_episode_length=p.max_episode_length,
+                           backend="gym", name=p.env_name)
+        spec = host_spec(p.env_name, env.O, env.A, env.limit)
+    else:
+        spec = get_spec(p.env_name)
+        env = make_vec_env(spec, 1, seed=p.seed + 7777, rank=0, device="cpu",
+                           max_episode_length=p.max_episode_length)
     model = ActorCritic(spec.obs_dim, spec.act_dim, p.hidden, p.value_mult)
     stats = RunningObsStats(spec.obs_dim)
-    env = make_vec_env(spec, 1, seed=p.seed + 7777, rank=0, device="cpu",
-                       max_episode_length=p.max_episode_length)
     key = rng.base_key(p.seed, rng.STREAM_EVAL, 0)
     start = time.time()
     while True:

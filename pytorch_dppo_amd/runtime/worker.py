@@ -24,7 +24,7 @@ from typing import Dict, Optional
 import torch
 
 from ..config import Params
-from ..envs import get_spec, make_vec_env
+from ..envs import get_spec, host_spec, make_vec_env
 from ..models.actor_critic import ActorCritic
 from ..parallel.dist import DistContext
 from ..utils import rng
@@ -45,14 +45,22 @@ class DPPOWorker:
         self.p = params
         self.ctx = ctx
         self.device = ctx.device
-        self.spec = get_spec(params.env_name)
+        if params.env_backend == "gym":
+            # real gym envs (main.py:45 / train.py:48): dims from the env's own spaces
+            self.env = make_vec_env(None, params.num_envs, seed=params.seed, rank=ctx.rank,
+                                    max_episode_length=params.max_episode_length, backend="gym",
+                                    name=params.env_name)
+            self.spec = host_spec(params.env_name, self.env.O, self.env.A, self.env.limit)
+        else:
+            self.spec = get_spec(params.env_name)
         torch.manual_seed(params.seed)          # main.py:44 — identical init on every rank
         self.model = ActorCritic(self.spec.obs_dim, self.spec.act_dim, params.hidden,
                                  params.value_mult).to(self.device)
         self.ctx.broadcast_(self.model.flat.data, src=0)   # R3 once at start
         action_rank = 0 if params.compat else ctx.rank     # Q6: reference workers share the seed
-        self.env = make_vec_env(self.spec, params.num_envs, seed=params.seed, rank=ctx.rank,
-                                device=self.device, max_episode_length=params.max_episode_length)
+        if params.env_backend != "gym":
+            self.env = make_vec_env(self.spec, params.num_envs, seed=params.seed, rank=ctx.rank,
+                                    device=self.device, max_episode_length=params.max_episode_length)
         self.stats = RunningObsStats(self.spec.obs_dim, self.device)
         self.engine = build_engine(params, self.model, self.env, self.stats, self.device, action_rank)
         # bucketed gradient all-reduce (GPU, multi-rank): the value-side 83 % of the gradient is

@@ -163,9 +163,9 @@ def test_obs_reduce_and_merge_kernels_match_torch_welford(O, nblk, alias):
     assert torch.allclose(dev_st.inv_std_f32, ref.inv_std_f32, rtol=1e-4)
 
 
-@pytest.mark.parametrize("T,E,mode", [(33, 1031, 0), (33, 1031, 1), (2048, 1, 0), (2048, 3, 2), (1000, 5, 2),
-                                      (7, 2, 2)])
-def test_gae_kernel_matches_oracle(T, E, mode):
+@pytest.mark.parametrize("T,E,mode,seg", [(33, 1031, 0, 0), (33, 1031, 1, 0), (2048, 1, 0, 0), (2048, 3, 2, 0),
+                                          (1000, 5, 2, 0), (7, 2, 2, 0), (33, 1031, 1, 5), (1000, 5, 2, 64)])
+def test_gae_kernel_matches_oracle(T, E, mode, seg):
     """mode 1 = per-env lanes, 2 = parallel-in-time scan (auto picks it for 2048 x 1), ragged chunks included."""
     ext = _ext()
     g = torch.Generator(device="cpu").manual_seed(T * 7 + E)
@@ -174,8 +174,8 @@ def test_gae_kernel_matches_oracle(T, E, mode):
     d = (torch.rand(T, E, generator=g) < 0.05).float().to(DEV)
     adv = torch.empty(T, E, device=DEV)
     ret = torch.empty(T, E, device=DEV)
-    ext.gae(r, v, d, adv, ret, 0.99, 0.95, mode)
-    a_ref, r_ref = oracle.gae(r.double(), v.double(), d.double(), 0.99, 0.95)
+    ext.gae(r, v, d, adv, ret, 0.99, 0.95, mode, seg)
+    a_ref, r_ref = oracle.gae(r.double(), v.double(), d.double(), 0.99, 0.95, segment=seg)
     assert torch.allclose(adv.double(), a_ref, atol=2e-5, rtol=2e-5)
     assert torch.allclose(ret.double(), r_ref, atol=2e-5, rtol=2e-5)
 
@@ -726,3 +726,22 @@ def test_learning_reduced_precision_tracks_fp32_accurate():
     gain = late["bf16x3"] - early["bf16x3"]
     for k in ("bf16", "fp8"):
         assert abs(late[k] - late["bf16x3"]) <= 0.2 * gain + 0.002, (k, late)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3"])
+def test_compat_bootstrap_uses_raw_state_on_gpu(dtype):
+    """--compat Q8 on the HIP engine: the bootstrap row of values_buf is
+    V(raw s_T) (train.py:109-112), the other rows V(normalised s_t); matches the torch engine."""
+    p = dppo_preset(device="gpu", env_name="HalfCheetah-v2", num_envs=48, exploration_size=48 * 4,
+                    batch_size=48 * 4, dtype=dtype, compat=True)
+    eng, model, env, stats = _engine(p)
+    stats.observes(env.observe())
+    eng.rollout()
+    eng.values()
+    raw = env.observe()
+    with torch.no_grad():
+        _, _, v_raw = model(raw)
+        _, _, v_norm = model(eng.decode(eng.x_buf)[eng.N:, :model.num_inputs])
+    vb = eng.values_buf[eng.N:]
+    assert torch.allclose(vb, v_raw.reshape(-1), atol=5e-5, rtol=5e-5)
+    assert not torch.allclose(vb, v_norm.reshape(-1), atol=1e-3)

@@ -44,6 +44,44 @@ def test_gae_matches_reference_loop_with_segment_breaks():
                 start = end
 
 
+@pytest.mark.parametrize("seg", [5, 8, 13])
+def test_gae_segment_length_matches_reference_num_steps_segments(seg):
+    """num_steps (train.py:82 / ppo.py:87): a segment ends at done OR after num_steps steps; a
+    not-done segment end bootstraps R = V(s_end) (train.py:109-112) and the GAE loop restarts."""
+    g = torch.Generator().manual_seed(seg)
+    T, E = 40, 3
+    r = torch.randn(T, E, generator=g, dtype=torch.float64)
+    v = torch.randn(T + 1, E, generator=g, dtype=torch.float64)
+    d = torch.zeros(T, E, dtype=torch.float64)
+    d[7, 0] = d[22, 0] = d[39, 1] = d[0, 2] = d[11, 2] = 1.0
+    adv, ret = oracle.gae(r, v, d, 0.99, 0.95, segment=seg)
+    for e in range(E):
+        start = 0
+        for t in range(T):
+            if d[t, e] > 0 or t == T - 1 or (t + 1) % seg == 0:
+                end = t + 1
+                boot = 0.0 if d[t, e] > 0 else float(v[end, e])
+                a_ref, r_ref = _gae_reference_loop(r[start:end, e].tolist(), v[start:end, e].tolist() + [boot],
+                                                   0.99, 0.95)
+                assert torch.allclose(adv[start:end, e], torch.tensor(a_ref, dtype=torch.float64))
+                assert torch.allclose(ret[start:end, e], torch.tensor(r_ref, dtype=torch.float64))
+                start = end
+
+
+def test_inert_reference_knobs_warn():
+    """update_treshold != N-1 cannot be honoured by synchronous collectives: it warns instead of
+    being a silent no-op."""
+    from pytorch_dppo_amd.config import dppo_preset
+    with pytest.warns(UserWarning, match="update_treshold"):
+        dppo_preset(num_processes=4, update_treshold=1)
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        p = dppo_preset(num_processes=4)
+        assert p.update_treshold == 3 and p.gae_segment() == 0
+    assert dppo_preset(num_envs=4, exploration_size=400, num_steps=30).gae_segment() == 30
+
+
 @pytest.mark.parametrize("conv", ["std", "var"])
 def test_gaussian_logp_and_entropy_match_torch_distributions(conv):
     g = torch.Generator().manual_seed(1)
