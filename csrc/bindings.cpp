@@ -519,6 +519,11 @@ void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
   after_launch(__func__);
 }
 
+void debug_invalid_launch() {
+  launch_debug_invalid(nullptr, cur_stream());
+  after_launch(__func__);
+}
+
 void pack(torch::Tensor p, torch::Tensor wimg, torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul) {
   const int64_t n = p.numel();
   check(p, "p", at::kFloat, n);
@@ -565,6 +570,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam", &adam);
   m.def("gather_adam", &gather_adam);
   m.def("pack", &pack);
+  m.def("debug_invalid_launch", &debug_invalid_launch);
   m.def("metrics_pack", &metrics_pack);
   m.attr("arch") = "gfx950";
 }

@@ -116,6 +116,7 @@ extern "C" {
 // first launch / attribute error recorded since the last call (0 = none), message into msg;
 // resets the record (csrc/common.h dppo_note_error)
 int dppo_take_error(char* msg, int cap);
+void launch_debug_invalid(double* out, hipStream_t s);   // test hook: a launch the runtime refuses
 void launch_rollout(int dt, const RolloutArgs& a, int rows, hipStream_t s);
 void set_rollout_waves(int nw);                 // 4 or 8 waves per rollout workgroup (A/B)
 void launch_mlp_value(int dt, const MlpArgs& a, hipStream_t s);

@@ -374,6 +374,16 @@ extern "C" int dppo_take_error(char* msg, int cap) {
   return code;
 }
 
+// test hook (tests/test_gpu_kernels.py): a launch the runtime refuses (2048-thread workgroup,
+// the limit is 1024) — nothing reaches the GPU; exercises the launch-error channel end to end
+__global__ void noop_kernel() {}
+
+extern "C" void launch_debug_invalid(double* out, hipStream_t s) {
+  (void)out;
+  hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(2048), 0, s);   // empty body: nothing to fault
+  HIP_CHECK_LAUNCH();
+}
+
 extern "C" void launch_metrics_pack(const double* ep, const float* loss8, const float* norm_part, int nblk,
                                     double* out, hipStream_t s) {
   hipLaunchKernelGGL(metrics_pack_kernel, dim3(1), dim3(256), 0, s, ep, loss8, norm_part, nblk, out);

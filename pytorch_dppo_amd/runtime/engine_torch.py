@@ -72,7 +72,7 @@ class TorchEngine:
             norm_stats = self.local_stats
         ep_ret_sum = torch.zeros((), dtype=torch.float64, device=self.device)
         ep_count = torch.zeros((), dtype=torch.float64, device=self.device)
-        eidx = self.env.env_idx
+        eidx = self.env.env_idx.to(self.device)
         dims = torch.arange(self.A, device=self.device, dtype=torch.int64)
         log_std = self.model.view("log_std")
         log_sigma = log_std if p.std_convention == "std" else 0.5 * log_std

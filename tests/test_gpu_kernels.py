@@ -745,3 +745,40 @@ def test_compat_bootstrap_uses_raw_state_on_gpu(dtype):
     vb = eng.values_buf[eng.N:]
     assert torch.allclose(vb, v_raw.reshape(-1), atol=5e-5, rtol=5e-5)
     assert not torch.allclose(vb, v_norm.reshape(-1), atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", ["bf16x3", "fp8"])
+def test_gpu_resume_continues_bit_identically(dtype, tmp_path):
+    """SURVEY §5.4 on the HIP engine: 3 iterations straight == 2 iterations,
+    checkpoint, resume (load + broadcast + params_changed), 1 more — parameters, Adam moments,
+    Adam step and the packed weight images (fp8: the e4m3 forward image and its scales) agree
+    bit for bit."""
+    from pytorch_dppo_amd.parallel.dist import DistContext
+    from pytorch_dppo_amd.runtime.launcher import run_worker
+    base = dict(device="gpu", env_name="Humanoid-v2", num_processes=1, num_envs=64, exploration_size=64 * 4,
+                batch_size=64 * 4, num_epoch=2, dtype=dtype, seed=4)
+    ctx = DistContext(device=DEV)
+    w_full, _ = run_worker(dppo_preset(max_iters=3, **base), ctx, evaluator=False, quiet=True)
+    ck = str(tmp_path / "ck")
+    run_worker(dppo_preset(max_iters=2, checkpoint_dir=ck, **base), ctx, evaluator=False, quiet=True)
+    w_res, _ = run_worker(dppo_preset(max_iters=3, resume=ck, **base), ctx, evaluator=False, quiet=True)
+    torch.cuda.synchronize()
+    assert w_res.iteration == 3 and w_res.engine.adam_step == w_full.engine.adam_step
+    a, b = w_full.engine, w_res.engine
+    assert torch.equal(w_full.model.flat.data, w_res.model.flat.data)
+    assert torch.equal(a.adam_m, b.adam_m) and torch.equal(a.adam_v, b.adam_v)
+    assert torch.equal(a.wimg, b.wimg) and torch.equal(a.wimg_fwd, b.wimg_fwd) and torch.equal(a.qscale, b.qscale)
+    assert torch.equal(w_full.stats.mean, w_res.stats.mean)
+
+
+def test_launch_error_raises_instead_of_stale_result():
+    """A refused launch raises a Python exception naming the op (launch errors
+    were only printed).  debug_invalid_launch asks the runtime for a 2048-thread workgroup (the
+    limit is 1024): the runtime refuses it before anything reaches the GPU, the launcher records
+    the error, and the binding raises; the channel is clean again afterwards."""
+    ext = _ext()
+    with pytest.raises(RuntimeError, match="debug_invalid_launch: HIP launch failed"):
+        ext.debug_invalid_launch()
+    g = torch.zeros(4, 4, device=DEV)
+    ext.gae(g, torch.zeros(5, 4, device=DEV), g, torch.empty_like(g), torch.empty_like(g), 0.99, 0.95, 0, 0)
+    torch.cuda.synchronize()
