@@ -327,6 +327,14 @@ int64_t train_rows(int64_t dt, std::vector<int64_t> layout, int64_t A) {
   return mlp_train_rows((int)dt, a);
 }
 
+int64_t train_waves(int64_t dt, std::vector<int64_t> layout, int64_t A) {
+  const Layout L = parse_layout(layout);
+  MlpArgs a{};
+  for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
+  a.A = (int)A;
+  return mlp_train_waves((int)dt, a);
+}
+
 void set_mlp_rows(int64_t rows) {
   TORCH_CHECK(rows == 0 || rows == 16 || rows == 32 || rows == 64, "rows: 0 (auto), 16, 32 or 64");
   set_mlp_rows_override((int)rows);
@@ -546,7 +554,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_train", &mlp_train);
   m.def("train_lds_bytes", &train_lds_bytes);
   m.def("train_rows", &train_rows);
+  m.def("train_waves", &train_waves);
   m.def("set_mlp_rows", &set_mlp_rows);
+  m.def("set_s3_value_waves", [](int64_t nw) {
+    TORCH_CHECK(nw == 4 || nw == 8, "split-bf16 value waves: 4 or 8");
+    set_s3_value_waves((int)nw);
+  });
   m.def("set_s3_train_waves", [](int64_t nw) {
     TORCH_CHECK(nw == 4 || nw == 8, "split-bf16 train waves: 4 or 8");
     set_s3_train_waves((int)nw);

@@ -125,6 +125,7 @@ size_t mlp_train_lds_bytes(int dt, const MlpArgs& a);
 int mlp_train_rows(int dt, const MlpArgs& a);   // row tile the launcher will use (LDS-fit)
 void set_mlp_rows_override(int rows);           // 0 auto; 16/32/64 force (A/B diagnostics)
 void set_s3_train_waves(int nw);                // split-bf16 32-row tile: 4 or 8 waves (A/B)
+void set_s3_value_waves(int nw);                // split-bf16 value forward: 4 or 8 waves (A/B)
 int mlp_train_waves(int dt, const MlpArgs& a);  // workgroup waves the launcher will use
 void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
 void set_wgrad_stages(int st);                 // bf16 wgrad DMA ring depth 3 / 4 / 6 (A/B)

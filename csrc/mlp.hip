@@ -257,7 +257,10 @@ __global__ __launch_bounds__(NW * 64, (TrainOcc<DT, NW>::V)) void mlp_train_kern
   // dgrad-fc2 and the value head's fc2.  Off: the phase timeline (scripts/phase_timeline.py)
   // showed the layers are latency-, not balance-bound, and fc1 lost more to the doubled weight
   // traffic of 32-row items than the barriers gained (18.4M vs 19.1M env steps/s).
-  constexpr bool SPLIT = false;   // measured: splitting costs fc1 more B traffic than it saves
+  // split-bf16 at 8 waves (32 rows): fc1 = 4 policy + 16 value tile pairs on 8 waves (3 vs 2 per
+  // wave whole); as policy half-pair items every wave takes 2 value pairs + 1 policy half
+  // (phase timeline: fc1 barrier wait 7.3 k -> 4.1 k cycles per tile)
+  constexpr bool SPLIT = IsSplit<DT>::value && NW == 8;
   constexpr int HR = SPLIT ? ROWS / 2 : ROWS;     // rows of one split item
   constexpr int SNW = SPLIT ? 4 : NW;             // "waves" of a split call
   const int sw = SPLIT ? (wave & 3) : wave;       // wave index inside a split call
@@ -601,10 +604,17 @@ void train_t(const MlpArgs& a, hipStream_t s) {
   }
 }
 
+int g_s3_value_waves = 8;   // split-bf16 value forward: 4 or 8 waves per 32-row workgroup (A/B)
+
 template <int DT>
 void value_t(const MlpArgs& a, hipStream_t s) {
   if constexpr (DT == DT_F32) {
     value_launch<DT, 32, 4>(a, s);
+  } else if constexpr (DT == DT_S3) {
+    // like the update: the 32-row tile takes most of LDS (one workgroup per CU), so a second
+    // wave per SIMD is the latency hiding (scripts/ab_train.py: 162 vs 217 us per call)
+    if (g_s3_value_waves == 8) value_launch<DT, 32, 8>(a, s);
+    else value_launch<DT, 32, 4>(a, s);
   } else {
     if (value_rows_t<DT>(a) == 64) value_launch<DT, 64, 8>(a, s);
     else value_launch<DT, 32, 4>(a, s);
@@ -649,6 +659,7 @@ extern "C" int mlp_train_rows(int dt, const MlpArgs& a) {
 
 extern "C" void set_mlp_rows_override(int rows) { g_rows_override = rows; }
 extern "C" void set_s3_train_waves(int nw) { g_s3_train_waves = nw == 8 ? 8 : 4; }
+extern "C" void set_s3_value_waves(int nw) { g_s3_value_waves = nw == 8 ? 8 : 4; }
 extern "C" int mlp_train_waves(int dt, const MlpArgs& a) {
   if (dt == DT_F32) return 4;
   if (dt == DT_BF16) return train_waves_t<DT_BF16>(a);

@@ -94,6 +94,14 @@ DEV void store4q_T(typename Prec<DT>::T* dst, const typename Prec<DT>::T (&q)[4]
 
 // (split-bf16 fragments are twice the registers: one k-step per chunk keeps the 8-wave, 2-waves-
 // per-SIMD form inside 256 VGPRs; the second wave per SIMD hides the latency instead)
+// register sets in the layer_gemm rotation (prefetch distance NB - 1 steps).  split-bf16 at 8
+// waves runs one k-step per chunk with VGPRs to spare, so it prefetches deeper: a step is only
+// 12 MFMAs there, far shorter than the L2 latency of the weight fragments it waits for.
+#ifndef DPPO_S3_NBUF
+#define DPPO_S3_NBUF 2
+#endif
+template <int DT, int NW> struct GemmDepth { static constexpr int NB = (IsSplit<DT>::value && NW == 8) ? DPPO_S3_NBUF : 2; };
+
 template <int DT, int RB> struct KChunk { static constexpr int KC = IsSplit<DT>::value ? 1 : 2; };
 
 // B fragments of a wave's FIRST (tile pair, k-chunk) step of one layer_gemm call, loaded ahead
@@ -294,26 +302,74 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) acc[t][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
-  Buf buf0, buf1;
+  // NB register sets in rotation: the loads of step s + NB - 1 are issued while step s
+  // computes (prefetch distance NB - 1 steps).  Past the end, a load re-reads the last step's
+  // (valid) addresses, so every step issues the same loads and the compiler's vmcnt waits stay
+  // exact.  The load cursor (ntl, kcl, sl) runs NB - 1 steps ahead of the compute cursor.
+  constexpr int NB = GemmDepth<DT, NW>::NB;
+  if constexpr (NB == 2) {
+    // the two-set form: prefetch step s+1 into `nx` (unconditionally: past the end it re-loads
+    // valid addresses), compute step s from `cur`, epilogue at the end of a pair
+    Buf buf0, buf1;
+    int nt0 = first_pair, kc = 0;
+    if constexpr (PRE) {
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        buf0.b0[j] = pre->b0[j];
+        buf0.b1[j] = pre->b1[j];
+      }
+      load_a0(buf0);
+    } else {
+      load(buf0, nt0, 0);
+    }
+    auto step = [&](int s, const Buf& cur, Buf& nx) {
+      int nt1 = nt0, kc1 = kc + 1;
+      if (kc1 == nchunks) { kc1 = 0; nt1 = nt0 + NW * NT2; }
+      if (s + 1 >= nsteps) { nt1 = nt0; kc1 = kc; }
+      load(nx, nt1, kc1);
+      compute(cur, kc);
+      if (++kc == nchunks) {
+        epilogue(nt0);
+        kc = 0;
+        nt0 += NW * NT2;
+      }
+    };
+    int s = 0;
+    for (; s + 1 < nsteps; s += 2) {
+      step(s, buf0, buf1);
+      step(s + 1, buf1, buf0);
+    }
+    if (s < nsteps) step(s, buf0, buf1);
+    return;
+  }
+  Buf buf[NB];
   int nt0 = first_pair, kc = 0;
+  int ntl = first_pair, kcl = 0, sl = 0;
+  const int nt_last = first_pair + (npairs - 1) * NW * NT2, kc_last = nchunks - 1;
+  auto load_next = [&](Buf& d) {
+    const bool v = sl < nsteps;
+    load(d, v ? ntl : nt_last, v ? kcl : kc_last);
+    if (++kcl == nchunks) { kcl = 0; ntl += NW * NT2; }
+    ++sl;
+  };
   if constexpr (PRE) {
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
-      buf0.b0[j] = pre->b0[j];
-      buf0.b1[j] = pre->b1[j];
+      buf[0].b0[j] = pre->b0[j];
+      buf[0].b1[j] = pre->b1[j];
     }
-    load_a0(buf0);
+    load_a0(buf[0]);
+    if (++kcl == nchunks) { kcl = 0; ntl += NW * NT2; }
+    ++sl;
   } else {
-    load(buf0, nt0, 0);
+    load_next(buf[0]);
   }
-  // One step: prefetch step s+1 into `nx` (unconditionally: past the end it re-loads valid
-  // addresses, so the number of loads in flight is the same on every path and the compiler's
-  // waitcnt is exact), compute step s from `cur`, epilogue at the end of a pair.
-  auto step = [&](int s, const Buf& cur, Buf& nx) {
-    int nt1 = nt0, kc1 = kc + 1;
-    if (kc1 == nchunks) { kc1 = 0; nt1 = nt0 + NW * NT2; }
-    if (s + 1 >= nsteps) { nt1 = nt0; kc1 = kc; }
-    load(nx, nt1, kc1);
+#pragma unroll
+  for (int j = 1; j < NB - 1; ++j) load_next(buf[j]);
+  // one step: prefetch into the set NB - 1 ahead, compute the current set, epilogue at the end
+  // of a tile pair
+  auto step = [&](const Buf& cur, Buf& nx) {
+    load_next(nx);
     compute(cur, kc);
     if (++kc == nchunks) {
       epilogue(nt0);
@@ -322,11 +378,13 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
     }
   };
   int s = 0;
-  for (; s + 1 < nsteps; s += 2) {
-    step(s, buf0, buf1);
-    step(s + 1, buf1, buf0);
+  for (; s + NB <= nsteps; s += NB) {
+#pragma unroll
+    for (int u = 0; u < NB; ++u) step(buf[u], buf[(u + NB - 1) % NB]);
   }
-  if (s < nsteps) step(s, buf0, buf1);
+#pragma unroll
+  for (int u = 0; u < NB - 1; ++u)
+    if (s + u < nsteps) step(buf[u], buf[(u + NB - 1) % NB]);
 }
 
 __host__ __device__ inline size_t al16(size_t b) { return (b + 15) & ~size_t(15); }

@@ -79,6 +79,12 @@ def main():
         "train": (waves(8), train), "wgrad": (waves(8), wgrad),
         "grad": (waves(8), lambda: eng.grad(None)), "values": (waves(8), eng.values),
         "rollout": (waves(8), eng.rollout),
+        "abl0": (lambda: ext.set_train_ablation(0), train), "abl1": (lambda: ext.set_train_ablation(1), train),
+        "abl2": (lambda: ext.set_train_ablation(2), train), "abl4": (lambda: ext.set_train_ablation(4), train),
+        "abl8": (lambda: ext.set_train_ablation(8), train), "abl16": (lambda: ext.set_train_ablation(16), train),
+        "abl7": (lambda: ext.set_train_ablation(7), train),
+        "val4": (lambda: ext.set_s3_value_waves(4), eng.values),
+        "val8": (lambda: ext.set_s3_value_waves(8), eng.values),
         "roll4": (lambda: ext.set_rollout_waves(4), eng.rollout),
         "roll8": (lambda: ext.set_rollout_waves(8), eng.rollout),
     }
@@ -89,6 +95,7 @@ def main():
             setup()
             res[k].append(timed(fn))
     ext.set_s3_train_waves(8)
+    ext.set_train_ablation(0)
     out = {k: {"median_us": sorted(v)[len(v) // 2], "all_us": [round(x, 1) for x in v]} for k, v in res.items()}
     print(json.dumps({"dtype": dtype, "arms": out}, indent=1))
 

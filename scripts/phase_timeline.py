@@ -46,7 +46,7 @@ def main():
     for rows in [int(r) for r in os.environ.get("TIMELINE_ROWS", "64,32").split(",")]:
         ext.set_mlp_rows(rows)
         eng.sync_tile()
-        nw = 8 if rows == 64 else 4
+        nw = int(ext.train_waves(eng.dt, eng.layout, eng.A))
         nblk = eng.ldT // rows
         buf = torch.zeros(((nblk + EVERY - 1) // EVERY) * nw * 16, dtype=torch.int64, device=dev)
         for _ in range(3):
