@@ -527,6 +527,23 @@ void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
   after_launch(__func__);
 }
 
+void fp8_refresh(torch::Tensor p, torch::Tensor lid, torch::Tensor qscale, torch::Tensor part, torch::Tensor wimg,
+                 torch::Tensor w_map, torch::Tensor wt_map) {
+  check(part, "part", at::kFloat, 128 * 6);
+  const int64_t n = p.numel();
+  check(p, "p", at::kFloat, n);
+  check(lid, "lid", at::kInt, n);
+  check(qscale, "qscale", at::kFloat, 6);
+  check(w_map, "w_map", at::kInt, n);
+  check(wt_map, "wt_map", at::kInt, n);
+  check(wimg, "wimg", at::kByte, 1);
+  // lid must name a layer in [0, 6) for every parameter with an image entry (the kernel's scale
+  // index): HipEngine validates the static map once at construction (no per-call device sync)
+  launch_fp8_refresh(p.data_ptr<float>(), lid.data_ptr<int>(), (int)n, qscale.data_ptr<float>(), part.data_ptr<float>(),
+                     wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), cur_stream());
+  after_launch(__func__);
+}
+
 void debug_invalid_launch() {
   launch_debug_invalid(nullptr, cur_stream());
   after_launch(__func__);
@@ -584,6 +601,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gather_adam", &gather_adam);
   m.def("pack", &pack);
   m.def("debug_invalid_launch", &debug_invalid_launch);
+  m.def("fp8_refresh", &fp8_refresh);
   m.def("metrics_pack", &metrics_pack);
   m.attr("arch") = "gfx950";
 }

@@ -150,6 +150,11 @@ void launch_gather_adam(const float* slab, const int* src_off, const int* src_me
                         hipStream_t s);
 void launch_pack(const float* p, int n, void* wimg, const int* w_map, const int* wt_map, int dt,
                  const float* img_scale, hipStream_t s);
+// fp8 forward image: qscale[6] = per-layer amax / 416 of p (lid: layer of each parameter, -1
+// none; must be < 6), then the e4m3 image of p / qscale[lid] (two launches; part: 128 x 6
+// floats of per-block maxima)
+void launch_fp8_refresh(const float* p, const int* lid, int n, float* qscale, float* part, void* wimg,
+                        const int* w_map, const int* wt_map, hipStream_t s);
 void launch_obs_reduce(const float* part, int nblk, int O, double* s12, const float* epstat, double* ep,
                        hipStream_t s);
 void launch_obs_merge(const double* s12, int O, double count, double n_a, const float* shift, double* mean,

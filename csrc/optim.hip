@@ -331,7 +331,74 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ p, 
   }
 }
 
+// fp8 forward image refresh (dtype fp8), step 1: per-block, per-layer amax of the fp32 master
+// weights -> part[block][6] (max is order-independent: no atomics).  Step 2 (pack_fp8_kernel):
+// every block folds the partials into qscale[l] = amax_l / 416 (e4m3's largest finite value is
+// 448: ~7 % headroom) and quantises its elements with it.  Two launches replace ~20 small torch
+// ops per iteration (~200 us host-bound back to back).
+constexpr int FP8_AMAX_BLOCKS = 128;
+
+__global__ __launch_bounds__(256) void fp8_amax_kernel(const float* __restrict__ p, const int* __restrict__ lid,
+                                                        int n, float* __restrict__ part) {
+  float m[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int l = lid[i];
+    const float a = fabsf(p[i]);
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if (l == k) m[k] = fmaxf(m[k], a);
+  }
+  __shared__ float red[4][6];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    float v = m[k];
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    if (lane == 0) red[w][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6)
+    part[blockIdx.x * 6 + threadIdx.x] =
+        fmaxf(fmaxf(red[0][threadIdx.x], red[1][threadIdx.x]), fmaxf(red[2][threadIdx.x], red[3][threadIdx.x]));
+}
+
+// step 2: e4m3 images of every weight with its layer's scale (x / qscale[l]); kernels multiply
+// the accumulator by qscale[l].  IEEE divisions (__fdiv_rn): the tests compare with torch.
+__global__ __launch_bounds__(256) void pack_fp8_kernel(const float* __restrict__ p, int n, uint8_t* __restrict__ wimg,
+                                                        const int* __restrict__ w_map, const int* __restrict__ wt_map,
+                                                        const int* __restrict__ lid, const float* __restrict__ part,
+                                                        int npart, float* __restrict__ qscale) {
+  using P = Prec<DT_FP8>;
+  __shared__ float sc[6];
+  if (threadIdx.x < 6) {
+    float v = 0.f;
+    for (int b = 0; b < npart; ++b) v = fmaxf(v, part[b * 6 + threadIdx.x]);
+    sc[threadIdx.x] = fmaxf(__fdiv_rn(v, 416.f), 1e-12f);
+    if (blockIdx.x == 0) qscale[threadIdx.x] = sc[threadIdx.x];
+  }
+  __syncthreads();
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int wi = w_map[i];
+    if (wi >= 0) {
+      const float q = __fdiv_rn(p[i], sc[lid[i]]);
+      P::put(wimg, wi, q);
+      P::put(wimg, wt_map[i], q);
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" void launch_fp8_refresh(const float* p, const int* lid, int n, float* qscale, float* part, void* wimg,
+                                   const int* w_map, const int* wt_map, hipStream_t s) {
+  hipLaunchKernelGGL(fp8_amax_kernel, dim3(FP8_AMAX_BLOCKS), dim3(256), 0, s, p, lid, n, part);
+  HIP_CHECK_LAUNCH();
+  int grid = (n + 255) / 256;
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(pack_fp8_kernel, dim3(grid), dim3(256), 0, s, p, n, (uint8_t*)wimg, w_map, wt_map, lid, part,
+                     FP8_AMAX_BLOCKS, qscale);
+  HIP_CHECK_LAUNCH();
+}
 
 // Per-iteration metric staging in ONE launch (replaces ~6 small torch ops at the iteration tail):
 // out[0..1] = episode (return sum, count), out[2..9] = the 8 loss-term sums of the last

@@ -69,6 +69,12 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   uint32_t* kes = cv.take<uint32_t>(3 * ROWS);   // per-env key prefixes of this step: action, env, reset
   float* wdrv = cv.take<float>(S);                // synthetic dynamics: drive weight of state dim d
   int* jdx = cv.take<int>(S);                     //                     action index driving dim d
+  // fp8: the MFMA tile is e4m3 but the buffer rows are bf16 — a bf16 staging tile lets them
+  // leave as 16-byte row chunks (element stores strided by the row length were 2.6x the bf16
+  // kernel's time)
+  using XB = typename Prec<XStore<DT>::DTX>::T;
+  constexpr bool STAGE = DT == DT_FP8;
+  XB* xsb = STAGE ? cv.take<XB>(ROWS * a.d1) : nullptr;
 
   const T* W = reinterpret_cast<const T*>(a.W);
   const T* W1 = W + a.off_w1;
@@ -110,7 +116,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   // bf16 / fp32: the LDS tile and the buffer share the element type (fp8 tiles feed a bf16 buffer)
   // (split-bf16: the LDS tile and the buffer share the 32-byte hi|lo group layout too)
   constexpr bool SPLIT = IsSplit<DT>::value;
-  constexpr bool XO_FROM_LDS = (sizeof(T) == sizeof(typename PX::T) && sizeof(T) == 2) || SPLIT;
+  constexpr bool XO_FROM_LDS = std::is_same_v<T, typename PX::T> || SPLIT || STAGE;
   // the observe loop keeps this feature's ROWS values in the buffer type, or as fp32 for split
   // storage (split once, at the 32-byte x^T group store)
   using GT = std::conditional_t<SPLIT, float, typename PX::T>;
@@ -150,8 +156,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
           P::put(xs, r * ld1 + d, xv);
           if constexpr (SPLIT) grp[r] = xv;
           else grp[r] = PX::cvt(xv);
-          if constexpr (!XO_FROM_LDS)
-            if (r < nvalid) xo[((size_t)tb * a.buf_E + e0 + r) * a.d1 + d] = grp[r];
+          if constexpr (STAGE) xsb[r * a.d1 + d] = grp[r];
         }
         if (d < O) { s1[d] += ls1; s2[d] += ls2; }
         // full-batch update operand: rows m = tb*E + e0 + r are contiguous 8-groups of the FM
@@ -192,12 +197,14 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
       // row-major buffer rows from the normalised LDS tile: one 16-byte store per 16 bytes of
       // features instead of ROWS element stores per feature (fire-and-forget, overlaps the MFMA
       // layers)
-      constexpr int EPC = 16 / sizeof(T);
+      constexpr int EPC = 16 / sizeof(XB);
       const int ch = a.d1 / EPC;
       for (int i = tid; i < nvalid * ch; i += NTHR) {
         const int r = i / ch, c = i - r * ch;
+        const void* src = STAGE ? static_cast<const void*>(xsb + r * a.d1 + c * EPC)
+                                : static_cast<const void*>(xs + r * ld1 + c * EPC);
         *reinterpret_cast<uint4*>(xo + ((size_t)tb * a.buf_E + e0 + r) * a.d1 + c * EPC) =
-            *reinterpret_cast<const uint4*>(xs + r * ld1 + c * EPC);
+            *reinterpret_cast<const uint4*>(src);
       }
     }
     if (last) break;
@@ -396,6 +403,7 @@ size_t rollout_lds(const RolloutArgs& a) {
   b += al(sizeof(float) * ROWS) + al(sizeof(int) * ROWS) + al(sizeof(float) * ROWS) + al(sizeof(float) * 2 * ROWS);
   b += al(sizeof(uint32_t) * 3 * ROWS);
   b += al(sizeof(float) * a.S) + al(sizeof(int) * a.S);
+  if (DT == DT_FP8) b += al(sizeof(__bf16) * ROWS * a.d1);   // bf16 staging tile of the buffer rows
   return b;
 }
 

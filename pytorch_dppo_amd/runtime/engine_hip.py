@@ -110,8 +110,10 @@ class HipEngine:
                 for suffix in ("weight", "bias"):
                     o, n_ = model.offsets[f"{l.name}.{suffix}"]
                     lid[o:o + n_] = li
-            self.layer_id = lid.to(device)
-            self.layer_slices = [[model.offsets[f"{l.name}.{s}"] for s in ("weight", "bias")] for l in ls]
+            # the device refresh indexes qscale[lid]: validate the static map once here
+            assert bool(((lid >= 0) == (L.flat_to_w >= 0)).all()) and int(lid.max()) < 6
+            self.layer_id = lid.to(torch.int32).to(device)
+            self.fp8_part = torch.zeros(128 * 6, **f32)   # per-block layer maxima (fp8_amax_kernel)
         else:
             self.wimg_fwd = self.wimg
         self.d0 = ls[0].d_in
@@ -363,18 +365,14 @@ class HipEngine:
 
     @torch.no_grad()
     def refresh_fwd_image(self) -> None:
-        """fp8 only: per-layer amax scales + e4m3 image of the current weights, all on the
-        device (no host sync).  s_l = amax_l / 416 keeps every weight inside e4m3's finite range
-        (448) with headroom; the kernels multiply each layer's accumulator by s_l."""
+        """fp8 only: per-layer amax scales + e4m3 image of the current weights, on the device in
+        two launches (csrc/optim.hip fp8_amax_kernel + pack_fp8_kernel; no host sync).
+        s_l = amax_l / 416 keeps every weight inside e4m3's finite range (448) with headroom;
+        the kernels multiply each layer's accumulator by s_l."""
         if not self.fp8:
             return
-        flat = self.model.flat.data
-        amax = torch.stack([torch.maximum(flat[wo:wo + wn].abs().amax(), flat[bo:bo + bn].abs().amax())
-                            for (wo, wn), (bo, bn) in self.layer_slices])
-        s = torch.clamp(amax / 416.0, min=1e-12)
-        self.qscale.copy_(s)
-        qmul = torch.where(self.layer_id >= 0, (1.0 / s)[self.layer_id.clamp(min=0)], torch.zeros_like(flat))
-        self.ext.pack(flat, self.wimg_fwd, self.w_map, self.wt_map, self.dt_fwd, qmul)
+        self.ext.fp8_refresh(self.model.flat.data, self.layer_id, self.qscale, self.fp8_part, self.wimg_fwd, self.w_map,
+                             self.wt_map)
 
     def decode(self, t: torch.Tensor) -> torch.Tensor:
         """a storage-precision buffer of this engine (x_buf, an operand buffer) as fp32"""

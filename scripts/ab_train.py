@@ -85,6 +85,7 @@ def main():
         "abl7": (lambda: ext.set_train_ablation(7), train),
         "val4": (lambda: ext.set_s3_value_waves(4), eng.values),
         "val8": (lambda: ext.set_s3_value_waves(8), eng.values),
+        "refresh": (lambda: None, eng.refresh_fwd_image),
         "roll4": (lambda: ext.set_rollout_waves(4), eng.rollout),
         "roll8": (lambda: ext.set_rollout_waves(8), eng.rollout),
     }

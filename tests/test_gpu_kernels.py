@@ -782,3 +782,29 @@ def test_launch_error_raises_instead_of_stale_result():
     g = torch.zeros(4, 4, device=DEV)
     ext.gae(g, torch.zeros(5, 4, device=DEV), g, torch.empty_like(g), torch.empty_like(g), 0.99, 0.95, 0, 0)
     torch.cuda.synchronize()
+
+
+def test_fp8_device_refresh_matches_torch_quantisation():
+    """fp8 forward image refresh on the device (fp8_scale + pack_fp8 kernels): per-layer scales ==
+    amax / 416 over each layer's weight and bias, and the e4m3 image == torch's float8_e4m3fn
+    rounding of p / scale (both round to nearest even; no value reaches the 448 saturation)."""
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 4, batch_size=64 * 4,
+                    dtype="fp8")
+    eng, model, _, _ = _engine(p)
+    with torch.no_grad():
+        model.flat.data.mul_(torch.linspace(0.5, 3.0, model.num_params, device=DEV))   # distinct layer amax
+    eng.refresh_fwd_image()
+    L = model.packed_layout()
+    names = [l.name for l in L.layers]
+    amax = torch.stack([torch.maximum(model.view(f"{n}.weight").abs().amax(), model.view(f"{n}.bias").abs().amax())
+                        for n in names])
+    # (torch divides by a python scalar as a multiply by its reciprocal: allow that 1-ulp gap;
+    # the kernel divides exactly, as the tensor-by-tensor division below does)
+    assert torch.allclose(eng.qscale, torch.clamp(amax.detach() / 416.0, min=1e-12), rtol=2e-7, atol=0)
+    lid = eng.layer_id.long()
+    sel = lid >= 0
+    q = (model.flat.data[sel] / eng.qscale[lid[sel]]).to(torch.float8_e4m3fn).view(torch.uint8)
+    w_map = L.flat_to_w.to(DEV).long()[sel]
+    wt_map = L.flat_to_wt.to(DEV).long()[sel]
+    same = (eng.wimg_fwd[w_map] == q).float().mean().item()
+    assert same > 0.9999 and torch.equal(eng.wimg_fwd[w_map], eng.wimg_fwd[wt_map]), same
