@@ -54,6 +54,8 @@ void set_train_tstamp(torch::Tensor buf, int64_t every) {
   g_tstamp = reinterpret_cast<unsigned long long*>(buf.data_ptr<int64_t>());
   g_tstamp_every = (int)every;
 }
+int g_x_stream = 0;     // A/B: non-temporal observation-row loads in the value / update kernels
+void set_x_stream(int64_t on) { g_x_stream = on ? 1 : 0; }
 int g_wgrad_impl = 0;   // 0: LDS-DMA staged, 1: register-streamed (A/B diagnostics)
 void set_wgrad_impl(int64_t impl) {
   TORCH_CHECK(impl == 0 || impl == 1, "wgrad impl: 0 LDS-DMA, 1 register");
@@ -232,6 +234,7 @@ MlpArgs base_mlp(int dt, const Layout& L, const std::vector<double>& scales, tor
   }
   a.A = (int)A;
   a.log_std = flat.data_ptr<float>();
+  a.x_stream = g_x_stream;
   return a;
 }
 
@@ -343,8 +346,8 @@ void set_mlp_rows(int64_t rows) {
 void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor> xT, std::vector<int64_t> g_rows,
            std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab,
            int64_t waves) {
-  TORCH_CHECK(waves == 8 || (waves == 16 && dt == 1 && g_wgrad_impl == 0),
-              "wgrad workgroup waves: 8, or 16 for the bf16 LDS-DMA kernel");
+  TORCH_CHECK(waves == 8 || (waves == 16 && (dt == 1 || dt == 3) && g_wgrad_impl == 0),
+              "wgrad workgroup waves: 8, or 16 for the bf16 / bf16x3 LDS-DMA kernel");
   TORCH_CHECK(dt != 3 || g_wgrad_impl == 0, "split-bf16 wgrad runs on the LDS-DMA kernel only");
   const int wmax = (int)waves, smax = waves == 16 ? 8 : 6;
   TORCH_CHECK(gT.size() == 6 && xT.size() == 6 && g_rows.size() == 6 && x_rows.size() == 6, "6 layers");
@@ -602,6 +605,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pack", &pack);
   m.def("debug_invalid_launch", &debug_invalid_launch);
   m.def("fp8_refresh", &fp8_refresh);
+  m.def("set_x_stream", &set_x_stream);
   m.def("metrics_pack", &metrics_pack);
   m.attr("arch") = "gfx950";
 }

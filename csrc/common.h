@@ -147,6 +147,18 @@ __host__ __device__ inline size_t fm_frag(int rt, int ks, int cols, int lane) {
   return ((size_t)rt * (size_t)(cols >> 5) + (size_t)ks) * 512u + (size_t)lane * 8u;
 }
 
+// Store of a wgrad operand (the feature-major activations / gradients the fused update writes
+// and the wgrad kernel reads back): non-temporal by default (streaming: keeps the weight images
+// in L2); DPPO_T_CACHED: plain stores (A/B of Infinity-Cache residency).
+template <typename V>
+DEV void opnd_store(const V& v, V* p) {
+#ifdef DPPO_T_CACHED
+  *p = v;
+#else
+  __builtin_nontemporal_store(v, p);
+#endif
+}
+
 // storage precision of the normalised-observation buffer written by the rollout and read by
 // the value/update kernels: fp8 forward kernels keep it in bf16 (the update runs in bf16)
 template <int DT> struct XStore { static constexpr int DTX = (DT == DT_FP8) ? DT_BF16 : DT; };

@@ -44,7 +44,7 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 template <int DT, int NT, typename F>
 DEV void load_rows(const typename Prec<DT>::T* xb, const int* idx, int row0, int m0, int nvalid,
                    int d, typename Prec<DT>::T* X, int ldx, int ROWS, int tid, F&& between,
-                   bool skip = false) {
+                   bool skip = false, bool stream = false) {
   constexpr int E16 = 16 / Prec<DT>::BYTES;
   constexpr int B = 8;
   const int chunks = d / E16;
@@ -63,8 +63,12 @@ DEV void load_rows(const typename Prec<DT>::T* xb, const int* idx, int row0, int
         off[j] = r * ldx + c * E16;
         if (r < nvalid && !skip) {
           const int src = idx ? idx[m0 + r] : row0 + m0 + r;
-          // streaming load: each observation row is read once per kernel, keep L2 for weights
-          const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xb + (size_t)src * d + c * E16));
+          // plain (cached) load: the observation buffer (100 MB at split-bf16) is re-read by every
+          // epoch and stays in the 256 MB Infinity Cache between them; measured at the bench
+          // geometry, split-bf16 update 299 -> 269 us (the X gather fell from ~38 to ~5 us) and the
+          // value forward 162 -> 147 us vs non-temporal loads; bf16 neutral (134-138 us)
+          const u32x4* sp = reinterpret_cast<const u32x4*>(xb + (size_t)src * d + c * E16);
+          const u32x4 t = stream ? __builtin_nontemporal_load(sp) : *sp;
           v[j] = make_uint4(t.x, t.y, t.z, t.w);
         }
       }
@@ -123,8 +127,8 @@ DEV void write_transposed(const typename Prec<DT>::T* tile, int ld, int nfeat, v
         l[j] = p[8];
       }
       u32x4* o = reinterpret_cast<u32x4*>(P::hi_ptr(dst, fm_index(f, m0 + c * 8, ldT)));
-      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(&h), o);
-      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(&l), o + 1);
+      opnd_store(*reinterpret_cast<const u32x4*>(&h), o);
+      opnd_store(*reinterpret_cast<const u32x4*>(&l), o + 1);
     }
     return;
   }
@@ -138,7 +142,7 @@ DEV void write_transposed(const typename Prec<DT>::T* tile, int ld, int nfeat, v
       reinterpret_cast<uint4*>(o)[0] = reinterpret_cast<const uint4*>(buf)[0];
       reinterpret_cast<uint4*>(o)[1] = reinterpret_cast<const uint4*>(buf)[1];
     } else if constexpr (DT == DT_BF16) {   // streaming store: see store4q_T
-      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(buf), reinterpret_cast<u32x4*>(o));
+      opnd_store(*reinterpret_cast<const u32x4*>(buf), reinterpret_cast<u32x4*>(o));
     } else {
       *reinterpret_cast<uint2*>(o) = *reinterpret_cast<const uint2*>(buf);
     }
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_value_kernel(MlpArgs a) {
                               ldx, ROWS, tid);
   } else {
     load_rows<DT, NT>(reinterpret_cast<const T*>(a.x_buf), a.idx, a.row0, m0, nvalid, a.d_in[3], X, ldx, ROWS, tid,
-                      [] {});
+                      [] {}, false, a.x_stream != 0);
   }
   preset_pad<DT>(H1, ld1, ROWS, a.n_out[3], tid, NT);
   preset_pad<DT>(H2, ld2, ROWS, a.n_out[4], tid, NT);
@@ -280,7 +284,7 @@ __global__ __launch_bounds__(NW * 64, (TrainOcc<DT, NW>::V)) void mlp_train_kern
                       preset_pad<DT>(H1p, ld1p, ROWS, a.n_out[0], tid, NT);
                       preset_pad<DT>(H1v, ld1v, ROWS, a.n_out[3], tid, NT);
                     },
-                    (a.ablate & 16) != 0);
+                    (a.ablate & 16) != 0, a.x_stream != 0);
   __syncthreads();
   STAMP(1);
   // ---------------- forward ----------------

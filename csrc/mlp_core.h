@@ -84,11 +84,11 @@ typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4v;
 template <int DT>
 DEV void store4q_T(typename Prec<DT>::T* dst, const typename Prec<DT>::T (&q)[4]) {
   if constexpr (DT == DT_F32) {
-    __builtin_nontemporal_store(f32x4s{q[0], q[1], q[2], q[3]}, reinterpret_cast<f32x4s*>(dst));
+    opnd_store(f32x4s{q[0], q[1], q[2], q[3]}, reinterpret_cast<f32x4s*>(dst));
   } else if constexpr (DT == DT_BF16) {
-    __builtin_nontemporal_store(*reinterpret_cast<const u32x2*>(q), reinterpret_cast<u32x2*>(dst));
+    opnd_store(*reinterpret_cast<const u32x2*>(q), reinterpret_cast<u32x2*>(dst));
   } else {
-    __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(q), reinterpret_cast<uint32_t*>(dst));
+    opnd_store(*reinterpret_cast<const uint32_t*>(q), reinterpret_cast<uint32_t*>(dst));
   }
 }
 
@@ -265,8 +265,8 @@ DEV void layer_gemm(const typename Prec<DT>::T* __restrict__ A, int lda, int kdi
               }
               if (outT != nullptr) {
                 __bf16* p = P::hi_ptr(outT, fm_index(c, m0 + r0, ldT));
-                __builtin_nontemporal_store(*reinterpret_cast<const u32x2*>(&hv), reinterpret_cast<u32x2*>(p));
-                __builtin_nontemporal_store(*reinterpret_cast<const u32x2*>(&lv), reinterpret_cast<u32x2*>(p + 8));
+                opnd_store(*reinterpret_cast<const u32x2*>(&hv), reinterpret_cast<u32x2*>(p));
+                opnd_store(*reinterpret_cast<const u32x2*>(&lv), reinterpret_cast<u32x2*>(p + 8));
               }
             } else {
               typename P::T q[4];

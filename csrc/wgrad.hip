@@ -286,7 +286,8 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
   } else if (dt == DT_F32) {
     launch_wgrad_lds<DT_F32, 3>(a, s);
   } else if (dt == DT_S3) {
-    launch_wgrad_lds<DT_S3, 3>(a, s);
+    if (a.waves == 16) launch_wgrad_lds<DT_S3, 2, 16>(a, s);   // 2 x 32 slots x 2 KiB = 128 KiB
+    else launch_wgrad_lds<DT_S3, 3>(a, s);
   } else if (a.waves == 16) {
     launch_wgrad_lds<DT_BF16, 4, 16>(a, s);
   } else if (g_wgrad_stages == 3) {

@@ -63,6 +63,9 @@ def _compile(src: str, cflags, verbose: bool) -> str:
     # (~1,600 v_accvgpr_* in mlp_train, 96 per wgrad k-step pair); with it those copies vanish.
     base = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
             "-mllvm", "-amdgpu-mfma-vgpr-form"]
+    # A/B builds of compile-time variants (e.g. DPPO_EXTRA_CFLAGS="-DDPPO_X_CACHED"); the
+    # flags enter the object cache key, so switching back rebuilds nothing stale
+    base += os.environ.get("DPPO_EXTRA_CFLAGS", "").split()
     flags = base + cflags
     key = _digest(deps, " ".join(flags))
     obj = os.path.join(BUILD, f"{os.path.splitext(src)[0]}-{key}.o")

@@ -170,7 +170,7 @@ class HipEngine:
         # fewer operand rows — 1,792 vs 2,304 per step for v_fc1 — but took 243 vs 226 us per
         # grad call; bf16 only, env DPPO_WGRAD_WAVES=16)
         self.wgrad_waves = int(os.environ.get("DPPO_WGRAD_WAVES", 8))
-        if self.dt != 1:
+        if self.dt not in (1, 3):
             self.wgrad_waves = 8
         self._pending_reduce = []        # async all-reduce works of the current step's buckets
         self._reduce_stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None

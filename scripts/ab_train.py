@@ -34,7 +34,8 @@ def timed(fn, reps=10):
 
 def build(dtype):
     dev = torch.device("cuda", 0)
-    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536, batch_size=65536,
+    E = int(os.environ.get("AB_ENVS", 4096))   # rows = 16 * E
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=E, exploration_size=16 * E, batch_size=16 * E,
                     dtype=dtype)
     spec = get_spec(p.env_name)
     torch.manual_seed(0)
