@@ -28,11 +28,12 @@ DEVICE_SRCS = ["rollout.hip", "mlp.hip", "wgrad.hip", "optim.hip", "obs.hip"]
 HEADERS = ["common.h", "mlp_core.h", "kernels.h"]
 
 
-def ext_path() -> str:
-    return os.path.join(OUT_DIR, EXT_NAME + sysconfig.get_config_var("EXT_SUFFIX"))
+def ext_path(variant: str = "") -> str:
+    name = EXT_NAME + (f"_{variant}" if variant else "")
+    return os.path.join(OUT_DIR, name + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
-def _torch_flags():
+def _torch_flags(ext_name: str = EXT_NAME):
     import torch
     from torch.utils import cpp_extension as ce
     inc = ce.include_paths(device_type="cuda")
@@ -40,7 +41,7 @@ def _torch_flags():
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     cflags = [f"-I{p}" for p in inc] + [f"-I{sysconfig.get_paths()['include']}",
                                          f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-                                         f"-DTORCH_EXTENSION_NAME={EXT_NAME}",
+                                         f"-DTORCH_EXTENSION_NAME={ext_name}",
                                          "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1"]
     ldflags = [f"-L{p}" for p in libdirs] + [f"-Wl,-rpath,{p}" for p in libdirs] + [
         "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip"]
@@ -55,9 +56,9 @@ def _digest(paths, extra: str) -> str:
     return h.hexdigest()[:16]
 
 
-def _compile(src: str, cflags, verbose: bool) -> str:
-    srcp = os.path.join(CSRC, src)
-    deps = [srcp] + [os.path.join(CSRC, h) for h in HEADERS]
+def _compile(src: str, cflags, verbose: bool, csrc: str = CSRC) -> str:
+    srcp = os.path.join(csrc, src)
+    deps = [srcp] + [os.path.join(csrc, h) for h in HEADERS]
     # -amdgpu-mfma-vgpr-form: MFMA accumulators in ordinary VGPRs (gfx90a+ unified register
     # file).  With AGPR accumulators the allocator shuffled them through VGPRs every loop turn
     # (~1,600 v_accvgpr_* in mlp_train, 96 per wgrad k-step pair); with it those copies vanish.
@@ -80,13 +81,17 @@ def _compile(src: str, cflags, verbose: bool) -> str:
     return obj
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
+def build(verbose: bool = False, force: bool = False, variant: str = "", csrc: str = CSRC) -> str:
+    """Build the extension.  ``variant`` + ``csrc`` (A/B diagnostics): the same bindings built
+    from another source tree (e.g. an earlier commit's csrc/) as module ``_dppo_hip_<variant>``,
+    loadable next to the default one (ops/native.py load_variant) so two kernel versions can be
+    timed interleaved in one process on one box."""
     os.makedirs(BUILD, exist_ok=True)
-    tcflags, ldflags = _torch_flags()
+    tcflags, ldflags = _torch_flags(EXT_NAME + (f"_{variant}" if variant else ""))
     jobs = [(s, []) for s in DEVICE_SRCS] + [("bindings.cpp", tcflags)]
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
-        objs = list(ex.map(lambda j: _compile(j[0], j[1], verbose), jobs))
-    out = ext_path()
+        objs = list(ex.map(lambda j: _compile(j[0], j[1], verbose, csrc), jobs))
+    out = ext_path(variant)
     key = _digest(objs, " ".join(ldflags))
     stamp = out + ".stamp"
     if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
@@ -105,5 +110,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
 
 
 if __name__ == "__main__":
-    p = build(verbose="-v" in sys.argv, force="--force" in sys.argv)
+    args = sys.argv[1:]
+    var = args[args.index("--variant") + 1] if "--variant" in args else ""
+    src = args[args.index("--src") + 1] if "--src" in args else CSRC
+    p = build(verbose="-v" in args, force="--force" in args, variant=var, csrc=src)
     print(p)

@@ -38,6 +38,15 @@ def load(build_if_missing: bool = False):
     return _MOD
 
 
+def load_variant(name: str):
+    """A/B diagnostics: the extension built from another source tree as ``_dppo_hip_<name>``
+    (``python -m pytorch_dppo_amd.ops._build --variant <name> --src <dir>``)."""
+    mod = importlib.import_module(f"pytorch_dppo_amd.ops._dppo_hip_{name}")
+    if getattr(mod, "arch", None) != "gfx950":
+        raise RuntimeError(f"variant {name} built for {getattr(mod, 'arch', '?')}")
+    return mod
+
+
 def available() -> bool:
     try:
         load()

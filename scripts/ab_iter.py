@@ -32,7 +32,21 @@ def main():
                     dtype=dtype, seed=1, phase_timing=0)
     w = DPPOWorker(p, ctx)
     ext = w.engine.ext
+    from pytorch_dppo_amd.ops import native
+    variants = {}
+
+    def use_ext(name):
+        # "A": the default build; any other name: the variant module _dppo_hip_<name> (same
+        # bindings, another kernel source tree: ops/_build.py --variant)
+        if name == "A":
+            w.engine.ext = ext
+        else:
+            if name not in variants:
+                variants[name] = native.load_variant(name)
+            w.engine.ext = variants[name]
+
     arms = {
+        "A": lambda: use_ext("A"), "B": lambda: use_ext("b"), "C": lambda: use_ext("c"),
         "x_cached": lambda: ext.set_x_stream(0), "x_stream": lambda: ext.set_x_stream(1),
         "s3w8": lambda: ext.set_s3_train_waves(8), "s3w4": lambda: ext.set_s3_train_waves(4),
     }

@@ -60,9 +60,12 @@ def main():
     M = eng.mb
 
     def train():
+        train_with(ext)
+
+    def train_with(mod):
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
                 1 if p.std_convention == "var" else 0, 0, eng.npart]
-        ext.mlp_train(eng.dt, eng.x_buf, eng.empty, 0, M, eng.wimg, eng.layout, eng.scales, eng.model.flat.data,
+        mod.mlp_train(eng.dt, eng.x_buf, eng.empty, 0, M, eng.wimg, eng.layout, eng.scales, eng.model.flat.data,
                       eng.log_std_old, eng.A, eng.actions, eng.logp, eng.adv, eng.ret, eng.values_buf, eng.mu_prev,
                       eng.v_prev, opts, [float(p.clip), float(p.ent_coeff)], eng.tbufs, eng.ldT, eng.part, False,
                       eng._xT_valid)
@@ -72,11 +75,27 @@ def main():
         ext.wgrad(eng.dt, eng.wg_g, eng.wg_x, eng.g_rows, eng.x_rows, eng.ldT, b["tasks"], b["tasks_host"], b["slab"],
                   eng.wgrad_waves)
 
+    from pytorch_dppo_amd.ops import native
+    ext_a = ext
+    variants = {}
+
+    def use_ext(name):   # "A" default build, else the variant module _dppo_hip_<name>
+        if name == "A":
+            mod = ext_a
+        else:
+            mod = variants.setdefault(name, native.load_variant(name))
+        eng.ext = mod
+        return mod
+
     def waves(n):
         return lambda: (ext.set_s3_train_waves(n), eng.sync_tile())
 
     arms = {
         "s3w4": (waves(4), train), "s3w8": (waves(8), train),
+        "trainA": (lambda: use_ext("A"), lambda: train_with(ext_a)),
+        "trainB": (lambda: use_ext("b"), lambda: train_with(variants["b"])),
+        "valA": (lambda: use_ext("A"), eng.values), "valB": (lambda: use_ext("b"), eng.values),
+        "rollA": (lambda: use_ext("A"), eng.rollout), "rollB": (lambda: use_ext("b"), eng.rollout),
         "train": (waves(8), train), "wgrad": (waves(8), wgrad),
         "grad": (waves(8), lambda: eng.grad(None)), "values": (waves(8), eng.values),
         "rollout": (waves(8), eng.rollout),
@@ -96,6 +115,7 @@ def main():
             setup, fn = arms[k]
             setup()
             res[k].append(timed(fn))
+    use_ext("A")
     ext.set_s3_train_waves(8)
     ext.set_train_ablation(0)
     out = {k: {"median_us": sorted(v)[len(v) // 2], "all_us": [round(x, 1) for x in v]} for k, v in res.items()}
