@@ -87,11 +87,17 @@ def main():
         eng.ext = mod
         return mod
 
+    def plan_mode(aligned):   # wgrad task plan: proportional chunks per tile vs one aligned row grid
+        if getattr(eng, "wgrad_aligned", None) != aligned:
+            eng.wgrad_aligned = aligned
+            eng._build_wgrad_plan(eng.model)
+
     def waves(n):
         return lambda: (ext.set_s3_train_waves(n), eng.sync_tile())
 
     arms = {
         "s3w4": (waves(4), train), "s3w8": (waves(8), train),
+        "wg_prop": (lambda: plan_mode(False), wgrad), "wg_aligned": (lambda: plan_mode(True), wgrad),
         "trainA": (lambda: use_ext("A"), lambda: train_with(ext_a)),
         "trainB": (lambda: use_ext("b"), lambda: train_with(variants["b"])),
         "valA": (lambda: use_ext("A"), eng.values), "valB": (lambda: use_ext("b"), eng.values),
@@ -116,6 +122,7 @@ def main():
             setup()
             res[k].append(timed(fn))
     use_ext("A")
+    plan_mode(False)
     ext.set_s3_train_waves(8)
     ext.set_train_ablation(0)
     out = {k: {"median_us": sorted(v)[len(v) // 2], "all_us": [round(x, 1) for x in v]} for k, v in res.items()}
