@@ -584,6 +584,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     TORCH_CHECK(nw == 4 || nw == 8, "split-bf16 train waves: 4 or 8");
     set_s3_train_waves((int)nw);
   });
+  m.def("s3_stream_state", []() { return (int64_t)s3_stream_state(); });
+  m.def("set_s3_stream", [](bool enable, int64_t stages) {
+    TORCH_CHECK(stages >= 3 && stages <= 6, "split-bf16 streaming update: 3..6 ring stages");
+    set_s3_stream(enable ? 1 : 0, (int)stages);
+  });
   m.def("set_debug_sync", &set_debug_sync);
   m.def("set_rollout_waves", [](int64_t nw) {
     TORCH_CHECK(nw == 4 || nw == 8, "rollout waves: 4 or 8");

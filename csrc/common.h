@@ -209,6 +209,17 @@ DEV float gauss(uint32_t base, uint32_t env, uint32_t step, uint32_t dim) {
   return (dim & 1u) ? g.y : g.x;
 }
 
+// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4): `lds` is the wave-uniform base, lane l
+// lands at lds + 16 * l; the global source address is per lane.
+DEV void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 |
+// lgkmcnt[11:8]=15 | vmcnt[5:4] in [15:14])
+#define WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt((((n) & 15) | (7 << 4) | (15 << 8) | ((((n) >> 4) & 3) << 14)))
+
 // Launch-error channel (optim.hip): every launcher records the first failed launch or
 // attribute call; every binding (bindings.cpp after_launch) takes it after its launch and raises
 // a Python exception naming the op — a refused launch never leaves a silently stale result.

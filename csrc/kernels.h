@@ -94,6 +94,14 @@ struct MlpArgs {
   int tstamp_every;
 };
 
+// row-stationary weight-streaming split-bf16 update (mlp_stream.hip): the default mlp_train
+// kernel for DT_S3 whenever the shapes fit its register tiles
+extern "C" int mlp_rs_applies(const MlpArgs& a);
+extern "C" size_t mlp_rs_lds_bytes();
+extern "C" void launch_mlp_train_rs(const MlpArgs& a, hipStream_t s);
+extern "C" void set_s3_stream(int enable, int stages);
+extern "C" int s3_stream_state();   // 0 off, else the ring depth
+
 struct WgradTask {
   int layer;      // 0..5
   int n0, k0;     // output tile origin

@@ -535,8 +535,10 @@ int train_rows_t(const MlpArgs& a) {
   if constexpr (DT == DT_F32) {
     return 16;
   } else if constexpr (DT == DT_S3) {
+    // the row-stationary streaming kernel (mlp_stream.hip) owns 64 rows per workgroup; otherwise
     // split-bf16 fragments are fp32-sized: the 64-row / 8-wave form spills (2 x 256 VGPRs per
     // SIMD is not enough), and at Humanoid dims only the 32-row tile fits LDS anyway
+    if (g_rows_override == 0 && mlp_rs_applies(a)) return 64;
     return g_rows_override == 16 ? 16 : 32;
   } else {
     const int want = g_rows_override;
@@ -585,6 +587,7 @@ int g_s3_train_waves = 8;
 template <int DT>
 int train_waves_t(const MlpArgs& a) {
   const int rows = train_rows_t<DT>(a);
+  if (DT == DT_S3 && rows == 64) return 4;   // streaming kernel
   if (rows == 64) return 8;
   if (DT == DT_S3 && rows == 32 && g_s3_train_waves == 8) return 8;
   return 4;
@@ -597,6 +600,10 @@ void train_t(const MlpArgs& a, hipStream_t s) {
   } else {
     const int rows = train_rows_t<DT>(a);
     if constexpr (DT == DT_S3) {
+      if (rows == 64) {
+        launch_mlp_train_rs(a, s);
+        return;
+      }
       if (rows == 32 && train_waves_t<DT>(a) == 8) {
         train_launch<DT, 32, 8>(a, s);
         return;
@@ -628,6 +635,7 @@ void value_t(const MlpArgs& a, hipStream_t s) {
 template <int DT>
 size_t train_lds_any(const MlpArgs& a) {
   const int rows = train_rows_t<DT>(a);
+  if (DT == DT_S3 && rows == 64) return mlp_rs_lds_bytes();
   return rows == 64 ? train_lds<DT, 64>(a) : rows == 32 ? train_lds<DT, 32>(a) : train_lds<DT, 16>(a);
 }
 

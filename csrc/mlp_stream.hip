@@ -1,0 +1,808 @@
+// Row-stationary, weight-streaming fused PPO update for split-bf16 operands (DT_S3, the
+// fp32-accurate headline mode).  Same math and outputs as mlp_train_kernel (mlp.hip), which stays
+// the generic path for every other precision and shape (the loss is
+// the corrected ppo.py:148-167 or the reference DPPO loss train.py:142-161).
+//
+// Why a second kernel.  mlp_train_kernel keeps a 32-row tile's activations in LDS and lets each
+// wave stream ITS weight columns from L2 into registers: at split-bf16 the 32-row tile already
+// takes 134 of 160 KiB of LDS, so a weight fragment fetched from L2 feeds only 32 rows, and the
+// kernel runs at the per-CU L2->CU rate (~80 GB/s per CU in v_fc1, MI355X_MICROARCH.md
+// §Indexed rows: 66-73 GB/s for L2-resident rows) — 1.7 MB of hi|lo weights per 32 rows.
+// Here the roles swap:
+//  * a workgroup is 4 waves (one per SIMD, up to 512 VGPRs each) and owns 64 batch rows; wave w
+//    owns rows 16w..16w+15 through the WHOLE chain (fc1 -> fc2 -> fc3 -> loss -> dgrad fc3 ->
+//    dgrad fc2).  Activations never leave registers (MFMA C layout); the next layer's A operand
+//    is rebuilt from them through a 2.3 KiB per-wave LDS transpose, so no layer waits on another
+//    wave and no activation tile occupies LDS;
+//  * the weights stream through an S-stage LDS ring filled by LDS-DMA (global_load_lds_dwordx4,
+//    no VGPR holds in-flight data): a stage is 8 split-bf16 fragments (16 KiB), each wave DMAs 2,
+//    all 4 read all 8 — one L2 read of a fragment feeds 64 rows, half the L2->CU bytes per row;
+//  * the observation rows come through the same ring: one fragment per wave per fc1 k-step,
+//    gathered by per-lane source addresses (rows of x_buf, or of idx[]), two k-steps ahead.
+//    Counted vmcnt waits + a raw s_barrier keep S-1 stages in flight across every barrier
+//    (cdna_hip_programming.md 'Pipelining across barriers'); past-the-end stages re-load the last
+//    one, so every wave issues exactly GL DMAs per stage and the count is exact.
+// Stream schedule of one tile (steps = ring stages):
+//   0                      X[0] | X[1] of every wave
+//   fc1, 6 per k-step      stage 0: 4 weight fragments + each wave's X[ks + 2]; stages 1-5: 8 weight
+//                          fragments — 44 slots for the 7 policy + 32 value output tiles
+//   fc2 policy / value     one per k-step: the 8 output tiles of that k-step
+//   fc3                    mu: 2 tiles x 4 k-steps;  v: 1 tile x 4 k-steps
+//   dgrad fc3              policy, value: the 8 output tiles (K = 32)
+//   dgrad fc2              2 output tiles x 4 k-steps per stage (policy 4 stages, value 16)
+#include <type_traits>
+
+#include "kernels.h"
+#include "mlp_core.h"
+
+namespace {
+
+using P = Prec<DT_S3>;
+using T = P::T;
+using Frag = P::Frag;
+
+constexpr float RS_LOG_2PI = 1.8378770664093453f;
+constexpr int RS_NPART = 8;           // fixed loss-term columns of a partial row (mlp.hip NPART_FIXED)
+constexpr int NW = 4, ROWS = 64;      // waves, rows per workgroup (16 per wave)
+constexpr int FB = 2048;              // bytes of one split-bf16 fragment (512 slots x 4 B)
+constexpr int NSLOT = 8;              // fragments per ring stage (2 DMA'd by each wave)
+constexpr int SB = NSLOT * FB;        // 16 KiB per stage
+constexpr int GL = 4;                 // global_load_lds per wave per stage (2 fragments x hi | lo)
+constexpr int SST = 36;               // fp32 row stride of a [16][32] transpose tile (conflict-free)
+constexpr int TILE_F = 16 * SST;
+constexpr int P1 = 7, V1 = 32;        // fc1 output tiles held: policy <= 7 (hidden <= 112), value <= 32
+constexpr int NACC1 = 8 + V1;         // acc1[t] policy tile t (t = 7 stays 0), acc1[8 + t] value tile t
+constexpr int JMAX = 8;               // action dims per lane held in registers (A <= 4 * JMAX)
+constexpr int TPR = 4;                // lanes per row in the loss (16 rows x 4 = 64 lanes)
+// per-wave scratch (floats): transpose tile, dL/dmu tile, dL/dv tile, mu [16][32], v [16],
+// dL/dlog_std per row [16][32], loss terms per row [16][8]
+constexpr int WS_F = 3 * TILE_F + 16 * 32 + 16 + 16 * 32 + 16 * RS_NPART;
+
+constexpr int MAX_STEPS = 128;        // stream steps of one tile (117 at Humanoid dims)
+
+int g_rs_enable = 0;   // A/B: default off until it beats the 32-row tile kernel (set_s3_stream)
+int g_rs_stages = 4;
+
+template <int S>
+constexpr size_t rs_lds_bytes() { return (size_t)S * SB + (size_t)NW * WS_F * sizeof(float); }
+
+struct Plan {
+  int ks1, kp2, kv2, k3p, k3v, kq2p, kq2v;   // k-steps: fc1, fc2 p / v, fc3 p / v, dgrad fc2 p / v
+  int np1, nv1, np2, nv2, nmu;               // output tiles: fc1 p / v (real), fc2 p / v, mu
+  int nd3p, nd3v, nd2p, nd2v;                // tiles of the transposed images (dgrad outputs)
+  int s_fc2p, s_fc2v, s_fc3, s_dg3, s_dg2p, s_dg2v, s_end;
+};
+
+DEV Plan make_plan(const MlpArgs& a) {
+  Plan p;
+  p.ks1 = a.d_in[0] >> 5;
+  p.kp2 = a.d_in[1] >> 5;
+  p.kv2 = a.d_in[4] >> 5;
+  p.k3p = a.d_in[2] >> 5;
+  p.k3v = a.d_in[5] >> 5;
+  p.kq2p = a.d_out[1] >> 5;
+  p.kq2v = a.d_out[4] >> 5;
+  p.np1 = (a.n_out[0] + 15) >> 4;
+  p.nv1 = (a.n_out[3] + 15) >> 4;
+  p.np2 = a.d_out[1] >> 4;
+  p.nv2 = a.d_out[4] >> 4;
+  p.nmu = a.d_out[2] >> 4;
+  p.nd3p = a.d_in[2] >> 4;
+  p.nd3v = a.d_in[5] >> 4;
+  p.nd2p = a.d_in[1] >> 4;
+  p.nd2v = a.d_in[4] >> 4;
+  p.s_fc2p = 1 + 6 * p.ks1;
+  p.s_fc2v = p.s_fc2p + p.kp2;
+  p.s_fc3 = p.s_fc2v + p.kv2;
+  p.s_dg3 = p.s_fc3 + 2;
+  p.s_dg2p = p.s_dg3 + 2;
+  p.s_dg2v = p.s_dg2p + ((p.np1 + 1) >> 1);
+  p.s_end = p.s_dg2v + ((p.nv1 + 1) >> 1);
+  return p;
+}
+
+// Ring slot q of stream step st: element offset of a weight fragment (wave-uniform), or -1 - ks for
+// the issuing wave's own observation fragment of fc1 k-step ks.  Slots past a layer's extent
+// re-load a valid fragment of the same layer (an L2 hit whose MFMA result is never stored).
+DEV int step_src(const MlpArgs& a, const Plan& p, int st, int q) {
+  if (st >= p.s_end) st = p.s_end - 1;
+  if (st == 0) return -1 - (q & 1);
+  if (st < p.s_fc2p) {
+    const int j = st - 1, ks = j / 6, sub = j - 6 * ks;
+    int f;
+    if (sub == 0) {
+      if (q & 1) return -1 - min(ks + 2, p.ks1 - 1);
+      f = q >> 1;
+    } else {
+      f = 4 + 8 * (sub - 1) + q;
+    }
+    if (f < P1) return a.off_w[0] + (int)fm_frag(f < p.np1 ? f : 0, ks, a.d_in[0], 0);
+    f -= P1;
+    return a.off_w[3] + (int)fm_frag(f < p.nv1 ? f : 0, ks, a.d_in[3], 0);
+  }
+  if (st < p.s_fc2v) return a.off_w[1] + (int)fm_frag(q < p.np2 ? q : 0, st - p.s_fc2p, a.d_in[1], 0);
+  if (st < p.s_fc3) return a.off_w[4] + (int)fm_frag(q < p.nv2 ? q : 0, st - p.s_fc2v, a.d_in[4], 0);
+  if (st == p.s_fc3) {
+    const int t = q >> 2, ks = q & 3;
+    return a.off_w[2] + (int)fm_frag(t < p.nmu ? t : 0, ks < p.k3p ? ks : 0, a.d_in[2], 0);
+  }
+  if (st == p.s_fc3 + 1) {
+    const int ks = q & 3;
+    return a.off_w[5] + (int)fm_frag(0, ks < p.k3v ? ks : 0, a.d_in[5], 0);
+  }
+  if (st == p.s_dg3) return a.off_wt[2] + (int)fm_frag(q < p.nd3p ? q : 0, 0, a.d_out[2], 0);
+  if (st == p.s_dg3 + 1) return a.off_wt[5] + (int)fm_frag(q < p.nd3v ? q : 0, 0, a.d_out[5], 0);
+  const bool pol = st < p.s_dg2v;
+  const int j = st - (pol ? p.s_dg2p : p.s_dg2v);
+  const int t = 2 * j + (q >> 2), ks = q & 3;
+  const int kq = pol ? p.kq2p : p.kq2v;
+  const int nt = pol ? p.nd2p : p.nd2v;
+  return (pol ? a.off_wt[1] : a.off_wt[4]) +
+         (int)fm_frag(t < nt ? t : 0, ks < kq ? ks : 0, pol ? a.d_out[1] : a.d_out[4], 0);
+}
+
+// fragment in ring slot q (the DMA de-interleaved it: every lane's hi 16 B, then every lane's lo)
+DEV Frag rfrag(const char* stg, int q, int lane) {
+  const char* b = stg + q * FB + lane * 16;
+  return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + 1024)};
+}
+
+// all N fragments of a stage into registers before any MFMA uses them: left to itself hipcc
+// interleaves each fragment's read with its 3 MFMAs and, at one wave per SIMD, pays the LDS
+// latency once per fragment instead of once per step
+template <int N>
+DEV void rfrags(const char* stg, int lane, Frag (&b)[N]) {
+#pragma unroll
+  for (int q = 0; q < N; ++q) b[q] = rfrag(stg, q, lane);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+DEV Frag split8(const f32x8& x) {
+  const bf16x8 h = __builtin_convertvector(x, bf16x8);
+  const bf16x8 l = __builtin_convertvector(x - __builtin_convertvector(h, f32x8), bf16x8);
+  return Frag{h, l};
+}
+
+DEV f32x8 join8(const Frag& f) {
+  return __builtin_convertvector(f.h, f32x8) + __builtin_convertvector(f.l, f32x8);
+}
+
+// C-layout tiles of features c0..c0+15 (v0) and c0+16..c0+31 (v1) -> [16][SST] fp32 (row = lane's
+// 4 rows 4*lg + i, column = lr): bank ((4lg + i) * 36 + lr) mod 64 is distinct over the wave
+DEV void tp_put(float* tp, const f32x4& v0, const f32x4& v1, int lane) {
+  const int lr = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    tp[(4 * lg + i) * SST + lr] = v0[i];
+    tp[(4 * lg + i) * SST + 16 + lr] = v1[i];
+  }
+}
+
+// A operand (row lr, k = 8 * lg .. 8 * lg + 7) of a [16][SST] tile, split to hi | lo.  The two
+// reads and their lgkmcnt wait are ONE asm statement: as plain loads, hipcc's waitcnt pass makes
+// every read of this per-wave tile wait vmcnt(0) for the ring's in-flight LDS-DMA (it cannot
+// tell the two LDS regions apart), which would drain the ring at every chained layer step.  The
+// tile is written by this wave's own ds_writes just before (LDS executes one wave's DS
+// instructions in order).
+DEV Frag tp_getA(const float* tp, int lane) {
+  const float* r = tp + (lane & 15) * SST + 8 * (lane >> 4);
+  const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)r;
+  float4 x0, x1;
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(x0), "=&v"(x1)
+               : "v"(addr)
+               : "memory");
+  return split8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
+}
+
+// activation chained into the next layer: features >= nb are zero padding except the constant-1
+// bias column nb (PackedLayout: the bias is column K of every weight image)
+DEV f32x4 bias_col(const f32x4& v, int c, int nb) {
+  const float o = c == nb ? 1.f : 0.f;
+  return c < nb ? v : f32x4{o, o, o, o};
+}
+
+// 4 consecutive m (rows 4lg..4lg+3 of the wave) of feature c -> the FM wgrad operand
+DEV void store_T(void* outT, const f32x4& v, int c, int m, int ldT) {
+  const bf16x4v hv = __builtin_convertvector(v, bf16x4v);
+  const bf16x4v lv = __builtin_convertvector(v - __builtin_convertvector(hv, f32x4), bf16x4v);
+  __bf16* p = P::hi_ptr(reinterpret_cast<T*>(outT), fm_index(c, m, ldT));
+  opnd_store(*reinterpret_cast<const u32x2*>(&hv), reinterpret_cast<u32x2*>(p));
+  opnd_store(*reinterpret_cast<const u32x2*>(&lv), reinterpret_cast<u32x2*>(p + 8));
+}
+
+// 8 consecutive m (rows 8h..8h+7) of column col of a [16][ld] fp32 tile -> one 32-byte FM group
+// of feature `feat`
+DEV void store_T8(void* outT, const float* tile, int ld, int col, int h, int feat, int m, int ldT) {
+  f32x8 x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = tile[(8 * h + j) * ld + col];
+  const Frag s = split8(x);
+  u32x4* o = reinterpret_cast<u32x4*>(P::hi_ptr(reinterpret_cast<T*>(outT), fm_index(feat, m, ldT)));
+  opnd_store(*reinterpret_cast<const u32x4*>(&s.h), o);
+  opnd_store(*reinterpret_cast<const u32x4*>(&s.l), o + 1);
+}
+
+// s_waitcnt vmcnt(BASE + extra): vector-memory operations retire in issue order (loads, stores
+// and LDS-DMA together, MI355X_MICROARCH.md §Per-instruction cycle constants), so a wait for the
+// DMA batch of step `cur` may leave outstanding every younger operation: the S-2 later batches
+// AND the `extra` stores this wave issued since its last batch.  Undercounting `extra` is safe
+// (the wait is longer), overcounting is not — callers pass exact counts or 0.
+template <int BASE, int E = 0>
+DEV void wait_batch(int extra) {
+  if constexpr (E >= 20 || BASE + E >= 63) {
+    WAIT_VMCNT(BASE + E);
+  } else {
+    if (extra <= E) WAIT_VMCNT(BASE + E);
+    else wait_batch<BASE, E + 1>(extra);
+  }
+}
+
+// phase timeline (diagnostics, scripts/phase_timeline.py): lane 0 of each wave of every
+// tstamp_every-th workgroup records the shader clock at the phase boundaries
+#define RS_STAMP(i)                                                                               \
+  do {                                                                                            \
+    if (a.tstamp != nullptr && (blockIdx.x % a.tstamp_every) == 0 && lane == 0)                   \
+      a.tstamp[((size_t)(blockIdx.x / a.tstamp_every) * NW + wave) * 16 + (i)] =                  \
+          __builtin_amdgcn_s_memtime();                                                           \
+  } while (0)
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1 (register-array indices
+// stay constants whatever the unroller decides for big bodies)
+template <int B, int E, typename F>
+DEV void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+template <int G>
+DEV float gsum(float x) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+template <int S>
+__global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int m0 = blockIdx.x * ROWS;
+  const int A = a.A;
+  const Plan p = make_plan(a);
+  char* ring = smem;
+  float* scr = reinterpret_cast<float*>(smem + (size_t)S * SB) + wave * WS_F;
+  float* tp = scr;
+  float* dmu = scr + TILE_F;
+  float* dvt = scr + 2 * TILE_F;
+  float* mus = scr + 3 * TILE_F;
+  float* vs = mus + 16 * 32;
+  float* dls = vs + 16;
+  float* lss = dls + 16 * 32;
+
+  // source row of tile row r (rows past M re-read row m0: finite data, zero gradient)
+  auto src_of = [&](int r) __attribute__((always_inline)) {
+    const int rr = (m0 + r < a.M) ? m0 + r : m0;
+    return a.idx ? a.idx[rr] : a.row0 + rr;
+  };
+  const int mw = m0 + 16 * wave;   // first row (m) of this wave
+  // the loss's row (TPR lanes per row): its source index is read before any DMA is in flight
+  const int lrow = lane / TPR, lsub = lane % TPR;
+  const bool lvalid = mw + lrow < a.M;
+  const int lsrc = src_of(16 * wave + lrow);
+
+  // DMA sources: raw buffer resources, so an issue is 2 buffer_load ... lds per slot with the
+  // per-lane part of the address in a constant VGPR (weights: the lane's 32 bytes of a
+  // fragment; X: the lane's row and k-group) and the step's offset in an SGPR
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x_buf), (short)0, 0x7fffffff, 0x00020000);
+  const unsigned vw = (unsigned)lane * 32u;
+  const unsigned vx = (unsigned)(((size_t)src_of(16 * wave + lr) * a.d_in[0] + 8 * lg) * sizeof(T));
+
+  // The stream's sources, computed once per workgroup and held in two VGPRs: lane l of cw[0] packs
+  // this wave's two slot codes of step l, cw[1] those of step 64 + l, 16 bits each — a weight
+  // fragment index (element offset / 512), or 0x8000 | ks for this wave's X fragment of k-step
+  // ks.  An issue reads its step with v_readlane: no LDS table read (which hipcc would make wait
+  // for the ring's DMA) and none of step_src's ~250 scalar instructions per step (at one wave per
+  // SIMD every issued instruction costs the MFMA pipe ~4 cycles).
+  auto code16 = [&](int st, int q) __attribute__((always_inline)) {
+    const int c = step_src(a, p, min(st, p.s_end - 1), q);
+    return (uint32_t)(c >= 0 ? (c >> 9) : (0x8000 | (-1 - c)));
+  };
+  const uint32_t cw0 = code16(lane, 2 * wave) | (code16(lane, 2 * wave + 1) << 16);
+  const uint32_t cw1 = code16(64 + lane, 2 * wave) | (code16(64 + lane, 2 * wave + 1) << 16);
+
+  auto issue = [&](int st, int stage) __attribute__((always_inline)) {
+    const uint32_t w0 = __builtin_amdgcn_readlane(cw0, st & 63);
+    const uint32_t w1 = __builtin_amdgcn_readlane(cw1, st & 63);
+    const uint32_t w = st < 64 ? w0 : w1;
+    __attribute__((address_space(3))) char* stg =
+        (__attribute__((address_space(3))) char*)(ring + stage * SB) + 2 * wave * FB;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t code = (w >> (16 * u)) & 0xffffu;
+      // (the instruction's immediate offset would move the LDS destination too: the hi | lo
+      // 16-byte halves differ in the SGPR offset instead)
+      if (!(code & 0x8000u)) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB, 16, vw, code * 2048u, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB + 1024, 16, vw, code * 2048u + 16u, 0, 0);
+      } else {
+        const uint32_t xo = (code & 0x7fffu) * 128u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, stg + u * FB, 16, vx, xo, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, stg + u * FB + 1024, 16, vx, xo + 16u, 0, 0);
+      }
+    }
+  };
+  int cur = 0, cst = 0, ist = 0;   // next step to consume, its stage, the stage refill() fills
+  // store instructions of each of the last S-2 steps: a step's stores precede its refill, so they
+  // are younger than the batch of every step up to S-2 later (and older than later batches)
+  constexpr int NH = S - 2 > 0 ? S - 2 : 1;
+  int hist[NH];
+#pragma unroll
+  for (int i = 0; i < NH; ++i) hist[i] = 0;
+  // Ring sync for step `cur`: this wave's DMAs of it by count (every younger vector-memory
+  // operation may stay in flight: the S-2 later batches and the last S-2 steps' stores), every
+  // wave's by the barrier, which also retires every wave's reads of the stage refill() refills.
+  // `stores` = store instructions of the previous step (undercounting is safe, overcounting not).
+  auto wait_step = [&](int stores) __attribute__((always_inline)) -> const char* {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = NH - 1; i > 0; --i) hist[i] = hist[i - 1];
+    hist[0] = stores;
+    int extra = 0;
+#pragma unroll
+    for (int i = 0; i < NH; ++i) extra += hist[i];
+    wait_batch<GL * (S - 2)>(S > 2 ? extra : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* stg = ring + cst * SB;
+    ist = cst == 0 ? S - 1 : cst - 1;
+    cst = cst + 1 == S ? 0 : cst + 1;
+    ++cur;
+    return stg;
+  };
+  // last thing of every step (after its reads and stores): DMA step cur + S - 2 into the stage the
+  // previous step used
+  auto refill = [&]() __attribute__((always_inline)) { issue(cur + S - 2, ist); };
+  RS_STAMP(0);
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st) issue(st, st);
+
+  // ---------------- fc1 (policy + value heads share X) ----------------
+  f32x4 acc1[NACC1];
+#pragma unroll
+  for (int t = 0; t < NACC1; ++t) acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const char* stg = wait_step(0);
+  Frag xa = rfrag(stg, 2 * wave, lane), xb = rfrag(stg, 2 * wave + 1, lane);
+  refill();
+  const bool want_xT = !a.xT_ready && (a.ablate & 1) == 0;
+  for (int ks = 0; ks < p.ks1; ++ks) {
+    stg = wait_step(0);
+    // slots 2f: weights f = 0..3; slot 2 * wave + 1: this wave's X[ks + 2]
+    Frag b0[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) b0[f] = rfrag(stg, 2 * f, lane);
+    const Frag xc = rfrag(stg, 2 * wave + 1, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, 4>([&](auto fc) __attribute__((always_inline)) {
+      constexpr int f = decltype(fc)::value;
+      acc1[f] = P::mma(acc1[f], xa, b0[f]);
+    });
+    int nstx = 0;
+    if (want_xT) {
+      // the rollout did not write this call's X^T: transpose the wave's 16 x 32 block here
+      const f32x8 x = join8(xa);
+      float4* w = reinterpret_cast<float4*>(tp + lr * SST + 8 * lg);
+      w[0] = float4{x[0], x[1], x[2], x[3]};
+      w[1] = float4{x[4], x[5], x[6], x[7]};
+      store_T8(a.xT, tp, SST, lane >> 1, lane & 1, 32 * ks + (lane >> 1), mw + 8 * (lane & 1), a.ldT);
+      nstx = 2;
+    }
+    refill();
+    static_for<1, 6>([&](auto sc) __attribute__((always_inline)) {
+      constexpr int sub = decltype(sc)::value;
+      stg = wait_step(sub == 1 ? nstx : 0);
+      Frag b[NSLOT];
+      rfrags(stg, lane, b);
+      static_for<0, NSLOT>([&](auto qc) __attribute__((always_inline)) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int f = 4 + 8 * (sub - 1) + q;
+        constexpr int t = f < P1 ? f : f + 1;
+        if constexpr (f < P1 + V1) acc1[t] = P::mma(acc1[t], xa, b[q]);
+      });
+      refill();
+    });
+    xa = xb;
+    xb = xc;
+  }
+
+  RS_STAMP(1);
+  // ---------------- fc2: h1 = tanh(fc1) chained two tiles (one k-step) at a time ----------------
+  // Software-pipelined: step i's MFMAs and step i+1's operand (tanh, the h1^T stores, the LDS
+  // transpose) share one scheduling region, so the VALU work fills the MFMA shadow.
+  const bool no_T = (a.ablate & 1) != 0;
+  const int n1p = a.n_out[0], n1v = a.n_out[3], n2p = a.n_out[1], n2v = a.n_out[4];
+  f32x4 acc2p[8], acc2v[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc2p[t] = acc2v[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int mr = mw + 4 * lg;   // first of the lane's 4 rows (C layout)
+  // operand of fc2 step i (i < 4: policy k-step i, else value k-step i - 4); returns its stores
+  auto prep_h1 = [&](int i, Frag& out) __attribute__((always_inline)) -> int {
+    const bool pol = i < 4;
+    const int ks = pol ? i : i - 4;
+    const int t0 = pol ? 2 * ks : 8 + 2 * ks;
+    const int nr = pol ? n1p : n1v;
+    const f32x4 h0 = act_tanh4<DT_S3>(acc1[t0]), h1 = act_tanh4<DT_S3>(acc1[t0 + 1]);
+    acc1[t0] = h0;
+    acc1[t0 + 1] = h1;
+    const int c0 = 32 * ks + lr;
+    int nst = 0;
+    if (!no_T) {
+      void* oT = pol ? a.h1pT : a.h1vT;
+      if (c0 < nr) store_T(oT, h0, c0, mr, a.ldT);
+      if (c0 + 16 < nr) store_T(oT, h1, c0 + 16, mr, a.ldT);
+      nst = (32 * ks < nr ? 2 : 0) + (32 * ks + 16 < nr ? 2 : 0);
+    }
+    tp_put(tp, bias_col(h0, c0, nr), bias_col(h1, c0 + 16, nr), lane);
+    out = tp_getA(tp, lane);
+    return nst;
+  };
+  Frag ah;
+  int nst = prep_h1(0, ah);
+  static_for<0, 20>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    stg = wait_step(nst);
+    Frag b[8];
+    rfrags(stg, lane, b);
+    if constexpr (i < 4) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc2p[q] = P::mma(acc2p[q], ah, b[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc2v[q] = P::mma(acc2v[q], ah, b[q]);
+    }
+    if constexpr (i + 1 < 20) nst = prep_h1(i + 1, ah);
+    if constexpr (i == 19) {
+      RS_STAMP(2);
+      // h2 = tanh(fc2), kept for dgrad fc3; its stores belong to this step (before the refill)
+      nst = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        acc2p[q] = act_tanh4<DT_S3>(acc2p[q]);
+        acc2v[q] = act_tanh4<DT_S3>(acc2v[q]);
+        const int c = 16 * q + lr;
+        if (!no_T && c < n2p) store_T(a.h2pT, acc2p[q], c, mr, a.ldT);
+        if (!no_T && c < n2v) store_T(a.h2vT, acc2v[q], c, mr, a.ldT);
+        if (!no_T) nst += (16 * q < n2p ? 2 : 0) + (16 * q < n2v ? 2 : 0);
+      }
+    }
+    refill();
+  });
+
+  // loss inputs of this lane's row (TPR lanes per row): issued now, consumed after fc3
+  // (every global value the loss reads is loaded here: with the ring's LDS-DMA in flight, hipcc
+  // waits vmcnt(0) at the first use of an ordinary load, so they must all be in flight together)
+  const bool ref_loss = a.loss_kind != 0;
+  float actv[JMAX], lsv[JMAX], lsov[JMAX], mupv[JMAX];
+#pragma unroll
+  for (int q = 0; q < JMAX; ++q) {
+    const int j = lsub + q * TPR;
+    actv[q] = j < A ? a.actions[(size_t)lsrc * A + j] : 0.f;
+    lsv[q] = j < A ? a.log_std[j] : 0.f;
+    lsov[q] = (ref_loss && j < A) ? a.log_std_old[j] : 0.f;
+    mupv[q] = (ref_loss && j < A) ? a.mu_prev[(size_t)lsrc * A + j] : 0.f;
+  }
+  const float l_adv = a.adv[lsrc], l_ret = a.ret[lsrc];
+  const float l_lpo = !ref_loss ? a.logp_old[lsrc] : 0.f;
+  const float l_vold = !ref_loss ? a.v_old[lsrc] : 0.f;
+  const float l_vprev = ref_loss ? a.v_prev[lsrc] : 0.f;
+
+  // ---------------- fc3 (mu, v) ----------------
+  Frag am[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int c0 = 32 * ks + lr;
+    tp_put(tp, bias_col(acc2p[2 * ks], c0, n2p), bias_col(acc2p[2 * ks + 1], c0 + 16, n2p), lane);
+    am[ks] = tp_getA(tp, lane);
+  }
+  stg = wait_step(nst);
+  f32x4 amu0 = f32x4{0.f, 0.f, 0.f, 0.f}, amu1 = amu0, av0 = amu0;
+  {
+    Frag b[8];
+    rfrags(stg, lane, b);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      amu0 = P::mma(amu0, am[ks], b[ks]);
+      amu1 = P::mma(amu1, am[ks], b[4 + ks]);
+    }
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int c0 = 32 * ks + lr;
+    tp_put(tp, bias_col(acc2v[2 * ks], c0, n2v), bias_col(acc2v[2 * ks + 1], c0 + 16, n2v), lane);
+    am[ks] = tp_getA(tp, lane);
+  }
+  refill();
+  stg = wait_step(0);
+  {
+    Frag b[4];
+    rfrags(stg, lane, b);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) av0 = P::mma(av0, am[ks], b[ks]);
+  }
+
+  RS_STAMP(3);
+  // ---------------- loss + dL/d(mu, log_std, v) (inside the fc3-v step: before its refill) -------
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * lg + i;
+    if (lr < A) mus[r * 32 + lr] = amu0[i];
+    if (16 + lr < A) mus[r * 32 + 16 + lr] = amu1[i];
+    if (lr == 0) vs[r] = av0[i];
+  }
+  {
+    // zero the dL/dmu and dL/dv tiles (columns >= A / >= 1 are the padded K of dgrad fc3)
+    float4* z0 = reinterpret_cast<float4*>(dmu + lr * SST + 8 * lg);
+    float4* z1 = reinterpret_cast<float4*>(dvt + lr * SST + 8 * lg);
+    z0[0] = z0[1] = z1[0] = z1[1] = float4{0.f, 0.f, 0.f, 0.f};
+  }
+  {
+    const int r = lrow, sub = lsub, src = lsrc;
+    const bool valid = lvalid;
+    // action dim j = sub + q * TPR < A <= TPR * JMAX: every loop over j is unrolled over q, so
+    // actv[q] is a static register index
+    const float advv = l_adv;
+    const float v = vs[r];
+    const float cvar = a.std_var ? 0.5f : 1.f;
+    float lclip = 0.f, lent = 0.f, kl = 0.f, cf = 0.f, vold;
+    if (a.loss_kind == 0) {
+      // ---- corrected PPO (ppo.py:148-167) ----
+      float logp = 0.f;
+#pragma unroll
+      for (int q = 0; q < JMAX; ++q) {
+        const int j = sub + q * TPR;
+        if (j >= A) break;
+        const float lsig = cvar * lsv[q];
+        const float z = (actv[q] - mus[r * 32 + j]) * __expf(-lsig);
+        logp += -0.5f * z * z - 0.5f * RS_LOG_2PI - lsig;
+      }
+      logp = gsum<TPR>(logp);
+      const float lrat = logp - l_lpo;
+      const float ratio = __expf(lrat);
+      const float s1 = ratio * advv;
+      const float s2 = fminf(fmaxf(ratio, 1.f - a.clip), 1.f + a.clip) * advv;
+      lclip = -fminf(s1, s2);
+      const float dlogp = (s1 <= s2) ? -advv * ratio : 0.f;
+      kl = (ratio - 1.f) - lrat;
+      cf = (fabsf(ratio - 1.f) > a.clip) ? 1.f : 0.f;
+#pragma unroll
+      for (int q = 0; q < JMAX; ++q) {
+        const int j = sub + q * TPR;
+        if (j >= A) break;
+        const float lsig = cvar * lsv[q];
+        const float isig = __expf(-lsig);
+        const float z = (actv[q] - mus[r * 32 + j]) * isig;
+        dmu[r * SST + j] = valid ? dlogp * z * isig : 0.f;
+        // d/dlog_std: logp term + entropy bonus (-ent_coeff * sum_j log sigma_j)
+        dls[r * 32 + j] = valid ? (dlogp * (z * z - 1.f) - a.ent_coeff) * cvar : 0.f;
+        lent += -a.ent_coeff * (0.5f + 0.5f * RS_LOG_2PI + lsig);
+      }
+      lent = gsum<TPR>(lent);
+      vold = l_vold;
+    } else {
+      // ---- reference DPPO loss (train.py:142-161): per-dim pdf ratio, variance convention ----
+      const float invA = 1.f / (float)A;
+      const bool first = a.first_step != 0;
+#pragma unroll
+      for (int q = 0; q < JMAX; ++q) {
+        const int j = sub + q * TPR;
+        if (j >= A) break;
+        const float mu = mus[r * 32 + j];
+        const float var = __expf(lsv[q]);
+        const float mu_o = first ? mu : mupv[q];
+        const float var_o = first ? var : __expf(lsov[q]);
+        const float x = actv[q];
+        const float pd = __expf(-(x - mu) * (x - mu) / (2.f * var)) * rsqrtf(2.f * var * 3.14159265358979f);
+        const float po = __expf(-(x - mu_o) * (x - mu_o) / (2.f * var_o)) * rsqrtf(2.f * var_o * 3.14159265358979f);
+        const float ratio = pd / (1e-10f + po);
+        const float s1 = ratio * advv;
+        const float s2 = fminf(fmaxf(ratio, 1.f - a.clip), 1.f + a.clip) * advv;
+        lclip += -fminf(s1, s2) * invA;
+        const float dratio = (s1 <= s2) ? -advv * invA : 0.f;
+        float dp = dratio / (1e-10f + po);
+        const float lgp = logf(pd + 1e-5f);
+        lent += -a.ent_coeff * pd * lgp * invA;
+        dp += -a.ent_coeff * invA * (lgp + pd / (pd + 1e-5f));
+        dmu[r * SST + j] = valid ? dp * pd * (x - mu) / var : 0.f;
+        dls[r * 32 + j] = valid ? dp * pd * ((x - mu) * (x - mu) / (2.f * var) - 0.5f) : 0.f;
+        cf += (fabsf(ratio - 1.f) > a.clip) ? invA : 0.f;
+        if (valid) a.mu_prev[(size_t)src * A + j] = mu;   // train.py:164 model_old <- model
+      }
+      lclip = gsum<TPR>(lclip);
+      lent = gsum<TPR>(lent);
+      cf = gsum<TPR>(cf);
+      vold = first ? v : l_vprev;
+    }
+    if (sub == 0) {
+      const float retv = l_ret;
+      float dv, lv;
+      if (a.value_loss == 0) {
+        const float d = v - retv;
+        lv = d * d;
+        dv = 2.f * d;
+      } else {
+        const float d1 = v - retv;
+        const float dd = v - vold;
+        const float vc = vold + fminf(fmaxf(dd, -a.clip), a.clip);
+        const float d2 = vc - retv;
+        const float f1 = d1 * d1, f2 = d2 * d2;
+        const float inr = (dd >= -a.clip && dd <= a.clip) ? 1.f : 0.f;
+        lv = 0.5f * fmaxf(f1, f2);
+        if (f1 > f2) dv = d1;
+        else if (f2 > f1) dv = d2 * inr;
+        else dv = 0.5f * d1 + 0.5f * d2 * inr;
+      }
+      if (a.loss_kind != 0 && valid) a.v_prev[src] = v;
+      dvt[r * SST] = valid ? dv : 0.f;
+      float* lrw = lss + r * RS_NPART;
+      const float vm = valid ? 1.f : 0.f;
+      lrw[0] = lclip * vm; lrw[1] = lv * vm; lrw[2] = lent * vm; lrw[3] = kl * vm; lrw[4] = cf * vm;
+      lrw[5] = vm; lrw[6] = 0.f; lrw[7] = 0.f;
+    }
+  }
+  // dY^T of the output layers: item = (feature, 8-row half) of this wave's 16 rows
+  for (int it = lane; it < 2 * A + 2; it += 64) {
+    if (it < 2 * A) store_T8(a.g3pT, dmu, SST, it >> 1, it & 1, it >> 1, mw + 8 * (it & 1), a.ldT);
+    else store_T8(a.g3vT, dvt, SST, 0, it - 2 * A, 0, mw + 8 * (it - 2 * A), a.ldT);
+  }
+
+  refill();   // (the loss's stores are not counted: the next S-2 waits also wait for them)
+
+  RS_STAMP(4);
+  // ---------------- dgrad fc3: dpre2 = (dY W3) * (1 - h2^2) ----------------
+  Frag a2p[4], a2v[4];
+  auto dgrad3 = [&](const Frag& ad, const f32x4 (&h2)[8], int n2, void* oT, Frag (&a2)[4]) __attribute__((always_inline)) -> int {
+    f32x4 d[8];
+    Frag b[8];
+    rfrags(stg, lane, b);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) d[q] = P::mma(f32x4{0.f, 0.f, 0.f, 0.f}, ad, b[q]);
+    int n = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = 16 * q + lr;
+      d[q] = c < n2 ? d[q] * (1.0f - h2[q] * h2[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!no_T && c < n2) store_T(oT, d[q], c, mr, a.ldT);
+      if (!no_T) n += 16 * q < n2 ? 2 : 0;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      tp_put(tp, d[2 * ks], d[2 * ks + 1], lane);
+      a2[ks] = tp_getA(tp, lane);
+    }
+    return n;
+  };
+  {
+    const Frag ad = tp_getA(dmu, lane);
+    stg = wait_step(0);
+    nst = dgrad3(ad, acc2p, n2p, a.g2pT, a2p);
+    refill();
+  }
+  {
+    const Frag ad = tp_getA(dvt, lane);
+    stg = wait_step(nst);
+    nst = dgrad3(ad, acc2v, n2v, a.g2vT, a2v);
+    refill();
+  }
+
+  RS_STAMP(5);
+  // ---------------- dgrad fc2: g1 = (dpre2 W2) * (1 - h1^2), only the wgrad operand ----------------
+  // 4 policy + 16 value steps of 2 output tiles; step j's epilogue (dtanh + stores) runs in step
+  // j+1 beside its MFMAs
+  f32x4 gp0 = f32x4{0.f, 0.f, 0.f, 0.f}, gp1 = gp0;
+  auto epi_g1 = [&](int j) __attribute__((always_inline)) -> int {
+    const bool pol = j < 4;
+    const int jj = pol ? j : j - 4;
+    const int t0 = pol ? 2 * jj : 8 + 2 * jj;
+    const int nr = pol ? n1p : n1v;
+    void* oT = pol ? a.g1pT : a.g1vT;
+    const int c0 = 32 * jj + lr;
+    if (c0 < nr) store_T(oT, gp0 * (1.0f - acc1[t0] * acc1[t0]), c0, mr, a.ldT);
+    if (c0 + 16 < nr) store_T(oT, gp1 * (1.0f - acc1[t0 + 1] * acc1[t0 + 1]), c0 + 16, mr, a.ldT);
+    return (32 * jj < nr ? 2 : 0) + (32 * jj + 16 < nr ? 2 : 0);
+  };
+  static_for<0, 20>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    stg = wait_step(nst);
+    f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
+    Frag b[8];
+    rfrags(stg, lane, b);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const Frag& a2 = j < 4 ? a2p[ks] : a2v[ks];
+      g0 = P::mma(g0, a2, b[ks]);
+      g1 = P::mma(g1, a2, b[4 + ks]);
+    }
+    if constexpr (j > 0) nst = epi_g1(j - 1);
+    else nst = 0;
+    gp0 = g0;
+    gp1 = g1;
+    refill();
+    if constexpr (j == 3) RS_STAMP(6);
+  });
+  epi_g1(19);
+  RS_STAMP(7);
+
+  // ---------------- per-workgroup partials (deterministic fixed order) ----------------
+  WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
+  __syncthreads();
+  const float* sc0 = reinterpret_cast<const float*>(smem + (size_t)S * SB);
+  for (int q = tid; q < RS_NPART + A; q += NW * 64) {
+    float s = 0.f;
+    for (int w = 0; w < NW; ++w) {
+      const float* b = sc0 + w * WS_F + 3 * TILE_F + 16 * 32 + 16;   // dls of wave w
+      if (q < RS_NPART) {
+        for (int r = 0; r < 16; ++r) s += b[16 * 32 + r * RS_NPART + q];
+      } else {
+        for (int r = 0; r < 16; ++r) s += b[r * 32 + q - RS_NPART];
+      }
+    }
+    a.part[(size_t)blockIdx.x * a.npart + q] = s;
+  }
+}
+
+template <int S>
+void rs_launch(const MlpArgs& a, hipStream_t s) {
+  const size_t lds = rs_lds_bytes<S>();
+  set_max_lds_once<mlp_train_rs_kernel<S>>(lds);
+  const int nblk = (a.M + ROWS - 1) / ROWS;
+  hipLaunchKernelGGL((mlp_train_rs_kernel<S>), dim3(nblk), dim3(NW * 64), lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+// shapes the streaming kernel covers: its register tiles and unrolled step bodies are those of
+// the reference network (policy 100-100, value 500-100, hidden widths 97-112 / 481-511 / 97-127
+// give the same tile counts), any observation width <= 383 and action width <= 32; every other
+// shape runs the 32-row tile kernel
+extern "C" int mlp_rs_applies(const MlpArgs& a) {
+  if (!g_rs_enable) return 0;
+  return a.d_in[0] <= 384 && a.d_in[0] == a.d_in[3] && (a.n_out[0] + 15) / 16 == P1 &&
+         (a.n_out[3] + 15) / 16 == V1 && a.d_in[1] == 128 && a.d_in[4] == 512 && a.d_in[2] == 128 &&
+         a.d_in[5] == 128 && a.d_out[1] == 128 && a.d_out[4] == 128 && a.d_out[2] == 32 && a.d_out[5] == 32 &&
+         a.n_out[1] > 96 && a.n_out[4] > 96 && a.A >= 1 && a.A <= 32;
+}
+
+extern "C" size_t mlp_rs_lds_bytes() {
+  switch (g_rs_stages) {
+    case 3: return rs_lds_bytes<3>();
+    case 5: return rs_lds_bytes<5>();
+    case 6: return rs_lds_bytes<6>();
+    default: return rs_lds_bytes<4>();
+  }
+}
+
+extern "C" void launch_mlp_train_rs(const MlpArgs& a, hipStream_t s) {
+  switch (g_rs_stages) {
+    case 3: rs_launch<3>(a, s); break;
+    case 5: rs_launch<5>(a, s); break;
+    case 6: rs_launch<6>(a, s); break;
+    default: rs_launch<4>(a, s); break;
+  }
+}
+
+extern "C" int s3_stream_state() { return g_rs_enable ? g_rs_stages : 0; }
+
+extern "C" void set_s3_stream(int enable, int stages) {
+  g_rs_enable = enable ? 1 : 0;
+  if (stages >= 3 && stages <= 6) g_rs_stages = stages;
+}

@@ -109,14 +109,6 @@ constexpr size_t wgrad_lds_bytes() { return (size_t)S * WgSlots<W>::N * wgrad_fr
 // CU), 4 (96 KiB) or 6 (144 KiB; five steps = 120 KiB of DMA in flight per CU)
 int g_wgrad_stages = 4;
 
-DEV void glds16(const void* g, void* lds) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
-}
-
-// s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 |
-// lgkmcnt[11:8]=15 | vmcnt[5:4] in [15:14])
-#define WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt((((n) & 15) | (7 << 4) | (15 << 8) | ((((n) >> 4) & 3) << 14)))
 
 template <int DT, int S, int C, int W>
 DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {

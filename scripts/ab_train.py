@@ -57,6 +57,7 @@ def main():
     want = sys.argv[2].split(",") if len(sys.argv) > 2 else ["s3w4", "s3w8"]
     p, eng = build(dtype)
     ext = eng.ext
+    state = ext.s3_stream_state()
     M = eng.mb
 
     def train():
@@ -98,6 +99,11 @@ def main():
     arms = {
         "s3w4": (waves(4), train), "s3w8": (waves(8), train),
         "wg_prop": (lambda: plan_mode(False), wgrad), "wg_aligned": (lambda: plan_mode(True), wgrad),
+        "rs3": (lambda: (ext.set_s3_stream(True, 3), eng.sync_tile()), train),
+        "rs4": (lambda: (ext.set_s3_stream(True, 4), eng.sync_tile()), train),
+        "rs5": (lambda: (ext.set_s3_stream(True, 5), eng.sync_tile()), train),
+        "rs6": (lambda: (ext.set_s3_stream(True, 6), eng.sync_tile()), train),
+        "tile32": (lambda: (ext.set_s3_stream(False, 4), eng.sync_tile()), train),
         "trainA": (lambda: use_ext("A"), lambda: train_with(ext_a)),
         "trainB": (lambda: use_ext("b"), lambda: train_with(variants["b"])),
         "valA": (lambda: use_ext("A"), eng.values), "valB": (lambda: use_ext("b"), eng.values),
@@ -122,6 +128,8 @@ def main():
             setup()
             res[k].append(timed(fn))
     use_ext("A")
+    ext.set_s3_stream(state > 0, state or 4)
+    eng.sync_tile()
     plan_mode(False)
     ext.set_s3_train_waves(8)
     ext.set_train_ablation(0)

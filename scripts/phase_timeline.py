@@ -19,6 +19,8 @@ from pytorch_dppo_amd.models.actor_critic import ActorCritic  # noqa: E402
 from pytorch_dppo_amd.runtime.engine_hip import HipEngine  # noqa: E402
 from pytorch_dppo_amd.utils.obs_stats import RunningObsStats  # noqa: E402
 
+PHASES_RS = ["fc1 (X ring + 39 tiles)", "fc2 (chained)", "h2 epilogue + fc3", "loss + dY stores", "dgrad fc3",
+             "dgrad fc2 policy", "dgrad fc2 value"]
 PHASES = ["load_x+preset", "fc1 (p,v) own", "fc1 barrier wait", "preset", "fc2 own", "fc2 barrier wait",
           "fc3 + sync", "loss + sync", "partials+dY^T stores", "dgrad fc3 own", "dgrad fc3 barrier",
           "dgrad fc2 own"]
@@ -44,8 +46,12 @@ def main():
     ext = eng.ext
     out = {}
     for rows in [int(r) for r in os.environ.get("TIMELINE_ROWS", "64,32").split(",")]:
-        ext.set_mlp_rows(rows)
+        ext.set_mlp_rows(rows)      # 0: the default kernel (split-bf16: the streaming kernel)
         eng.sync_tile()
+        rs = rows == 0
+        rows = eng.train_rows
+        phases = PHASES_RS if rs else PHASES
+        nph = len(phases)
         nw = int(ext.train_waves(eng.dt, eng.layout, eng.A))
         nblk = eng.ldT // rows
         buf = torch.zeros(((nblk + EVERY - 1) // EVERY) * nw * 16, dtype=torch.int64, device=dev)
@@ -58,14 +64,14 @@ def main():
         ext.set_train_ablation(0)
         ext.set_train_tstamp(torch.empty(0, dtype=torch.int64, device=dev), 1)
         t = buf.view(-1, nw, 16).cpu().double()
-        d = t[:, :, 1:13] - t[:, :, 0:12]              # [blk][wave][phase]
-        tot = (t[:, :, 12] - t[:, :, 0])
-        res = {"rows": rows, "sampled_blocks": t.shape[0],
+        d = t[:, :, 1:nph + 1] - t[:, :, 0:nph]        # [blk][wave][phase]
+        tot = (t[:, :, nph] - t[:, :, 0])
+        res = {"rows": rows, "kernel": "streaming" if rs else "tile", "sampled_blocks": t.shape[0],
                "total_cycles_median": float(tot.median()),
                "phases_median_cycles(max over waves)": {ph: float(d[:, :, i].max(dim=1).values.median())
-                                                        for i, ph in enumerate(PHASES)},
+                                                        for i, ph in enumerate(phases)},
                "phases_median_cycles(mean over waves)": {ph: float(d[:, :, i].mean(dim=1).median())
-                                                         for i, ph in enumerate(PHASES)}}
+                                                         for i, ph in enumerate(phases)}}
         # per dispatch round (blocks b .. b + #CUs - 1 start together): is the x load slower in
         # the first, lockstep round than in later ones?  (s_memtime is per XCD: compare within
         # XCD = block % 8, relative to that XCD's first stamp.)
@@ -89,7 +95,7 @@ def main():
                 rel[m] = start[m] - start[m].min()
         res["start_rel_cycles_by_round"] = {int(r_): [float(v) for v in rel[rnd == r_].quantile(
             torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64))] for r_ in sorted(set(rnd.tolist()))}
-        out[f"rows{rows}"] = res
+        out[("rs" if rs else "rows") + str(rows)] = res
     ext.set_mlp_rows(0)
     # rollout: per-wave cycles per phase summed over the T steps, median over workgroups
     nblk = (eng.E + 15) // 16

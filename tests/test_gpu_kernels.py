@@ -272,6 +272,52 @@ def test_fused_loss_backward_row_tiles(rows, env_name, mb):
         ext.set_mlp_rows(0)
 
 
+@pytest.mark.parametrize("env_name,mb,stages", [("Humanoid-v2", 512, 4), ("Humanoid-v2", 200, 3),
+                                               ("HalfCheetah-v2", 256, 5), ("Pendulum-v0", 64, 6)])
+def test_s3_streaming_update_matches_tile_kernel(env_name, mb, stages):
+    """split-bf16: the row-stationary weight-streaming update (csrc/mlp_stream.hip, 64 rows per
+    workgroup, every ring depth) vs the 32-row tile kernel (mlp.hip) on the same minibatch —
+    gradients, loss terms and the wgrad operands both write (idx gather, ragged last tile, the
+    in-kernel X^T path)."""
+    ext = _ext()
+    p = ppo_preset(device="gpu", env_name=env_name, num_envs=64, exploration_size=64 * 8,
+                   batch_size=mb, dtype="bf16x3", ent_coeff=0.01)
+    eng, model, _, _ = _engine(p)
+    xq = _fill_buffer(eng, model)
+    idx = torch.randperm(eng.N, generator=torch.Generator().manual_seed(11))[:mb]
+    res = {}
+    state = ext.s3_stream_state()
+    try:
+        for on in (True, False):
+            ext.set_s3_stream(on, stages)
+            eng.sync_tile()
+            assert eng.train_rows == (64 if on else 32)
+            eng.begin_update()
+            eng.grad(idx)
+            res[on] = (eng.grad_flat.clone(), eng.last_losses(), eng.g1vT.clone(), eng.h1pT.clone())
+    finally:
+        ext.set_s3_stream(state > 0, state or 4)
+        eng.sync_tile()
+    g_rs, l_rs, g1_rs, h1_rs = res[True]
+    g_t, l_t, g1_t, h1_t = res[False]
+    rel = (g_rs - g_t).norm().item() / (g_t.norm().item() + 1e-12)
+    assert rel < 2e-5, rel
+    for k in ("loss_clip", "loss_value"):
+        assert abs(l_rs[k] - l_t[k]) < 1e-5 * (1 + abs(l_t[k])), (k, l_rs[k], l_t[k])
+    from pytorch_dppo_amd.models.actor_critic import fm_index
+
+    def rowmajor(buf, nfeat):   # FM [features][ldT] -> row-major, the call's mb columns
+        r = torch.arange(nfeat, device=DEV).repeat_interleave(mb)
+        c = torch.arange(mb, device=DEV).repeat(nfeat)
+        return eng.decode(buf).reshape(-1)[fm_index(r, c, eng.ldT)].view(nfeat, mb)
+
+    n1p, n1v = model.layer("p_fc1").fan_out, model.layer("v_fc1").fan_out
+    for a_, b_ in ((rowmajor(h1_rs, n1p), rowmajor(h1_t, n1p)), (rowmajor(g1_rs, n1v), rowmajor(g1_t, n1v))):
+        assert (a_ - b_).norm().item() <= 1e-5 * b_.norm().item()
+    g_ref, _ = _torch_grad(model, p, xq, eng, idx.to(DEV))
+    assert (g_rs - g_ref).norm().item() / g_ref.norm().item() < 2e-4
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "bf16x3"])
 def test_rollout_written_xT_equals_kernel_written_xT(dtype):
     """full-batch: the x^T operand the rollout emits == the one mlp_train would transpose."""
@@ -291,13 +337,19 @@ def test_rollout_written_xT_equals_kernel_written_xT(dtype):
     eng._xT_valid = False            # force the fused kernel to write x^T itself
     eng.xT.zero_()
     eng.grad(None)
-    assert torch.equal(eng.xT, xT_roll)
-    assert torch.equal(eng.grad_flat, g_roll)
+    # split-bf16: equal VALUES (hi + lo); the (hi, lo) bits may differ where a lo of -0.0 / a
+    # flushed denormal was re-split from the sum (the streaming kernel re-splits hi + lo)
+    assert torch.equal(eng.decode(eng.xT), eng.decode(xT_roll))
+    if dtype == "bf16":
+        assert torch.equal(eng.grad_flat, g_roll)
+    else:
+        assert (eng.grad_flat - g_roll).norm().item() <= 1e-6 * g_roll.norm().item()
 
 
-def test_dppo_ref_loss_two_steps_matches_autograd():
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3"])
+def test_dppo_ref_loss_two_steps_matches_autograd(dtype):
     p = dppo_preset(device="gpu", env_name="HalfCheetah-v2", num_envs=32, exploration_size=256,
-                    batch_size=256, dtype="fp32", loss="dppo_ref", ent_coeff=0.01)
+                    batch_size=256, dtype=dtype, loss="dppo_ref", ent_coeff=0.01)
     eng, model, _, _ = _engine(p)
     xq = _fill_buffer(eng, model)
     eng.begin_update()
