@@ -586,7 +586,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("s3_stream_state", []() { return (int64_t)s3_stream_state(); });
   m.def("set_s3_stream", [](bool enable, int64_t stages) {
-    TORCH_CHECK(stages >= 3 && stages <= 6, "split-bf16 streaming update: 3..6 ring stages");
+    TORCH_CHECK(stages == 2 || stages == 3, "split-bf16 streaming update: 2 or 3 ring stages (32 KiB each)");
     set_s3_stream(enable ? 1 : 0, (int)stages);
   });
   m.def("set_debug_sync", &set_debug_sync);

@@ -45,9 +45,10 @@ constexpr float RS_LOG_2PI = 1.8378770664093453f;
 constexpr int RS_NPART = 8;           // fixed loss-term columns of a partial row (mlp.hip NPART_FIXED)
 constexpr int NW = 4, ROWS = 64;      // waves, rows per workgroup (16 per wave)
 constexpr int FB = 2048;              // bytes of one split-bf16 fragment (512 slots x 4 B)
-constexpr int NSLOT = 8;              // fragments per ring stage (2 DMA'd by each wave)
-constexpr int SB = NSLOT * FB;        // 16 KiB per stage
-constexpr int GL = 4;                 // global_load_lds per wave per stage (2 fragments x hi | lo)
+constexpr int NSLOT = 16;             // fragments per ring stage (4 DMA'd by each wave)
+constexpr int SPW = NSLOT / NW;       // slots per wave: wave w DMAs slots SPW*w .. SPW*w + SPW-1
+constexpr int SB = NSLOT * FB;        // 32 KiB per stage
+constexpr int GL = 2 * SPW;           // buffer_load ... lds per wave per stage (hi | lo per fragment)
 constexpr int SST = 36;               // fp32 row stride of a [16][32] transpose tile (conflict-free)
 constexpr int TILE_F = 16 * SST;
 constexpr int P1 = 7, V1 = 32;        // fc1 output tiles held: policy <= 7 (hidden <= 112), value <= 32
@@ -58,26 +59,26 @@ constexpr int TPR = 4;                // lanes per row in the loss (16 rows x 4 
 // dL/dlog_std per row [16][32], loss terms per row [16][8]
 constexpr int WS_F = 3 * TILE_F + 16 * 32 + 16 + 16 * 32 + 16 * RS_NPART;
 
-constexpr int MAX_STEPS = 128;        // stream steps of one tile (117 at Humanoid dims)
+constexpr int MAX_STEPS = 64;         // stream steps of one tile (59 at Humanoid dims)
 
 int g_rs_enable = 0;   // A/B: default off until it beats the 32-row tile kernel (set_s3_stream)
-int g_rs_stages = 4;
+int g_rs_stages = 3;
 
 template <int S>
 constexpr size_t rs_lds_bytes() { return (size_t)S * SB + (size_t)NW * WS_F * sizeof(float); }
 
 struct Plan {
-  int ks1, kp2, kv2, k3p, k3v, kq2p, kq2v;   // k-steps: fc1, fc2 p / v, fc3 p / v, dgrad fc2 p / v
+  int ks1, k3p, k3v;                         // k-steps: fc1, fc3 p / v
   int np1, nv1, np2, nv2, nmu;               // output tiles: fc1 p / v (real), fc2 p / v, mu
-  int nd3p, nd3v, nd2p, nd2v;                // tiles of the transposed images (dgrad outputs)
-  int s_fc2p, s_fc2v, s_fc3, s_dg3, s_dg2p, s_dg2v, s_end;
+  int nd3p, nd3v, nd2p, nd2v, kq2p, kq2v;    // dgrad: tiles of the transposed images, their k-steps
+  int s_fc2, s_fc3, s_dg3, s_dg2, s_end;
 };
 
+// (the fc2 / dgrad-fc2 extents are the fixed ones mlp_rs_applies admits: 4 policy + 16 value
+// k-steps, 4 policy + 16 value output-tile pairs)
 DEV Plan make_plan(const MlpArgs& a) {
   Plan p;
   p.ks1 = a.d_in[0] >> 5;
-  p.kp2 = a.d_in[1] >> 5;
-  p.kv2 = a.d_in[4] >> 5;
   p.k3p = a.d_in[2] >> 5;
   p.k3v = a.d_in[5] >> 5;
   p.kq2p = a.d_out[1] >> 5;
@@ -91,50 +92,60 @@ DEV Plan make_plan(const MlpArgs& a) {
   p.nd3v = a.d_in[5] >> 4;
   p.nd2p = a.d_in[1] >> 4;
   p.nd2v = a.d_in[4] >> 4;
-  p.s_fc2p = 1 + 6 * p.ks1;
-  p.s_fc2v = p.s_fc2p + p.kp2;
-  p.s_fc3 = p.s_fc2v + p.kv2;
-  p.s_dg3 = p.s_fc3 + 2;
-  p.s_dg2p = p.s_dg3 + 2;
-  p.s_dg2v = p.s_dg2p + ((p.np1 + 1) >> 1);
-  p.s_end = p.s_dg2v + ((p.nv1 + 1) >> 1);
+  p.s_fc2 = 3 * p.ks1;
+  p.s_fc3 = p.s_fc2 + 10;
+  p.s_dg3 = p.s_fc3 + 1;
+  p.s_dg2 = p.s_dg3 + 1;
+  p.s_end = p.s_dg2 + 10;
   return p;
 }
 
-// Ring slot q of stream step st: element offset of a weight fragment (wave-uniform), or -1 - ks for
-// the issuing wave's own observation fragment of fc1 k-step ks.  Slots past a layer's extent
+// Ring slot q of stream step st: element offset of a weight fragment.  Slots past a layer's extent
 // re-load a valid fragment of the same layer (an L2 hit whose MFMA result is never stored).
-DEV int step_src(const MlpArgs& a, const Plan& p, int st, int q) {
+// fc1 k-step order is rotated per workgroup (rot = blockIdx % ks1).
+// Schedule (16 slots per step; wave w DMAs slots 4w..4w+3):
+//   fc1, 3/ks    fragment f = 16 sub + q (f < 7 policy tile f, else value tile f - 7, f >= 39 spare)
+//   fc2, 10      step j: fc2 k-steps i = 2j (slots 0-7) and 2j + 1 (slots 8-15), the 8 output tiles
+//                each (i < 4 policy k-step i, else value k-step i - 4)
+//   fc3, 1       slots 0-7 mu (tile q / 4, k-step q % 4), 8-11 v (k-step q % 4)
+//   dgrad fc3, 1 slots 0-7 policy, 8-15 value: the 8 output tiles (K = 32)
+//   dgrad fc2,10 step j: output-tile pairs P = 2j (slots 0-7) and 2j + 1 (8-15), tile 2P' + (q / 4 % 2),
+//                k-step q % 4 (P < 4 policy pair P' = P, else value pair P' = P - 4)
+DEV int fc1_ks(const Plan& p, int ks, int rot) {
+  const int k = ks + rot;
+  return k >= p.ks1 ? k - p.ks1 : k;
+}
+
+DEV int step_src(const MlpArgs& a, const Plan& p, int st, int q, int rot) {
   if (st >= p.s_end) st = p.s_end - 1;
-  if (st == 0) return -1 - (q & 1);
-  if (st < p.s_fc2p) {
-    const int j = st - 1, ks = j / 6, sub = j - 6 * ks;
-    int f;
-    if (sub == 0) {
-      if (q & 1) return -1 - min(ks + 2, p.ks1 - 1);
-      f = q >> 1;
-    } else {
-      f = 4 + 8 * (sub - 1) + q;
-    }
+  if (st < p.s_fc2) {
+    const int ks0 = st / 3, sub = st - 3 * ks0;
+    const int ks = fc1_ks(p, ks0, rot);
+    int f = 16 * sub + q;
     if (f < P1) return a.off_w[0] + (int)fm_frag(f < p.np1 ? f : 0, ks, a.d_in[0], 0);
     f -= P1;
     return a.off_w[3] + (int)fm_frag(f < p.nv1 ? f : 0, ks, a.d_in[3], 0);
   }
-  if (st < p.s_fc2v) return a.off_w[1] + (int)fm_frag(q < p.np2 ? q : 0, st - p.s_fc2p, a.d_in[1], 0);
-  if (st < p.s_fc3) return a.off_w[4] + (int)fm_frag(q < p.nv2 ? q : 0, st - p.s_fc2v, a.d_in[4], 0);
-  if (st == p.s_fc3) {
-    const int t = q >> 2, ks = q & 3;
-    return a.off_w[2] + (int)fm_frag(t < p.nmu ? t : 0, ks < p.k3p ? ks : 0, a.d_in[2], 0);
+  if (st < p.s_fc3) {
+    const int i = 2 * (st - p.s_fc2) + (q >> 3), t = q & 7;
+    if (i < 4) return a.off_w[1] + (int)fm_frag(t < p.np2 ? t : 0, i, a.d_in[1], 0);
+    return a.off_w[4] + (int)fm_frag(t < p.nv2 ? t : 0, i - 4, a.d_in[4], 0);
   }
-  if (st == p.s_fc3 + 1) {
+  if (st == p.s_fc3) {
+    if (q < 8) {
+      const int t = q >> 2, ks = q & 3;
+      return a.off_w[2] + (int)fm_frag(t < p.nmu ? t : 0, ks < p.k3p ? ks : 0, a.d_in[2], 0);
+    }
     const int ks = q & 3;
     return a.off_w[5] + (int)fm_frag(0, ks < p.k3v ? ks : 0, a.d_in[5], 0);
   }
-  if (st == p.s_dg3) return a.off_wt[2] + (int)fm_frag(q < p.nd3p ? q : 0, 0, a.d_out[2], 0);
-  if (st == p.s_dg3 + 1) return a.off_wt[5] + (int)fm_frag(q < p.nd3v ? q : 0, 0, a.d_out[5], 0);
-  const bool pol = st < p.s_dg2v;
-  const int j = st - (pol ? p.s_dg2p : p.s_dg2v);
-  const int t = 2 * j + (q >> 2), ks = q & 3;
+  if (st == p.s_dg3) {
+    if (q < 8) return a.off_wt[2] + (int)fm_frag(q < p.nd3p ? q : 0, 0, a.d_out[2], 0);
+    return a.off_wt[5] + (int)fm_frag(q - 8 < p.nd3v ? q - 8 : 0, 0, a.d_out[5], 0);
+  }
+  const int P = 2 * (st - p.s_dg2) + (q >> 3);
+  const bool pol = P < 4;
+  const int t = 2 * (pol ? P : P - 4) + ((q >> 2) & 1), ks = q & 3;
   const int kq = pol ? p.kq2p : p.kq2v;
   const int nt = pol ? p.nd2p : p.nd2v;
   return (pol ? a.off_wt[1] : a.off_wt[4]) +
@@ -145,16 +156,6 @@ DEV int step_src(const MlpArgs& a, const Plan& p, int st, int q) {
 DEV Frag rfrag(const char* stg, int q, int lane) {
   const char* b = stg + q * FB + lane * 16;
   return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + 1024)};
-}
-
-// all N fragments of a stage into registers before any MFMA uses them: left to itself hipcc
-// interleaves each fragment's read with its 3 MFMAs and, at one wave per SIMD, pays the LDS
-// latency once per fragment instead of once per step
-template <int N>
-DEV void rfrags(const char* stg, int lane, Frag (&b)[N]) {
-#pragma unroll
-  for (int q = 0; q < N; ++q) b[q] = rfrag(stg, q, lane);
-  __builtin_amdgcn_sched_barrier(0);
 }
 
 typedef __attribute__((ext_vector_type(8))) float f32x8;
@@ -205,13 +206,16 @@ DEV f32x4 bias_col(const f32x4& v, int c, int nb) {
   return c < nb ? v : f32x4{o, o, o, o};
 }
 
-// 4 consecutive m (rows 4lg..4lg+3 of the wave) of feature c -> the FM wgrad operand
-DEV void store_T(void* outT, const f32x4& v, int c, int m, int ldT) {
+// 4 consecutive m (rows 4lg..4lg+3 of the wave) of feature 16 t + (lane & 15) -> the FM wgrad
+// operand, from the lane's base pointer (its hi slot of feature lane & 15, row m) and the byte
+// stride tsb of one 16-feature row block:
+// fm_index(16 t + f, m, ld) = fm_index(f, m, ld) + t * (ld / 32) * 512
+DEV void store_Tt(__bf16* lane_base, int t, size_t tsb, const f32x4& v) {
   const bf16x4v hv = __builtin_convertvector(v, bf16x4v);
   const bf16x4v lv = __builtin_convertvector(v - __builtin_convertvector(hv, f32x4), bf16x4v);
-  __bf16* p = P::hi_ptr(reinterpret_cast<T*>(outT), fm_index(c, m, ldT));
+  char* p = reinterpret_cast<char*>(lane_base) + (size_t)t * tsb;
   opnd_store(*reinterpret_cast<const u32x2*>(&hv), reinterpret_cast<u32x2*>(p));
-  opnd_store(*reinterpret_cast<const u32x2*>(&lv), reinterpret_cast<u32x2*>(p + 8));
+  opnd_store(*reinterpret_cast<const u32x2*>(&lv), reinterpret_cast<u32x2*>(p + 16));
 }
 
 // 8 consecutive m (rows 8h..8h+7) of column col of a [16][ld] fp32 tile -> one 32-byte FM group
@@ -306,39 +310,56 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   const unsigned vw = (unsigned)lane * 32u;
   const unsigned vx = (unsigned)(((size_t)src_of(16 * wave + lr) * a.d_in[0] + 8 * lg) * sizeof(T));
 
-  // The stream's sources, computed once per workgroup and held in two VGPRs: lane l of cw[0] packs
-  // this wave's two slot codes of step l, cw[1] those of step 64 + l, 16 bits each — a weight
+  // The stream's sources, computed once per workgroup and held in two VGPRs: lane l of cw0 packs
+  // this wave's slot codes 4w, 4w+1 of step l, cw1 its slots 4w+2, 4w+3, 16 bits each — a weight
   // fragment index (element offset / 512), or 0x8000 | ks for this wave's X fragment of k-step
   // ks.  An issue reads its step with v_readlane: no LDS table read (which hipcc would make wait
-  // for the ring's DMA) and none of step_src's ~250 scalar instructions per step (at one wave per
+  // for the ring's DMA) and none of step_src's scalar phase arithmetic per step (at one wave per
   // SIMD every issued instruction costs the MFMA pipe ~4 cycles).
+  const int rot = (int)(blockIdx.x % (unsigned)p.ks1);
   auto code16 = [&](int st, int q) __attribute__((always_inline)) {
-    const int c = step_src(a, p, min(st, p.s_end - 1), q);
-    return (uint32_t)(c >= 0 ? (c >> 9) : (0x8000 | (-1 - c)));
+    return (uint32_t)(step_src(a, p, min(st, p.s_end - 1), q, rot) >> 9);
   };
-  const uint32_t cw0 = code16(lane, 2 * wave) | (code16(lane, 2 * wave + 1) << 16);
-  const uint32_t cw1 = code16(64 + lane, 2 * wave) | (code16(64 + lane, 2 * wave + 1) << 16);
+  const uint32_t cw0 = code16(lane, SPW * wave) | (code16(lane, SPW * wave + 1) << 16);
+  const uint32_t cw1 = code16(lane, SPW * wave + 2) | (code16(lane, SPW * wave + 3) << 16);
 
   auto issue = [&](int st, int stage) __attribute__((always_inline)) {
-    const uint32_t w0 = __builtin_amdgcn_readlane(cw0, st & 63);
-    const uint32_t w1 = __builtin_amdgcn_readlane(cw1, st & 63);
-    const uint32_t w = st < 64 ? w0 : w1;
+    const int l = min(st, MAX_STEPS - 1);
+    const uint32_t w01 = __builtin_amdgcn_readlane(cw0, l);
+    const uint32_t w23 = __builtin_amdgcn_readlane(cw1, l);
     __attribute__((address_space(3))) char* stg =
-        (__attribute__((address_space(3))) char*)(ring + stage * SB) + 2 * wave * FB;
+        (__attribute__((address_space(3))) char*)(ring + stage * SB) + SPW * wave * FB;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const uint32_t code = (w >> (16 * u)) & 0xffffu;
+    for (int u = 0; u < SPW; ++u) {
+      const uint32_t code = ((u < 2 ? w01 : w23) >> (16 * (u & 1))) & 0xffffu;
       // (the instruction's immediate offset would move the LDS destination too: the hi | lo
       // 16-byte halves differ in the SGPR offset instead)
-      if (!(code & 0x8000u)) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB, 16, vw, code * 2048u, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB + 1024, 16, vw, code * 2048u + 16u, 0, 0);
-      } else {
-        const uint32_t xo = (code & 0x7fffu) * 128u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, stg + u * FB, 16, vx, xo, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, stg + u * FB + 1024, 16, vx, xo + 16u, 0, 0);
-      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB, 16, vw, code * 2048u, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB + 1024, 16, vw, code * 2048u + 16u, 0, 0);
     }
+  };
+  // This wave's observation fragments (its 16 rows, 32 features of k-step ks) go to a private
+  // 3-slot LDS ring, DMA'd three k-steps (9 stream steps) ahead of use: a gather from HBM / the
+  // Infinity Cache outlasts the weight ring's one-stage lookahead.  The ring aliases the loss
+  // scratch (dead until fc3).
+  char* xring = reinterpret_cast<char*>(scr + TILE_F);
+  auto issue_x = [&](int ks0) __attribute__((always_inline)) {
+    const uint32_t xo = (uint32_t)fc1_ks(p, min(ks0, p.ks1 - 1), rot) * 128u;
+    __attribute__((address_space(3))) char* d = (__attribute__((address_space(3))) char*)(xring + (ks0 % 3) * FB);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d, 16, vx, xo, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d + 1024, 16, vx, xo + 16u, 0, 0);
+  };
+  // its fragment of k-step ks (the DMA landed: every vmcnt wait since covers it, in issue order);
+  // read and waited in one asm statement (a plain LDS load would wait for the ring's DMA)
+  auto read_x = [&](int ks0) __attribute__((always_inline)) {
+    const uint32_t addr =
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(xring + (ks0 % 3) * FB) + lane * 16;
+    bf16x8 h, l;
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(h), "=&v"(l)
+                 : "v"(addr)
+                 : "memory");
+    return Frag{h, l};
   };
   int cur = 0, cst = 0, ist = 0;   // next step to consume, its stage, the stage refill() fills
   // store instructions of each of the last S-2 steps: a step's stores precede its refill, so they
@@ -372,7 +393,30 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   // last thing of every step (after its reads and stores): DMA step cur + S - 2 into the stage the
   // previous step used
   auto refill = [&]() __attribute__((always_inline)) { issue(cur + S - 2, ist); };
+  // a stage's fragments [B, E) in two register halves: the second half's LDS reads are in flight
+  // while the first half's MFMAs run (left to itself hipcc reads each fragment right before its 3
+  // MFMAs and, at one wave per SIMD, exposes the LDS latency once per fragment)
+  auto for_stage = [&](const char* stg, auto bc, auto ec, auto&& f) __attribute__((always_inline)) {
+    constexpr int B = decltype(bc)::value, E = decltype(ec)::value, H = (B + E) / 2;
+    Frag b[E - B];
+    static_for<B, H>([&](auto qc) __attribute__((always_inline)) {
+      b[decltype(qc)::value - B] = rfrag(stg, decltype(qc)::value, lane);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<H, E>([&](auto qc) __attribute__((always_inline)) {
+      b[decltype(qc)::value - B] = rfrag(stg, decltype(qc)::value, lane);
+    });
+    static_for<B, H>([&](auto qc) __attribute__((always_inline)) { f(qc, b[decltype(qc)::value - B]); });
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<H, E>([&](auto qc) __attribute__((always_inline)) { f(qc, b[decltype(qc)::value - B]); });
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I12 = std::integral_constant<int, 12>;
+  using I16 = std::integral_constant<int, 16>;
   RS_STAMP(0);
+  issue_x(0);
+  issue_x(1);
+  issue_x(2);
 #pragma unroll
   for (int st = 0; st < S - 1; ++st) issue(st, st);
 
@@ -380,61 +424,73 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   f32x4 acc1[NACC1];
 #pragma unroll
   for (int t = 0; t < NACC1; ++t) acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const char* stg = wait_step(0);
-  Frag xa = rfrag(stg, 2 * wave, lane), xb = rfrag(stg, 2 * wave + 1, lane);
-  refill();
+  const char* stg;
   const bool want_xT = !a.xT_ready && (a.ablate & 1) == 0;
-  for (int ks = 0; ks < p.ks1; ++ks) {
-    stg = wait_step(0);
-    // slots 2f: weights f = 0..3; slot 2 * wave + 1: this wave's X[ks + 2]
-    Frag b0[4];
-#pragma unroll
-    for (int f = 0; f < 4; ++f) b0[f] = rfrag(stg, 2 * f, lane);
-    const Frag xc = rfrag(stg, 2 * wave + 1, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    static_for<0, 4>([&](auto fc) __attribute__((always_inline)) {
-      constexpr int f = decltype(fc)::value;
-      acc1[f] = P::mma(acc1[f], xa, b0[f]);
-    });
-    int nstx = 0;
-    if (want_xT) {
-      // the rollout did not write this call's X^T: transpose the wave's 16 x 32 block here
-      const f32x8 x = join8(xa);
-      float4* w = reinterpret_cast<float4*>(tp + lr * SST + 8 * lg);
-      w[0] = float4{x[0], x[1], x[2], x[3]};
-      w[1] = float4{x[4], x[5], x[6], x[7]};
-      store_T8(a.xT, tp, SST, lane >> 1, lane & 1, 32 * ks + (lane >> 1), mw + 8 * (lane & 1), a.ldT);
-      nstx = 2;
+  Frag xa;
+  // fc1 weight fragment f (of a k-step) -> accumulator
+  auto mma1 = [&](auto fc, const Frag& b) __attribute__((always_inline)) {
+    constexpr int f = decltype(fc)::value;
+    if constexpr (f < P1 + V1) {
+      constexpr int t = f < P1 ? f : f + 1;
+      acc1[t] = P::mma(acc1[t], xa, b);
     }
-    refill();
-    static_for<1, 6>([&](auto sc) __attribute__((always_inline)) {
+  };
+  int nstx = 0;
+  for (int ks = 0; ks < p.ks1; ++ks) {
+    // younger than the batch each wait retires (S = 3): sub 0 — the next batch only; sub 1 — sub
+    // 0's X^T stores, the next batch and the 2 X loads issued after it; sub 2 — those X loads and
+    // the next batch (the counts assume S = 3; S = 2 waits for everything)
+    static_for<0, 3>([&](auto sc) __attribute__((always_inline)) {
       constexpr int sub = decltype(sc)::value;
-      stg = wait_step(sub == 1 ? nstx : 0);
-      Frag b[NSLOT];
-      rfrags(stg, lane, b);
-      static_for<0, NSLOT>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        constexpr int f = 4 + 8 * (sub - 1) + q;
-        constexpr int t = f < P1 ? f : f + 1;
-        if constexpr (f < P1 + V1) acc1[t] = P::mma(acc1[t], xa, b[q]);
+      stg = wait_step(sub == 0 ? 0 : 2 + (sub == 1 ? nstx : 0));
+      if constexpr (sub == 0) xa = read_x(ks);
+      for_stage(stg, I0{}, I16{}, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+        mma1(std::integral_constant<int, 16 * sub + decltype(qc)::value>{}, b);
       });
-      refill();
+      if constexpr (sub == 0) {
+        nstx = 0;
+        if (want_xT) {
+          // the rollout did not write this call's X^T: transpose the wave's 16 x 32 block here
+          const f32x8 x = join8(xa);
+          float4* w = reinterpret_cast<float4*>(tp + lr * SST + 8 * lg);
+          w[0] = float4{x[0], x[1], x[2], x[3]};
+          w[1] = float4{x[4], x[5], x[6], x[7]};
+          store_T8(a.xT, tp, SST, lane >> 1, lane & 1, 32 * fc1_ks(p, ks, rot) + (lane >> 1),
+                   mw + 8 * (lane & 1), a.ldT);
+          nstx = 2;
+        }
+        refill();
+        issue_x(ks + 3);   // into the slot X[ks] just left
+      } else {
+        refill();
+      }
     });
-    xa = xb;
-    xb = xc;
   }
 
   RS_STAMP(1);
   // ---------------- fc2: h1 = tanh(fc1) chained two tiles (one k-step) at a time ----------------
-  // Software-pipelined: step i's MFMAs and step i+1's operand (tanh, the h1^T stores, the LDS
-  // transpose) share one scheduling region, so the VALU work fills the MFMA shadow.
+  // Software-pipelined: step j's MFMAs and step j+1's two operands (tanh, the h1^T stores, the
+  // LDS transposes) share one scheduling region, so the VALU work fills the MFMA shadow.
   const bool no_T = (a.ablate & 1) != 0;
   const int n1p = a.n_out[0], n1v = a.n_out[3], n2p = a.n_out[1], n2v = a.n_out[4];
   f32x4 acc2p[8], acc2v[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc2p[t] = acc2v[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int mr = mw + 4 * lg;   // first of the lane's 4 rows (C layout)
-  // operand of fc2 step i (i < 4: policy k-step i, else value k-step i - 4); returns its stores
+  // per-lane base pointers of the wgrad operands this kernel writes (feature lane & 15, row mr)
+  const size_t tsb = (size_t)a.ldT * 64;
+  auto lane_base = [&](void* buf) __attribute__((always_inline)) {
+    return P::hi_ptr(reinterpret_cast<T*>(buf), fm_index(lr, mr, a.ldT));
+  };
+  __bf16* const bh1p = lane_base(a.h1pT);
+  __bf16* const bh1v = lane_base(a.h1vT);
+  __bf16* const bh2p = lane_base(a.h2pT);
+  __bf16* const bh2v = lane_base(a.h2vT);
+  __bf16* const bg2p = lane_base(a.g2pT);
+  __bf16* const bg2v = lane_base(a.g2vT);
+  __bf16* const bg1p = lane_base(a.g1pT);
+  __bf16* const bg1v = lane_base(a.g1vT);
+  // operand of fc2 k-step i (i < 4: policy k-step i, else value k-step i - 4); returns its stores
   auto prep_h1 = [&](int i, Frag& out) __attribute__((always_inline)) -> int {
     const bool pol = i < 4;
     const int ks = pol ? i : i - 4;
@@ -446,31 +502,31 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
     const int c0 = 32 * ks + lr;
     int nst = 0;
     if (!no_T) {
-      void* oT = pol ? a.h1pT : a.h1vT;
-      if (c0 < nr) store_T(oT, h0, c0, mr, a.ldT);
-      if (c0 + 16 < nr) store_T(oT, h1, c0 + 16, mr, a.ldT);
+      __bf16* oT = pol ? bh1p : bh1v;
+      if (c0 < nr) store_Tt(oT, 2 * ks, tsb, h0);
+      if (c0 + 16 < nr) store_Tt(oT, 2 * ks + 1, tsb, h1);
       nst = (32 * ks < nr ? 2 : 0) + (32 * ks + 16 < nr ? 2 : 0);
     }
     tp_put(tp, bias_col(h0, c0, nr), bias_col(h1, c0 + 16, nr), lane);
     out = tp_getA(tp, lane);
     return nst;
   };
-  Frag ah;
-  int nst = prep_h1(0, ah);
-  static_for<0, 20>([&](auto ic) __attribute__((always_inline)) {
-    constexpr int i = decltype(ic)::value;
+  Frag ah0, ah1;
+  int nst = prep_h1(0, ah0);
+  nst += prep_h1(1, ah1);
+  static_for<0, 10>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
     stg = wait_step(nst);
-    Frag b[8];
-    rfrags(stg, lane, b);
-    if constexpr (i < 4) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc2p[q] = P::mma(acc2p[q], ah, b[q]);
+    for_stage(stg, I0{}, I16{}, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
+      constexpr int i = 2 * j + (q >> 3);
+      if constexpr (i < 4) acc2p[q & 7] = P::mma(acc2p[q & 7], q < 8 ? ah0 : ah1, b);
+      else acc2v[q & 7] = P::mma(acc2v[q & 7], q < 8 ? ah0 : ah1, b);
+    });
+    if constexpr (j + 1 < 10) {
+      nst = prep_h1(2 * j + 2, ah0);
+      nst += prep_h1(2 * j + 3, ah1);
     } else {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc2v[q] = P::mma(acc2v[q], ah, b[q]);
-    }
-    if constexpr (i + 1 < 20) nst = prep_h1(i + 1, ah);
-    if constexpr (i == 19) {
       RS_STAMP(2);
       // h2 = tanh(fc2), kept for dgrad fc3; its stores belong to this step (before the refill)
       nst = 0;
@@ -479,8 +535,8 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
         acc2p[q] = act_tanh4<DT_S3>(acc2p[q]);
         acc2v[q] = act_tanh4<DT_S3>(acc2v[q]);
         const int c = 16 * q + lr;
-        if (!no_T && c < n2p) store_T(a.h2pT, acc2p[q], c, mr, a.ldT);
-        if (!no_T && c < n2v) store_T(a.h2vT, acc2v[q], c, mr, a.ldT);
+        if (!no_T && c < n2p) store_Tt(bh2p, q, tsb, acc2p[q]);
+        if (!no_T && c < n2v) store_Tt(bh2v, q, tsb, acc2v[q]);
         if (!no_T) nst += (16 * q < n2p ? 2 : 0) + (16 * q < n2v ? 2 : 0);
       }
     }
@@ -505,42 +561,26 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   const float l_vold = !ref_loss ? a.v_old[lsrc] : 0.f;
   const float l_vprev = ref_loss ? a.v_prev[lsrc] : 0.f;
 
-  // ---------------- fc3 (mu, v) ----------------
-  Frag am[4];
+  // ---------------- fc3 (mu, v) + loss: one step ----------------
+  Frag am[4], av[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     const int c0 = 32 * ks + lr;
     tp_put(tp, bias_col(acc2p[2 * ks], c0, n2p), bias_col(acc2p[2 * ks + 1], c0 + 16, n2p), lane);
     am[ks] = tp_getA(tp, lane);
+    tp_put(tp, bias_col(acc2v[2 * ks], c0, n2v), bias_col(acc2v[2 * ks + 1], c0 + 16, n2v), lane);
+    av[ks] = tp_getA(tp, lane);
   }
   stg = wait_step(nst);
   f32x4 amu0 = f32x4{0.f, 0.f, 0.f, 0.f}, amu1 = amu0, av0 = amu0;
-  {
-    Frag b[8];
-    rfrags(stg, lane, b);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      amu0 = P::mma(amu0, am[ks], b[ks]);
-      amu1 = P::mma(amu1, am[ks], b[4 + ks]);
-    }
-  }
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const int c0 = 32 * ks + lr;
-    tp_put(tp, bias_col(acc2v[2 * ks], c0, n2v), bias_col(acc2v[2 * ks + 1], c0 + 16, n2v), lane);
-    am[ks] = tp_getA(tp, lane);
-  }
-  refill();
-  stg = wait_step(0);
-  {
-    Frag b[4];
-    rfrags(stg, lane, b);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) av0 = P::mma(av0, am[ks], b[ks]);
-  }
+  for_stage(stg, I0{}, I12{}, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    constexpr int q = decltype(qc)::value;
+    if constexpr (q < 4) amu0 = P::mma(amu0, am[q], b);
+    else if constexpr (q < 8) amu1 = P::mma(amu1, am[q - 4], b);
+    else av0 = P::mma(av0, av[q - 8], b);
+  });
 
   RS_STAMP(3);
-  // ---------------- loss + dL/d(mu, log_std, v) (inside the fc3-v step: before its refill) -------
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = 4 * lg + i;
@@ -667,78 +707,80 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   refill();   // (the loss's stores are not counted: the next S-2 waits also wait for them)
 
   RS_STAMP(4);
-  // ---------------- dgrad fc3: dpre2 = (dY W3) * (1 - h2^2) ----------------
+  // ---------------- dgrad fc3: dpre2 = (dY W3) * (1 - h2^2), both heads in one step ----------------
   Frag a2p[4], a2v[4];
-  auto dgrad3 = [&](const Frag& ad, const f32x4 (&h2)[8], int n2, void* oT, Frag (&a2)[4]) __attribute__((always_inline)) -> int {
-    f32x4 d[8];
-    Frag b[8];
-    rfrags(stg, lane, b);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) d[q] = P::mma(f32x4{0.f, 0.f, 0.f, 0.f}, ad, b[q]);
-    int n = 0;
+  {
+    const Frag adp = tp_getA(dmu, lane), adv = tp_getA(dvt, lane);
+    stg = wait_step(0);
+    f32x4 dp[8], dv[8];
+    for_stage(stg, I0{}, I16{}, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
+      if constexpr (q < 8) dp[q] = P::mma(f32x4{0.f, 0.f, 0.f, 0.f}, adp, b);
+      else dv[q - 8] = P::mma(f32x4{0.f, 0.f, 0.f, 0.f}, adv, b);
+    });
+    nst = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int c = 16 * q + lr;
-      d[q] = c < n2 ? d[q] * (1.0f - h2[q] * h2[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
-      if (!no_T && c < n2) store_T(oT, d[q], c, mr, a.ldT);
-      if (!no_T) n += 16 * q < n2 ? 2 : 0;
+      dp[q] = c < n2p ? dp[q] * (1.0f - acc2p[q] * acc2p[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[q] = c < n2v ? dv[q] * (1.0f - acc2v[q] * acc2v[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!no_T && c < n2p) store_Tt(bg2p, q, tsb, dp[q]);
+      if (!no_T && c < n2v) store_Tt(bg2v, q, tsb, dv[q]);
+      if (!no_T) nst += (16 * q < n2p ? 2 : 0) + (16 * q < n2v ? 2 : 0);
     }
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      tp_put(tp, d[2 * ks], d[2 * ks + 1], lane);
-      a2[ks] = tp_getA(tp, lane);
+      tp_put(tp, dp[2 * ks], dp[2 * ks + 1], lane);
+      a2p[ks] = tp_getA(tp, lane);
+      tp_put(tp, dv[2 * ks], dv[2 * ks + 1], lane);
+      a2v[ks] = tp_getA(tp, lane);
     }
-    return n;
-  };
-  {
-    const Frag ad = tp_getA(dmu, lane);
-    stg = wait_step(0);
-    nst = dgrad3(ad, acc2p, n2p, a.g2pT, a2p);
-    refill();
-  }
-  {
-    const Frag ad = tp_getA(dvt, lane);
-    stg = wait_step(nst);
-    nst = dgrad3(ad, acc2v, n2v, a.g2vT, a2v);
     refill();
   }
 
   RS_STAMP(5);
   // ---------------- dgrad fc2: g1 = (dpre2 W2) * (1 - h1^2), only the wgrad operand ----------------
-  // 4 policy + 16 value steps of 2 output tiles; step j's epilogue (dtanh + stores) runs in step
-  // j+1 beside its MFMAs
-  f32x4 gp0 = f32x4{0.f, 0.f, 0.f, 0.f}, gp1 = gp0;
-  auto epi_g1 = [&](int j) __attribute__((always_inline)) -> int {
-    const bool pol = j < 4;
-    const int jj = pol ? j : j - 4;
+  // 10 steps of two output-tile pairs (4 policy + 16 value pairs); step j's epilogue (dtanh +
+  // stores) runs in step j+1 beside its MFMAs
+  f32x4 gq[4];   // previous step's 4 tiles: pair 2j' tiles 0,1 and pair 2j'+1 tiles 0,1
+#pragma unroll
+  for (int u = 0; u < 4; ++u) gq[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto epi_pair = [&](int P_, const f32x4& g0, const f32x4& g1) __attribute__((always_inline)) -> int {
+    const bool pol = P_ < 4;
+    const int jj = pol ? P_ : P_ - 4;
     const int t0 = pol ? 2 * jj : 8 + 2 * jj;
     const int nr = pol ? n1p : n1v;
-    void* oT = pol ? a.g1pT : a.g1vT;
+    __bf16* oT = pol ? bg1p : bg1v;
     const int c0 = 32 * jj + lr;
-    if (c0 < nr) store_T(oT, gp0 * (1.0f - acc1[t0] * acc1[t0]), c0, mr, a.ldT);
-    if (c0 + 16 < nr) store_T(oT, gp1 * (1.0f - acc1[t0 + 1] * acc1[t0 + 1]), c0 + 16, mr, a.ldT);
+    if (c0 < nr) store_Tt(oT, 2 * jj, tsb, g0 * (1.0f - acc1[t0] * acc1[t0]));
+    if (c0 + 16 < nr) store_Tt(oT, 2 * jj + 1, tsb, g1 * (1.0f - acc1[t0 + 1] * acc1[t0 + 1]));
     return (32 * jj < nr ? 2 : 0) + (32 * jj + 16 < nr ? 2 : 0);
   };
-  static_for<0, 20>([&](auto jc) __attribute__((always_inline)) {
+  static_for<0, 10>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     stg = wait_step(nst);
-    f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
-    Frag b[8];
-    rfrags(stg, lane, b);
+    f32x4 g[4];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const Frag& a2 = j < 4 ? a2p[ks] : a2v[ks];
-      g0 = P::mma(g0, a2, b[ks]);
-      g1 = P::mma(g1, a2, b[4 + ks]);
+    for (int u = 0; u < 4; ++u) g[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for_stage(stg, I0{}, I16{}, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
+      constexpr int P_ = 2 * j + (q >> 3);
+      const Frag& a2 = P_ < 4 ? a2p[q & 3] : a2v[q & 3];
+      g[q >> 2] = P::mma(g[q >> 2], a2, b);
+    });
+    if constexpr (j > 0) {
+      nst = epi_pair(2 * j - 2, gq[0], gq[1]);
+      nst += epi_pair(2 * j - 1, gq[2], gq[3]);
+    } else {
+      nst = 0;
     }
-    if constexpr (j > 0) nst = epi_g1(j - 1);
-    else nst = 0;
-    gp0 = g0;
-    gp1 = g1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) gq[u] = g[u];
     refill();
-    if constexpr (j == 3) RS_STAMP(6);
+    if constexpr (j == 1) RS_STAMP(6);
   });
-  epi_g1(19);
+  epi_pair(18, gq[0], gq[1]);
+  epi_pair(19, gq[2], gq[3]);
   RS_STAMP(7);
 
   // ---------------- per-workgroup partials (deterministic fixed order) ----------------
@@ -782,27 +824,16 @@ extern "C" int mlp_rs_applies(const MlpArgs& a) {
          a.n_out[1] > 96 && a.n_out[4] > 96 && a.A >= 1 && a.A <= 32;
 }
 
-extern "C" size_t mlp_rs_lds_bytes() {
-  switch (g_rs_stages) {
-    case 3: return rs_lds_bytes<3>();
-    case 5: return rs_lds_bytes<5>();
-    case 6: return rs_lds_bytes<6>();
-    default: return rs_lds_bytes<4>();
-  }
-}
+extern "C" size_t mlp_rs_lds_bytes() { return g_rs_stages == 2 ? rs_lds_bytes<2>() : rs_lds_bytes<3>(); }
 
 extern "C" void launch_mlp_train_rs(const MlpArgs& a, hipStream_t s) {
-  switch (g_rs_stages) {
-    case 3: rs_launch<3>(a, s); break;
-    case 5: rs_launch<5>(a, s); break;
-    case 6: rs_launch<6>(a, s); break;
-    default: rs_launch<4>(a, s); break;
-  }
+  if (g_rs_stages == 2) rs_launch<2>(a, s);
+  else rs_launch<3>(a, s);
 }
 
 extern "C" int s3_stream_state() { return g_rs_enable ? g_rs_stages : 0; }
 
 extern "C" void set_s3_stream(int enable, int stages) {
   g_rs_enable = enable ? 1 : 0;
-  if (stages >= 3 && stages <= 6) g_rs_stages = stages;
+  if (stages == 2 || stages == 3) g_rs_stages = stages;
 }

@@ -99,11 +99,9 @@ def main():
     arms = {
         "s3w4": (waves(4), train), "s3w8": (waves(8), train),
         "wg_prop": (lambda: plan_mode(False), wgrad), "wg_aligned": (lambda: plan_mode(True), wgrad),
+        "rs2": (lambda: (ext.set_s3_stream(True, 2), eng.sync_tile()), train),
         "rs3": (lambda: (ext.set_s3_stream(True, 3), eng.sync_tile()), train),
-        "rs4": (lambda: (ext.set_s3_stream(True, 4), eng.sync_tile()), train),
-        "rs5": (lambda: (ext.set_s3_stream(True, 5), eng.sync_tile()), train),
-        "rs6": (lambda: (ext.set_s3_stream(True, 6), eng.sync_tile()), train),
-        "tile32": (lambda: (ext.set_s3_stream(False, 4), eng.sync_tile()), train),
+        "tile32": (lambda: (ext.set_s3_stream(False, 3), eng.sync_tile()), train),
         "trainA": (lambda: use_ext("A"), lambda: train_with(ext_a)),
         "trainB": (lambda: use_ext("b"), lambda: train_with(variants["b"])),
         "valA": (lambda: use_ext("A"), eng.values), "valB": (lambda: use_ext("b"), eng.values),
@@ -128,7 +126,7 @@ def main():
             setup()
             res[k].append(timed(fn))
     use_ext("A")
-    ext.set_s3_stream(state > 0, state or 4)
+    ext.set_s3_stream(state > 0, state or 3)
     eng.sync_tile()
     plan_mode(False)
     ext.set_s3_train_waves(8)

@@ -46,9 +46,11 @@ def main():
     ext = eng.ext
     out = {}
     for rows in [int(r) for r in os.environ.get("TIMELINE_ROWS", "64,32").split(",")]:
-        ext.set_mlp_rows(rows)      # 0: the default kernel (split-bf16: the streaming kernel)
-        eng.sync_tile()
+        ext.set_mlp_rows(rows)      # 0: split-bf16 -> the streaming kernel (mlp_stream.hip)
         rs = rows == 0
+        if rs:
+            ext.set_s3_stream(True, int(os.environ.get("TIMELINE_RS_STAGES", "3")))
+        eng.sync_tile()
         rows = eng.train_rows
         phases = PHASES_RS if rs else PHASES
         nph = len(phases)
@@ -96,6 +98,8 @@ def main():
         res["start_rel_cycles_by_round"] = {int(r_): [float(v) for v in rel[rnd == r_].quantile(
             torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64))] for r_ in sorted(set(rnd.tolist()))}
         out[("rs" if rs else "rows") + str(rows)] = res
+        if rs:
+            ext.set_s3_stream(False, 3)
     ext.set_mlp_rows(0)
     # rollout: per-wave cycles per phase summed over the T steps, median over workgroups
     nblk = (eng.E + 15) // 16
