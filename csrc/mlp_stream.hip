@@ -61,7 +61,9 @@ constexpr int WS_F = 3 * TILE_F + 16 * 32 + 16 + 16 * 32 + 16 * RS_NPART;
 
 constexpr int MAX_STEPS = 64;         // stream steps of one tile (59 at Humanoid dims)
 
-int g_rs_enable = 0;   // A/B: default off until it beats the 32-row tile kernel (set_s3_stream)
+// default on: whole iteration 5.34 vs 5.51 ms for the 32-row tile kernel (scripts/ab_iter.py
+// rs,tile, same box); set_s3_stream(False, ...) selects the tile kernel (A/B)
+int g_rs_enable = 1;
 int g_rs_stages = 3;
 
 template <int S>
@@ -323,7 +325,9 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   const uint32_t cw0 = code16(lane, SPW * wave) | (code16(lane, SPW * wave + 1) << 16);
   const uint32_t cw1 = code16(lane, SPW * wave + 2) | (code16(lane, SPW * wave + 3) << 16);
 
+  const bool abl_dma = (a.ablate & 2) != 0;   // diagnostics only (phase_timeline TIMELINE_ABLATE=2)
   auto issue = [&](int st, int stage) __attribute__((always_inline)) {
+    if (abl_dma) return;
     const int l = min(st, MAX_STEPS - 1);
     const uint32_t w01 = __builtin_amdgcn_readlane(cw0, l);
     const uint32_t w23 = __builtin_amdgcn_readlane(cw1, l);
@@ -344,6 +348,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   // scratch (dead until fc3).
   char* xring = reinterpret_cast<char*>(scr + TILE_F);
   auto issue_x = [&](int ks0) __attribute__((always_inline)) {
+    if (abl_dma) return;
     const uint32_t xo = (uint32_t)fc1_ks(p, min(ks0, p.ks1 - 1), rot) * 128u;
     __attribute__((address_space(3))) char* d = (__attribute__((address_space(3))) char*)(xring + (ks0 % 3) * FB);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d, 16, vx, xo, 0, 0);
