@@ -102,8 +102,9 @@ DEV Plan make_plan(const MlpArgs& a) {
   return p;
 }
 
-// Ring slot q of stream step st: element offset of a weight fragment.  Slots past a layer's extent
-// re-load a valid fragment of the same layer (an L2 hit whose MFMA result is never stored).
+// Ring slot q of stream step st: element offset of a weight fragment, or -1 for a slot no MFMA
+// reads (output tiles that are pure padding at the shapes mlp_rs_applies admits: fc1 f >= 39,
+// the 8th output tile of fc2 / dgrad fc3 / policy dgrad fc2, fc3 slots 12-15).
 // fc1 k-step order is rotated per workgroup (rot = blockIdx % ks1).
 // Schedule (16 slots per step; wave w DMAs slots 4w..4w+3):
 //   fc1, 3/ks    fragment f = 16 sub + q (f < 7 policy tile f, else value tile f - 7, f >= 39 spare)
@@ -124,12 +125,14 @@ DEV int step_src(const MlpArgs& a, const Plan& p, int st, int q, int rot) {
     const int ks0 = st / 3, sub = st - 3 * ks0;
     const int ks = fc1_ks(p, ks0, rot);
     int f = 16 * sub + q;
+    if (f >= P1 + V1) return -1;
     if (f < P1) return a.off_w[0] + (int)fm_frag(f < p.np1 ? f : 0, ks, a.d_in[0], 0);
     f -= P1;
     return a.off_w[3] + (int)fm_frag(f < p.nv1 ? f : 0, ks, a.d_in[3], 0);
   }
   if (st < p.s_fc3) {
     const int i = 2 * (st - p.s_fc2) + (q >> 3), t = q & 7;
+    if (t == 7) return -1;   // output tile 7 (features 112-127) is padding
     if (i < 4) return a.off_w[1] + (int)fm_frag(t < p.np2 ? t : 0, i, a.d_in[1], 0);
     return a.off_w[4] + (int)fm_frag(t < p.nv2 ? t : 0, i - 4, a.d_in[4], 0);
   }
@@ -138,16 +141,19 @@ DEV int step_src(const MlpArgs& a, const Plan& p, int st, int q, int rot) {
       const int t = q >> 2, ks = q & 3;
       return a.off_w[2] + (int)fm_frag(t < p.nmu ? t : 0, ks < p.k3p ? ks : 0, a.d_in[2], 0);
     }
+    if (q >= 12) return -1;
     const int ks = q & 3;
     return a.off_w[5] + (int)fm_frag(0, ks < p.k3v ? ks : 0, a.d_in[5], 0);
   }
   if (st == p.s_dg3) {
+    if ((q & 7) == 7) return -1;
     if (q < 8) return a.off_wt[2] + (int)fm_frag(q < p.nd3p ? q : 0, 0, a.d_out[2], 0);
     return a.off_wt[5] + (int)fm_frag(q - 8 < p.nd3v ? q - 8 : 0, 0, a.d_out[5], 0);
   }
   const int P = 2 * (st - p.s_dg2) + (q >> 3);
   const bool pol = P < 4;
   const int t = 2 * (pol ? P : P - 4) + ((q >> 2) & 1), ks = q & 3;
+  if (pol && t == 7) return -1;
   const int kq = pol ? p.kq2p : p.kq2v;
   const int nt = pol ? p.nd2p : p.nd2v;
   return (pol ? a.off_wt[1] : a.off_wt[4]) +
@@ -235,15 +241,15 @@ DEV void store_T8(void* outT, const float* tile, int ld, int col, int h, int fea
 // s_waitcnt vmcnt(BASE + extra): vector-memory operations retire in issue order (loads, stores
 // and LDS-DMA together, MI355X_MICROARCH.md §Per-instruction cycle constants), so a wait for the
 // DMA batch of step `cur` may leave outstanding every younger operation: the S-2 later batches
-// AND the `extra` stores this wave issued since its last batch.  Undercounting `extra` is safe
-// (the wait is longer), overcounting is not — callers pass exact counts or 0.
+// (BASE) AND the `extra` stores / X loads issued since.  Undercounting `extra` is safe (the wait
+// is longer), overcounting is not.
 template <int BASE, int E = 0>
-DEV void wait_batch(int extra) {
+DEV void wait_vm(int extra) {
   if constexpr (E >= 20 || BASE + E >= 63) {
     WAIT_VMCNT(BASE + E);
   } else {
     if (extra <= E) WAIT_VMCNT(BASE + E);
-    else wait_batch<BASE, E + 1>(extra);
+    else wait_vm<BASE, E + 1>(extra);
   }
 }
 
@@ -264,6 +270,32 @@ DEV void static_for(F&& f) {
     f(std::integral_constant<int, B>{});
     static_for<B + 1, E>(f);
   }
+}
+
+// A stage's fragments q in [0, N) with bit q of MASK set, in two register halves: the second
+// half's LDS reads are in flight while the first half's MFMAs run (left to itself hipcc reads each
+// fragment right before its 3 MFMAs and, at one wave per SIMD, exposes the LDS latency once per
+// fragment).  f(integral_constant<q>, fragment).
+template <unsigned MASK, int N, typename F>
+DEV void for_stage(const char* stg, int lane, F&& f) {
+  constexpr int H = N / 2;
+  Frag b[N];
+  static_for<0, H>([&](auto qc) __attribute__((always_inline)) {
+    constexpr int q = decltype(qc)::value;
+    if constexpr ((MASK >> q) & 1u) b[q] = rfrag(stg, q, lane);
+  });
+  __builtin_amdgcn_sched_barrier(0);
+  static_for<H, N>([&](auto qc) __attribute__((always_inline)) {
+    constexpr int q = decltype(qc)::value;
+    if constexpr ((MASK >> q) & 1u) b[q] = rfrag(stg, q, lane);
+  });
+  static_for<0, H>([&](auto qc) __attribute__((always_inline)) {
+    if constexpr ((MASK >> decltype(qc)::value) & 1u) f(qc, b[decltype(qc)::value]);
+  });
+  __builtin_amdgcn_sched_barrier(0);
+  static_for<H, N>([&](auto qc) __attribute__((always_inline)) {
+    if constexpr ((MASK >> decltype(qc)::value) & 1u) f(qc, b[decltype(qc)::value]);
+  });
 }
 
 template <int G>
@@ -320,7 +352,13 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   // SIMD every issued instruction costs the MFMA pipe ~4 cycles).
   const int rot = (int)(blockIdx.x % (unsigned)p.ks1);
   auto code16 = [&](int st, int q) __attribute__((always_inline)) {
-    return (uint32_t)(step_src(a, p, min(st, p.s_end - 1), q, rot) >> 9);
+    // a slot no MFMA reads re-loads the step's slot 0 (every wave then issues the same number of
+    // DMAs per step, so the vmcnt counts are compile-time; skipping them measured slower: 297.5
+    // vs 277.9 us, the per-wave runtime wait counts and the uneven batches cost more than the
+    // saved L2 reads)
+    int c = step_src(a, p, min(st, p.s_end - 1), q, rot);
+    if (c < 0) c = step_src(a, p, min(st, p.s_end - 1), 0, rot);
+    return (uint32_t)(c >> 9);
   };
   const uint32_t cw0 = code16(lane, SPW * wave) | (code16(lane, SPW * wave + 1) << 16);
   const uint32_t cw1 = code16(lane, SPW * wave + 2) | (code16(lane, SPW * wave + 3) << 16);
@@ -385,7 +423,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
     int extra = 0;
 #pragma unroll
     for (int i = 0; i < NH; ++i) extra += hist[i];
-    wait_batch<GL * (S - 2)>(S > 2 ? extra : 0);
+    wait_vm<GL * (S - 2)>(S > 2 ? extra : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -398,26 +436,6 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   // last thing of every step (after its reads and stores): DMA step cur + S - 2 into the stage the
   // previous step used
   auto refill = [&]() __attribute__((always_inline)) { issue(cur + S - 2, ist); };
-  // a stage's fragments [B, E) in two register halves: the second half's LDS reads are in flight
-  // while the first half's MFMAs run (left to itself hipcc reads each fragment right before its 3
-  // MFMAs and, at one wave per SIMD, exposes the LDS latency once per fragment)
-  auto for_stage = [&](const char* stg, auto bc, auto ec, auto&& f) __attribute__((always_inline)) {
-    constexpr int B = decltype(bc)::value, E = decltype(ec)::value, H = (B + E) / 2;
-    Frag b[E - B];
-    static_for<B, H>([&](auto qc) __attribute__((always_inline)) {
-      b[decltype(qc)::value - B] = rfrag(stg, decltype(qc)::value, lane);
-    });
-    __builtin_amdgcn_sched_barrier(0);
-    static_for<H, E>([&](auto qc) __attribute__((always_inline)) {
-      b[decltype(qc)::value - B] = rfrag(stg, decltype(qc)::value, lane);
-    });
-    static_for<B, H>([&](auto qc) __attribute__((always_inline)) { f(qc, b[decltype(qc)::value - B]); });
-    __builtin_amdgcn_sched_barrier(0);
-    static_for<H, E>([&](auto qc) __attribute__((always_inline)) { f(qc, b[decltype(qc)::value - B]); });
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I12 = std::integral_constant<int, 12>;
-  using I16 = std::integral_constant<int, 16>;
   RS_STAMP(0);
   issue_x(0);
   issue_x(1);
@@ -449,7 +467,9 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
       constexpr int sub = decltype(sc)::value;
       stg = wait_step(sub == 0 ? 0 : 2 + (sub == 1 ? nstx : 0));
       if constexpr (sub == 0) xa = read_x(ks);
-      for_stage(stg, I0{}, I16{}, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      // (sub 2: fragments f = 32..38 only; f >= 39 are not DMA'd)
+      constexpr unsigned M1 = sub == 2 ? ((1u << (P1 + V1 - 32)) - 1u) : 0xffffu;
+      for_stage<M1, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
         mma1(std::integral_constant<int, 16 * sub + decltype(qc)::value>{}, b);
       });
       if constexpr (sub == 0) {
@@ -522,7 +542,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   static_for<0, 10>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     stg = wait_step(nst);
-    for_stage(stg, I0{}, I16{}, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    for_stage<0x7f7fu, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
       constexpr int i = 2 * j + (q >> 3);
       if constexpr (i < 4) acc2p[q & 7] = P::mma(acc2p[q & 7], q < 8 ? ah0 : ah1, b);
@@ -578,7 +598,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   }
   stg = wait_step(nst);
   f32x4 amu0 = f32x4{0.f, 0.f, 0.f, 0.f}, amu1 = amu0, av0 = amu0;
-  for_stage(stg, I0{}, I12{}, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+  for_stage<0x0fffu, 12>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
     constexpr int q = decltype(qc)::value;
     if constexpr (q < 4) amu0 = P::mma(amu0, am[q], b);
     else if constexpr (q < 8) amu1 = P::mma(amu1, am[q - 4], b);
@@ -718,7 +738,9 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
     const Frag adp = tp_getA(dmu, lane), adv = tp_getA(dvt, lane);
     stg = wait_step(0);
     f32x4 dp[8], dv[8];
-    for_stage(stg, I0{}, I16{}, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dp[q] = dv[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for_stage<0x7f7fu, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
       if constexpr (q < 8) dp[q] = P::mma(f32x4{0.f, 0.f, 0.f, 0.f}, adp, b);
       else dv[q - 8] = P::mma(f32x4{0.f, 0.f, 0.f, 0.f}, adv, b);
@@ -767,7 +789,8 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
     f32x4 g[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) g[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for_stage(stg, I0{}, I16{}, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    constexpr unsigned M2 = j == 1 ? 0x0fffu : 0xffffu;   // policy pair 3's tile 7 is padding
+    for_stage<M2, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
       constexpr int P_ = 2 * j + (q >> 3);
       const Frag& a2 = P_ < 4 ? a2p[q & 3] : a2v[q & 3];
@@ -818,15 +841,15 @@ void rs_launch(const MlpArgs& a, hipStream_t s) {
 }  // namespace
 
 // shapes the streaming kernel covers: its register tiles and unrolled step bodies are those of
-// the reference network (policy 100-100, value 500-100, hidden widths 97-112 / 481-511 / 97-127
-// give the same tile counts), any observation width <= 383 and action width <= 32; every other
+// the reference network (policy 100-100, value 500-100; hidden widths 97-112 / 497-511 / 97-112
+// give the same tile counts and padding tiles), any observation width <= 383 and action width <= 32; every other
 // shape runs the 32-row tile kernel
 extern "C" int mlp_rs_applies(const MlpArgs& a) {
   if (!g_rs_enable) return 0;
   return a.d_in[0] <= 384 && a.d_in[0] == a.d_in[3] && (a.n_out[0] + 15) / 16 == P1 &&
          (a.n_out[3] + 15) / 16 == V1 && a.d_in[1] == 128 && a.d_in[4] == 512 && a.d_in[2] == 128 &&
          a.d_in[5] == 128 && a.d_out[1] == 128 && a.d_out[4] == 128 && a.d_out[2] == 32 && a.d_out[5] == 32 &&
-         a.n_out[1] > 96 && a.n_out[4] > 96 && a.A >= 1 && a.A <= 32;
+         a.n_out[1] > 96 && a.n_out[1] <= 112 && a.n_out[4] > 96 && a.n_out[4] <= 112 && a.A >= 1 && a.A <= 32;
 }
 
 extern "C" size_t mlp_rs_lds_bytes() { return g_rs_stages == 2 ? rs_lds_bytes<2>() : rs_lds_bytes<3>(); }
