@@ -55,9 +55,12 @@ constexpr int P1 = 7, V1 = 32;        // fc1 output tiles held: policy <= 7 (hid
 constexpr int NACC1 = 8 + V1;         // acc1[t] policy tile t (t = 7 stays 0), acc1[8 + t] value tile t
 constexpr int JMAX = 8;               // action dims per lane held in registers (A <= 4 * JMAX)
 constexpr int TPR = 4;                // lanes per row in the loss (16 rows x 4 = 64 lanes)
-// per-wave scratch (floats): transpose tile, dL/dmu tile, dL/dv tile, mu [16][32], v [16],
-// dL/dlog_std per row [16][32], loss terms per row [16][8]
-constexpr int WS_F = 3 * TILE_F + 16 * 32 + 16 + 16 * 32 + 16 * RS_NPART;
+// per-wave scratch (floats): the transpose tile (also mu [16][32] | v [16] in the loss), then a
+// region holding the 2-slot observation ring during fc1 and, from the loss on, dL/dmu [16][SST]
+// (dL/dv in its column 32) and the wave's partial sums [8 loss terms | 32 dlog_std]
+constexpr int XR_F = 2 * FB / 4;
+constexpr int WS_F = TILE_F + XR_F;
+static_assert(TILE_F + 40 <= XR_F + TILE_F && 16 * 32 + 16 <= TILE_F, "scratch aliasing");
 
 constexpr int MAX_STEPS = 64;         // stream steps of one tile (59 at Humanoid dims)
 
@@ -298,6 +301,16 @@ DEV void for_stage(const char* stg, int lane, F&& f) {
   });
 }
 
+// sum over the 16 lanes with the same lane & 3 (the wave's 16 rows in the loss layout), the same
+// value in every one of them, fixed order: DPP row rotations by 4 and 8 inside each 16-lane row,
+// then two cross-row exchanges
+DEV float rowsum16(float x) {
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x124, 0xf, 0xf, true));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128, 0xf, 0xf, true));
+  x += __shfl_xor(x, 16, 64);
+  return x + __shfl_xor(x, 32, 64);
+}
+
 template <int G>
 DEV float gsum(float x) {
 #pragma unroll
@@ -317,12 +330,10 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   char* ring = smem;
   float* scr = reinterpret_cast<float*>(smem + (size_t)S * SB) + wave * WS_F;
   float* tp = scr;
-  float* dmu = scr + TILE_F;
-  float* dvt = scr + 2 * TILE_F;
-  float* mus = scr + 3 * TILE_F;
-  float* vs = mus + 16 * 32;
-  float* dls = vs + 16;
-  float* lss = dls + 16 * 32;
+  float* mus = tp;                // (loss only)
+  float* vs = tp + 16 * 32;       // (loss only)
+  float* dmu = scr + TILE_F;      // (after fc1: aliases the observation ring)
+  float* wpart = dmu + TILE_F;
 
   // source row of tile row r (rows past M re-read row m0: finite data, zero gradient)
   auto src_of = [&](int r) __attribute__((always_inline)) {
@@ -381,14 +392,14 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
     }
   };
   // This wave's observation fragments (its 16 rows, 32 features of k-step ks) go to a private
-  // 3-slot LDS ring, DMA'd three k-steps (9 stream steps) ahead of use: a gather from HBM / the
-  // Infinity Cache outlasts the weight ring's one-stage lookahead.  The ring aliases the loss
-  // scratch (dead until fc3).
+  // 2-slot LDS ring, DMA'd two k-steps (6 stream steps) ahead of use: a gather from HBM / the
+  // Infinity Cache outlasts the weight ring's lookahead.  The ring aliases the loss scratch
+  // (dead until fc3).
   char* xring = reinterpret_cast<char*>(scr + TILE_F);
   auto issue_x = [&](int ks0) __attribute__((always_inline)) {
     if (abl_dma) return;
     const uint32_t xo = (uint32_t)fc1_ks(p, min(ks0, p.ks1 - 1), rot) * 128u;
-    __attribute__((address_space(3))) char* d = (__attribute__((address_space(3))) char*)(xring + (ks0 % 3) * FB);
+    __attribute__((address_space(3))) char* d = (__attribute__((address_space(3))) char*)(xring + (ks0 & 1) * FB);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d, 16, vx, xo, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d + 1024, 16, vx, xo + 16u, 0, 0);
   };
@@ -396,7 +407,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   // read and waited in one asm statement (a plain LDS load would wait for the ring's DMA)
   auto read_x = [&](int ks0) __attribute__((always_inline)) {
     const uint32_t addr =
-        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(xring + (ks0 % 3) * FB) + lane * 16;
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(xring + (ks0 & 1) * FB) + lane * 16;
     bf16x8 h, l;
     asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
                  : "=&v"(h), "=&v"(l)
@@ -405,25 +416,36 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
     return Frag{h, l};
   };
   int cur = 0, cst = 0, ist = 0;   // next step to consume, its stage, the stage refill() fills
-  // store instructions of each of the last S-2 steps: a step's stores precede its refill, so they
-  // are younger than the batch of every step up to S-2 later (and older than later batches)
-  constexpr int NH = S - 2 > 0 ? S - 2 : 1;
-  int hist[NH];
+  // Younger-than-the-waited-batch bookkeeping.  A step's stores precede its refill, so they are
+  // younger than the batches of the next S-2 steps; the X loads follow the refill, so they are
+  // younger than the next S-1 steps' batches (and every report made at a wait after the previous
+  // step's refill stays younger for that many waits).
+  constexpr int NH = S - 2 > 0 ? S - 2 : 1, NX = S - 1;
+  int hist[NH], xhist[NX];
 #pragma unroll
   for (int i = 0; i < NH; ++i) hist[i] = 0;
+#pragma unroll
+  for (int i = 0; i < NX; ++i) xhist[i] = 0;
   // Ring sync for step `cur`: this wave's DMAs of it by count (every younger vector-memory
-  // operation may stay in flight: the S-2 later batches and the last S-2 steps' stores), every
-  // wave's by the barrier, which also retires every wave's reads of the stage refill() refills.
-  // `stores` = store instructions of the previous step (undercounting is safe, overcounting not).
-  auto wait_step = [&](int stores) __attribute__((always_inline)) -> const char* {
+  // operation may stay in flight), every wave's by the barrier, which also retires every wave's
+  // reads of the stage refill() refills.  `stores` / `xs` = store / X-load instructions issued
+  // during the previous step (undercounting is safe, overcounting is not).
+  auto wait_step = [&](int stores, int xs = 0) __attribute__((always_inline)) -> const char* {
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = NH - 1; i > 0; --i) hist[i] = hist[i - 1];
     hist[0] = stores;
-    int extra = 0;
 #pragma unroll
-    for (int i = 0; i < NH; ++i) extra += hist[i];
-    wait_vm<GL * (S - 2)>(S > 2 ? extra : 0);
+    for (int i = NX - 1; i > 0; --i) xhist[i] = xhist[i - 1];
+    xhist[0] = xs;
+    int extra = 0;
+    if constexpr (S > 2) {
+#pragma unroll
+      for (int i = 0; i < NH; ++i) extra += hist[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) extra += xhist[i];
+    wait_vm<GL * (S - 2)>(extra);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -439,7 +461,6 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   RS_STAMP(0);
   issue_x(0);
   issue_x(1);
-  issue_x(2);
 #pragma unroll
   for (int st = 0; st < S - 1; ++st) issue(st, st);
 
@@ -460,12 +481,10 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   };
   int nstx = 0;
   for (int ks = 0; ks < p.ks1; ++ks) {
-    // younger than the batch each wait retires (S = 3): sub 0 — the next batch only; sub 1 — sub
-    // 0's X^T stores, the next batch and the 2 X loads issued after it; sub 2 — those X loads and
-    // the next batch (the counts assume S = 3; S = 2 waits for everything)
+    // (sub 0 issues the X^T stores, if any, and — after its refill — the 2 X loads of ks + 2)
     static_for<0, 3>([&](auto sc) __attribute__((always_inline)) {
       constexpr int sub = decltype(sc)::value;
-      stg = wait_step(sub == 0 ? 0 : 2 + (sub == 1 ? nstx : 0));
+      stg = sub == 1 ? wait_step(nstx, 2) : wait_step(0);
       if constexpr (sub == 0) xa = read_x(ks);
       // (sub 2: fragments f = 32..38 only; f >= 39 are not DMA'd)
       constexpr unsigned M1 = sub == 2 ? ((1u << (P1 + V1 - 32)) - 1u) : 0xffffu;
@@ -485,7 +504,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
           nstx = 2;
         }
         refill();
-        issue_x(ks + 3);   // into the slot X[ks] just left
+        issue_x(ks + 2);   // into the slot X[ks] just left
       } else {
         refill();
       }
@@ -614,11 +633,17 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
     if (lr == 0) vs[r] = av0[i];
   }
   {
-    // zero the dL/dmu and dL/dv tiles (columns >= A / >= 1 are the padded K of dgrad fc3)
+    // zero the dL/dmu tile (columns >= A are the padded K of dgrad fc3; column 32 takes dL/dv)
     float4* z0 = reinterpret_cast<float4*>(dmu + lr * SST + 8 * lg);
-    float4* z1 = reinterpret_cast<float4*>(dvt + lr * SST + 8 * lg);
-    z0[0] = z0[1] = z1[0] = z1[1] = float4{0.f, 0.f, 0.f, 0.f};
+    z0[0] = z0[1] = float4{0.f, 0.f, 0.f, 0.f};
   }
+  // per-lane dL/dlog_std (j = lsub + 4q) and, in the lsub == 0 lanes, the row's loss terms: summed
+  // over the wave's 16 rows by a fixed xor tree after the loss (deterministic)
+  float dlsv[JMAX], lt[6];
+#pragma unroll
+  for (int q = 0; q < JMAX; ++q) dlsv[q] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) lt[k] = 0.f;
   {
     const int r = lrow, sub = lsub, src = lsrc;
     const bool valid = lvalid;
@@ -657,7 +682,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
         const float z = (actv[q] - mus[r * 32 + j]) * isig;
         dmu[r * SST + j] = valid ? dlogp * z * isig : 0.f;
         // d/dlog_std: logp term + entropy bonus (-ent_coeff * sum_j log sigma_j)
-        dls[r * 32 + j] = valid ? (dlogp * (z * z - 1.f) - a.ent_coeff) * cvar : 0.f;
+        dlsv[q] = valid ? (dlogp * (z * z - 1.f) - a.ent_coeff) * cvar : 0.f;
         lent += -a.ent_coeff * (0.5f + 0.5f * RS_LOG_2PI + lsig);
       }
       lent = gsum<TPR>(lent);
@@ -687,7 +712,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
         lent += -a.ent_coeff * pd * lgp * invA;
         dp += -a.ent_coeff * invA * (lgp + pd / (pd + 1e-5f));
         dmu[r * SST + j] = valid ? dp * pd * (x - mu) / var : 0.f;
-        dls[r * 32 + j] = valid ? dp * pd * ((x - mu) * (x - mu) / (2.f * var) - 0.5f) : 0.f;
+        dlsv[q] = valid ? dp * pd * ((x - mu) * (x - mu) / (2.f * var) - 0.5f) : 0.f;
         cf += (fabsf(ratio - 1.f) > a.clip) ? invA : 0.f;
         if (valid) a.mu_prev[(size_t)src * A + j] = mu;   // train.py:164 model_old <- model
       }
@@ -716,17 +741,31 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
         else dv = 0.5f * d1 + 0.5f * d2 * inr;
       }
       if (a.loss_kind != 0 && valid) a.v_prev[src] = v;
-      dvt[r * SST] = valid ? dv : 0.f;
-      float* lrw = lss + r * RS_NPART;
+      dmu[r * SST + 32] = valid ? dv : 0.f;
       const float vm = valid ? 1.f : 0.f;
-      lrw[0] = lclip * vm; lrw[1] = lv * vm; lrw[2] = lent * vm; lrw[3] = kl * vm; lrw[4] = cf * vm;
-      lrw[5] = vm; lrw[6] = 0.f; lrw[7] = 0.f;
+      lt[0] = lclip * vm; lt[1] = lv * vm; lt[2] = lent * vm; lt[3] = kl * vm; lt[4] = cf * vm; lt[5] = vm;
     }
   }
-  // dY^T of the output layers: item = (feature, 8-row half) of this wave's 16 rows
+  // the wave's partial sums over its 16 rows (lanes lsub + 4r)
+#pragma unroll
+  for (int q = 0; q < JMAX; ++q) dlsv[q] = rowsum16(dlsv[q]);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) lt[k] = rowsum16(lt[k]);
+  if (lane < TPR) {
+#pragma unroll
+    for (int q = 0; q < JMAX; ++q)
+      if (lane + TPR * q < A) wpart[RS_NPART + lane + TPR * q] = dlsv[q];
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) wpart[k] = lt[k];
+      wpart[6] = wpart[7] = 0.f;
+    }
+  }
+  // dY^T of the output layers: item = (feature, 8-row half) of this wave's 16 rows (dL/dv is
+  // column 32 of the dL/dmu tile)
   for (int it = lane; it < 2 * A + 2; it += 64) {
     if (it < 2 * A) store_T8(a.g3pT, dmu, SST, it >> 1, it & 1, it >> 1, mw + 8 * (it & 1), a.ldT);
-    else store_T8(a.g3vT, dvt, SST, 0, it - 2 * A, 0, mw + 8 * (it - 2 * A), a.ldT);
+    else store_T8(a.g3vT, dmu, SST, 32, it - 2 * A, 0, mw + 8 * (it - 2 * A), a.ldT);
   }
 
   refill();   // (the loss's stores are not counted: the next S-2 waits also wait for them)
@@ -735,7 +774,15 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   // ---------------- dgrad fc3: dpre2 = (dY W3) * (1 - h2^2), both heads in one step ----------------
   Frag a2p[4], a2v[4];
   {
-    const Frag adp = tp_getA(dmu, lane), adv = tp_getA(dvt, lane);
+    // dL/dv as the A operand of the value head's dgrad: K = 32 with only k = 0 nonzero
+    const Frag adp = tp_getA(dmu, lane);
+    float dvv;
+    {
+      const uint32_t addr =
+          (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(dmu + lr * SST + 32);
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(dvv) : "v"(addr) : "memory");
+    }
+    const Frag adv = split8(f32x8{lg == 0 ? dvv : 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
     stg = wait_step(0);
     f32x4 dp[8], dv[8];
 #pragma unroll
@@ -817,14 +864,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   const float* sc0 = reinterpret_cast<const float*>(smem + (size_t)S * SB);
   for (int q = tid; q < RS_NPART + A; q += NW * 64) {
     float s = 0.f;
-    for (int w = 0; w < NW; ++w) {
-      const float* b = sc0 + w * WS_F + 3 * TILE_F + 16 * 32 + 16;   // dls of wave w
-      if (q < RS_NPART) {
-        for (int r = 0; r < 16; ++r) s += b[16 * 32 + r * RS_NPART + q];
-      } else {
-        for (int r = 0; r < 16; ++r) s += b[r * 32 + q - RS_NPART];
-      }
-    }
+    for (int w = 0; w < NW; ++w) s += sc0[w * WS_F + 2 * TILE_F + q];   // wpart of wave w
     a.part[(size_t)blockIdx.x * a.npart + q] = s;
   }
 }
@@ -852,16 +892,20 @@ extern "C" int mlp_rs_applies(const MlpArgs& a) {
          a.n_out[1] > 96 && a.n_out[1] <= 112 && a.n_out[4] > 96 && a.n_out[4] <= 112 && a.A >= 1 && a.A <= 32;
 }
 
-extern "C" size_t mlp_rs_lds_bytes() { return g_rs_stages == 2 ? rs_lds_bytes<2>() : rs_lds_bytes<3>(); }
+extern "C" size_t mlp_rs_lds_bytes() {
+  return g_rs_stages == 2 ? rs_lds_bytes<2>() : g_rs_stages == 3 ? rs_lds_bytes<3>() : rs_lds_bytes<4>();
+}
+static_assert(rs_lds_bytes<4>() <= 160 * 1024, "4-stage ring must fit LDS");
 
 extern "C" void launch_mlp_train_rs(const MlpArgs& a, hipStream_t s) {
   if (g_rs_stages == 2) rs_launch<2>(a, s);
-  else rs_launch<3>(a, s);
+  else if (g_rs_stages == 3) rs_launch<3>(a, s);
+  else rs_launch<4>(a, s);
 }
 
 extern "C" int s3_stream_state() { return g_rs_enable ? g_rs_stages : 0; }
 
 extern "C" void set_s3_stream(int enable, int stages) {
   g_rs_enable = enable ? 1 : 0;
-  if (stages == 2 || stages == 3) g_rs_stages = stages;
+  if (stages >= 2 && stages <= 4) g_rs_stages = stages;
 }
