@@ -586,7 +586,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("s3_stream_state", []() { return (int64_t)s3_stream_state(); });
   m.def("set_s3_stream", [](bool enable, int64_t stages) {
-    TORCH_CHECK(stages >= 2 && stages <= 4, "split-bf16 streaming update: 2..4 ring stages (32 KiB each)");
+    TORCH_CHECK(stages == 2 || stages == 3, "split-bf16 streaming update: 2 or 3 ring stages (32 KiB each)");
     set_s3_stream(enable ? 1 : 0, (int)stages);
   });
   m.def("set_debug_sync", &set_debug_sync);

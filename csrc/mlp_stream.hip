@@ -59,8 +59,8 @@ constexpr int TPR = 4;                // lanes per row in the loss (16 rows x 4 
 // region holding the 2-slot observation ring during fc1 and, from the loss on, dL/dmu [16][SST]
 // (dL/dv in its column 32) and the wave's partial sums [8 loss terms | 32 dlog_std]
 constexpr int XR_F = 2 * FB / 4;
-constexpr int WS_F = TILE_F + XR_F;
-static_assert(TILE_F + 40 <= XR_F + TILE_F && 16 * 32 + 16 <= TILE_F, "scratch aliasing");
+constexpr int WS_F = 2 * TILE_F + XR_F;
+static_assert(TILE_F + 40 <= XR_F && 16 * 32 + 16 <= TILE_F, "scratch aliasing");
 
 constexpr int MAX_STEPS = 64;         // stream steps of one tile (59 at Humanoid dims)
 
@@ -210,6 +210,22 @@ DEV Frag tp_getA(const float* tp, int lane) {
   return split8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
 }
 
+// the A operands of two [16][SST] tiles: four reads, one wait (one stall per fc2 step, not two)
+DEV void tp_get2A(const float* ta, const float* tb, int lane, Frag& fa, Frag& fb) {
+  const int o = (lane & 15) * SST + 8 * (lane >> 4);
+  const uint32_t aa = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(ta + o);
+  const uint32_t ab = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(tb + o);
+  float4 x0, x1, y0, y1;
+  asm volatile(
+      "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\tds_read_b128 %2, %5\n\t"
+      "ds_read_b128 %3, %5 offset:16\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(x0), "=&v"(x1), "=&v"(y0), "=&v"(y1)
+      : "v"(aa), "v"(ab)
+      : "memory");
+  fa = split8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
+  fb = split8(f32x8{y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w});
+}
+
 // activation chained into the next layer: features >= nb are zero padding except the constant-1
 // bias column nb (PackedLayout: the bias is column K of every weight image)
 DEV f32x4 bias_col(const f32x4& v, int c, int nb) {
@@ -330,9 +346,10 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   char* ring = smem;
   float* scr = reinterpret_cast<float*>(smem + (size_t)S * SB) + wave * WS_F;
   float* tp = scr;
+  float* tp2 = scr + TILE_F;      // second transpose tile (two operands per fc2 step)
   float* mus = tp;                // (loss only)
   float* vs = tp + 16 * 32;       // (loss only)
-  float* dmu = scr + TILE_F;      // (after fc1: aliases the observation ring)
+  float* dmu = scr + 2 * TILE_F;  // (after fc1: aliases the observation ring)
   float* wpart = dmu + TILE_F;
 
   // source row of tile row r (rows past M re-read row m0: finite data, zero gradient)
@@ -395,7 +412,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   // 2-slot LDS ring, DMA'd two k-steps (6 stream steps) ahead of use: a gather from HBM / the
   // Infinity Cache outlasts the weight ring's lookahead.  The ring aliases the loss scratch
   // (dead until fc3).
-  char* xring = reinterpret_cast<char*>(scr + TILE_F);
+  char* xring = reinterpret_cast<char*>(scr + 2 * TILE_F);
   auto issue_x = [&](int ks0) __attribute__((always_inline)) {
     if (abl_dma) return;
     const uint32_t xo = (uint32_t)fc1_ks(p, min(ks0, p.ks1 - 1), rot) * 128u;
@@ -534,30 +551,48 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   __bf16* const bg2v = lane_base(a.g2vT);
   __bf16* const bg1p = lane_base(a.g1pT);
   __bf16* const bg1v = lane_base(a.g1vT);
-  // operand of fc2 k-step i (i < 4: policy k-step i, else value k-step i - 4); returns its stores
-  auto prep_h1 = [&](int i, Frag& out) __attribute__((always_inline)) -> int {
-    const bool pol = i < 4;
-    const int ks = pol ? i : i - 4;
-    const int t0 = pol ? 2 * ks : 8 + 2 * ks;
-    const int nr = pol ? n1p : n1v;
-    const f32x4 h0 = act_tanh4<DT_S3>(acc1[t0]), h1 = act_tanh4<DT_S3>(acc1[t0 + 1]);
-    acc1[t0] = h0;
-    acc1[t0 + 1] = h1;
-    const int c0 = 32 * ks + lr;
+  // operands of fc2 k-steps 2J and 2J + 1 (i < 4: policy k-step i, else value k-step i - 4):
+  // tanh in place, the h1^T stores, both transposes, one LDS wait; returns the stores.  Only the
+  // last k-step of a head holds features >= its width (the bias column and padding): the shapes
+  // mlp_rs_applies admits make every other k-step's tiles all real.
+  auto prep2 = [&](auto Jc, Frag& fa, Frag& fb) __attribute__((always_inline)) -> int {
+    constexpr int J = decltype(Jc)::value;
     int nst = 0;
-    if (!no_T) {
+    static_for<0, 2>([&](auto uc) __attribute__((always_inline)) {
+      constexpr int u = decltype(uc)::value;
+      constexpr int i = 2 * J + u;
+      constexpr bool pol = i < 4;
+      constexpr int ks = pol ? i : i - 4;
+      constexpr int t0 = pol ? 2 * ks : 8 + 2 * ks;
+      constexpr bool last = pol ? ks == 3 : ks == 15;
+      const int nr = pol ? n1p : n1v;
+      const f32x4 h0 = act_tanh4<DT_S3>(acc1[t0]), h1 = act_tanh4<DT_S3>(acc1[t0 + 1]);
+      acc1[t0] = h0;
+      acc1[t0 + 1] = h1;
+      const int c0 = 32 * ks + lr;
       __bf16* oT = pol ? bh1p : bh1v;
-      if (c0 < nr) store_Tt(oT, 2 * ks, tsb, h0);
-      if (c0 + 16 < nr) store_Tt(oT, 2 * ks + 1, tsb, h1);
-      nst = (32 * ks < nr ? 2 : 0) + (32 * ks + 16 < nr ? 2 : 0);
-    }
-    tp_put(tp, bias_col(h0, c0, nr), bias_col(h1, c0 + 16, nr), lane);
-    out = tp_getA(tp, lane);
+      float* tt = u == 0 ? tp : tp2;
+      if constexpr (!last) {
+        if (!no_T) {
+          store_Tt(oT, 2 * ks, tsb, h0);
+          store_Tt(oT, 2 * ks + 1, tsb, h1);
+          nst += 4;
+        }
+        tp_put(tt, h0, h1, lane);
+      } else {
+        if (!no_T) {
+          if (c0 < nr) store_Tt(oT, 2 * ks, tsb, h0);
+          if (c0 + 16 < nr) store_Tt(oT, 2 * ks + 1, tsb, h1);
+          nst += (32 * ks < nr ? 2 : 0) + (32 * ks + 16 < nr ? 2 : 0);
+        }
+        tp_put(tt, bias_col(h0, c0, nr), bias_col(h1, c0 + 16, nr), lane);
+      }
+    });
+    tp_get2A(tp, tp2, lane, fa, fb);
     return nst;
   };
   Frag ah0, ah1;
-  int nst = prep_h1(0, ah0);
-  nst += prep_h1(1, ah1);
+  int nst = prep2(std::integral_constant<int, 0>{}, ah0, ah1);
   static_for<0, 10>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     stg = wait_step(nst);
@@ -568,8 +603,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
       else acc2v[q & 7] = P::mma(acc2v[q & 7], q < 8 ? ah0 : ah1, b);
     });
     if constexpr (j + 1 < 10) {
-      nst = prep_h1(2 * j + 2, ah0);
-      nst += prep_h1(2 * j + 3, ah1);
+      nst = prep2(std::integral_constant<int, j + 1>{}, ah0, ah1);
     } else {
       RS_STAMP(2);
       // h2 = tanh(fc2), kept for dgrad fc3; its stores belong to this step (before the refill)
@@ -864,7 +898,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   const float* sc0 = reinterpret_cast<const float*>(smem + (size_t)S * SB);
   for (int q = tid; q < RS_NPART + A; q += NW * 64) {
     float s = 0.f;
-    for (int w = 0; w < NW; ++w) s += sc0[w * WS_F + 2 * TILE_F + q];   // wpart of wave w
+    for (int w = 0; w < NW; ++w) s += sc0[w * WS_F + 3 * TILE_F + q];   // wpart of wave w
     a.part[(size_t)blockIdx.x * a.npart + q] = s;
   }
 }
@@ -892,20 +926,19 @@ extern "C" int mlp_rs_applies(const MlpArgs& a) {
          a.n_out[1] > 96 && a.n_out[1] <= 112 && a.n_out[4] > 96 && a.n_out[4] <= 112 && a.A >= 1 && a.A <= 32;
 }
 
-extern "C" size_t mlp_rs_lds_bytes() {
-  return g_rs_stages == 2 ? rs_lds_bytes<2>() : g_rs_stages == 3 ? rs_lds_bytes<3>() : rs_lds_bytes<4>();
-}
-static_assert(rs_lds_bytes<4>() <= 160 * 1024, "4-stage ring must fit LDS");
+// (a 4-stage ring measured no faster, 279 vs 274 us, and no longer fits beside two transpose
+// tiles per wave)
+extern "C" size_t mlp_rs_lds_bytes() { return g_rs_stages == 2 ? rs_lds_bytes<2>() : rs_lds_bytes<3>(); }
+static_assert(rs_lds_bytes<3>() <= 160 * 1024, "3-stage ring must fit LDS");
 
 extern "C" void launch_mlp_train_rs(const MlpArgs& a, hipStream_t s) {
   if (g_rs_stages == 2) rs_launch<2>(a, s);
-  else if (g_rs_stages == 3) rs_launch<3>(a, s);
-  else rs_launch<4>(a, s);
+  else rs_launch<3>(a, s);
 }
 
 extern "C" int s3_stream_state() { return g_rs_enable ? g_rs_stages : 0; }
 
 extern "C" void set_s3_stream(int enable, int stages) {
   g_rs_enable = enable ? 1 : 0;
-  if (stages >= 2 && stages <= 4) g_rs_stages = stages;
+  if (stages == 2 || stages == 3) g_rs_stages = stages;
 }

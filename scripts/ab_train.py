@@ -101,7 +101,6 @@ def main():
         "wg_prop": (lambda: plan_mode(False), wgrad), "wg_aligned": (lambda: plan_mode(True), wgrad),
         "rs2": (lambda: (ext.set_s3_stream(True, 2), eng.sync_tile()), train),
         "rs3": (lambda: (ext.set_s3_stream(True, 3), eng.sync_tile()), train),
-        "rs4": (lambda: (ext.set_s3_stream(True, 4), eng.sync_tile()), train),
         "tile32": (lambda: (ext.set_s3_stream(False, 3), eng.sync_tile()), train),
         "trainA": (lambda: use_ext("A"), lambda: train_with(ext_a)),
         "trainB": (lambda: use_ext("b"), lambda: train_with(variants["b"])),

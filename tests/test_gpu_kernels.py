@@ -273,7 +273,7 @@ def test_fused_loss_backward_row_tiles(rows, env_name, mb):
 
 
 @pytest.mark.parametrize("env_name,mb,stages", [("Humanoid-v2", 512, 3), ("Humanoid-v2", 200, 2),
-                                               ("HalfCheetah-v2", 256, 4), ("Pendulum-v0", 64, 3)])
+                                               ("HalfCheetah-v2", 256, 3), ("Pendulum-v0", 64, 3)])
 def test_s3_streaming_update_matches_tile_kernel(env_name, mb, stages):
     """split-bf16: the row-stationary weight-streaming update (csrc/mlp_stream.hip, 64 rows per
     workgroup, every ring depth) vs the 32-row tile kernel (mlp.hip) on the same minibatch —
