@@ -299,15 +299,17 @@ template <unsigned MASK, int N, typename F>
 DEV void for_stage(const char* stg, int lane, F&& f) {
   constexpr int H = N / 2;
   Frag b[N];
-  static_for<0, H>([&](auto qc) __attribute__((always_inline)) {
+  // one lane address per stage; every fragment then is an immediate offset (q * FB < 64 KiB)
+  const char* base = stg + lane * 16;
+  auto rd = [&](auto qc) __attribute__((always_inline)) {
     constexpr int q = decltype(qc)::value;
-    if constexpr ((MASK >> q) & 1u) b[q] = rfrag(stg, q, lane);
-  });
+    if constexpr ((MASK >> q) & 1u)
+      b[q] = Frag{*reinterpret_cast<const bf16x8*>(base + q * FB),
+                  *reinterpret_cast<const bf16x8*>(base + q * FB + 1024)};
+  };
+  static_for<0, H>(rd);
   __builtin_amdgcn_sched_barrier(0);
-  static_for<H, N>([&](auto qc) __attribute__((always_inline)) {
-    constexpr int q = decltype(qc)::value;
-    if constexpr ((MASK >> q) & 1u) b[q] = rfrag(stg, q, lane);
-  });
+  static_for<H, N>(rd);
   static_for<0, H>([&](auto qc) __attribute__((always_inline)) {
     if constexpr ((MASK >> decltype(qc)::value) & 1u) f(qc, b[decltype(qc)::value]);
   });
