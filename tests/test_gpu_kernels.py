@@ -318,6 +318,21 @@ def test_s3_streaming_update_matches_tile_kernel(env_name, mb, stages):
     assert (g_rs - g_ref).norm().item() / g_ref.norm().item() < 2e-4
 
 
+def test_s3_other_hidden_sizes_fall_back_to_tile_kernel():
+    """the streaming update is specialised for the reference network's tile counts; any other
+    hidden sizes run the 32-row tile kernel, still at fp32 accuracy"""
+    p = ppo_preset(device="gpu", env_name="HalfCheetah-v2", num_envs=64, exploration_size=64 * 8,
+                   batch_size=256, dtype="bf16x3", ent_coeff=0.01, hidden=(64, 48))
+    eng, model, _, _ = _engine(p)
+    assert eng.train_rows == 32
+    xq = _fill_buffer(eng, model)
+    idx = torch.randperm(eng.N, generator=torch.Generator().manual_seed(3))[:256]
+    eng.begin_update()
+    eng.grad(idx)
+    g_ref, _ = _torch_grad(model, p, xq, eng, idx.to(DEV))
+    assert (eng.grad_flat - g_ref).norm().item() / g_ref.norm().item() < 1e-4
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "bf16x3"])
 def test_rollout_written_xT_equals_kernel_written_xT(dtype):
     """full-batch: the x^T operand the rollout emits == the one mlp_train would transpose."""
