@@ -56,6 +56,7 @@ void set_train_tstamp(torch::Tensor buf, int64_t every) {
 }
 int g_x_stream = 0;     // A/B: non-temporal observation-row loads in the value / update kernels
 void set_x_stream(int64_t on) { g_x_stream = on ? 1 : 0; }
+int g_wgrad_dense = 1;   // split-bf16 wgrad: dense-DMA fragment layout
 int g_wgrad_impl = 0;   // 0: LDS-DMA staged, 1: register-streamed (A/B diagnostics)
 void set_wgrad_impl(int64_t impl) {
   TORCH_CHECK(impl == 0 || impl == 1, "wgrad impl: 0 LDS-DMA, 1 register");
@@ -385,6 +386,7 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
   a.slab = slab.data_ptr<float>();
   a.impl = g_wgrad_impl;
   a.waves = (int)waves;
+  a.dense = g_wgrad_dense;
   TORCH_CHECK(dt == 0 || dt == 1 || dt == 3, "wgrad runs in fp32, bf16 or bf16x3 (the fp8 mode's update is bf16)");
   launch_wgrad((int)dt, a, cur_stream());
   after_launch(__func__);
@@ -585,10 +587,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     set_s3_train_waves((int)nw);
   });
   m.def("s3_stream_state", []() { return (int64_t)s3_stream_state(); });
-  m.def("set_s3_stream", [](bool enable, int64_t stages) {
-    TORCH_CHECK(stages == 2 || stages == 3, "split-bf16 streaming update: 2 or 3 ring stages (32 KiB each)");
-    set_s3_stream(enable ? 1 : 0, (int)stages);
-  });
+  m.def(
+      "set_s3_stream",
+      [](bool enable, int64_t stages, int64_t dense) {
+        TORCH_CHECK(stages == 2 || stages == 3, "split-bf16 streaming update: 2 or 3 ring stages (32 KiB each)");
+        set_s3_stream(enable ? 1 : 0, (int)stages, (int)dense);
+      },
+      py::arg("enable"), py::arg("stages"), py::arg("dense") = -1);
   m.def("set_debug_sync", &set_debug_sync);
   m.def("set_rollout_waves", [](int64_t nw) {
     TORCH_CHECK(nw == 4 || nw == 8, "rollout waves: 4 or 8");
@@ -601,6 +606,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gae", &gae);
   m.def("set_train_ablation", &set_train_ablation);
   m.def("set_wgrad_impl", &set_wgrad_impl);
+  m.def("set_wgrad_dense", [](bool on) { g_wgrad_dense = on ? 1 : 0; });
+  m.def("wgrad_dense", []() { return (bool)g_wgrad_dense; });
   m.def("set_wgrad_stages", [](int64_t st) { set_wgrad_stages((int)st); });
   m.def("set_adam_fused", [](int64_t on) { set_adam_fused((int)on); });
   m.def("obs_reduce", &obs_reduce);

@@ -99,8 +99,8 @@ struct MlpArgs {
 extern "C" int mlp_rs_applies(const MlpArgs& a);
 extern "C" size_t mlp_rs_lds_bytes();
 extern "C" void launch_mlp_train_rs(const MlpArgs& a, hipStream_t s);
-extern "C" void set_s3_stream(int enable, int stages);
-extern "C" int s3_stream_state();   // 0 off, else the ring depth
+extern "C" void set_s3_stream(int enable, int stages, int dense);   // dense < 0: unchanged
+extern "C" int s3_stream_state();   // 0 off, else ring depth + 10 * dense-DMA layout
 
 struct WgradTask {
   int layer;      // 0..5
@@ -119,6 +119,7 @@ struct WgradArgs {
   float* slab;
   int impl;            // 0: LDS-DMA staged (default), 1: register-streamed (A/B diagnostics)
   int waves;           // workgroup size of the LDS-DMA kernel: 8, or 16 (bf16; tiles up to 16 quadrants)
+  int dense;           // split-bf16: dense-DMA fragment layout (csrc/mlp_stream.hip frag_lane_off)
 };
 
 extern "C" {

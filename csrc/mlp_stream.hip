@@ -68,6 +68,7 @@ constexpr int MAX_STEPS = 64;         // stream steps of one tile (59 at Humanoi
 // rs,tile, same box); set_s3_stream(False, ...) selects the tile kernel (A/B)
 int g_rs_enable = 1;
 int g_rs_stages = 3;
+int g_rs_dense = 1;   // dense-DMA fragment layout (frag_lane_off)
 
 template <int S>
 constexpr size_t rs_lds_bytes() { return (size_t)S * SB + (size_t)NW * WS_F * sizeof(float); }
@@ -163,11 +164,18 @@ DEV int step_src(const MlpArgs& a, const Plan& p, int st, int q, int rot) {
          (int)fm_frag(t < nt ? t : 0, ks < kq ? ks : 0, pol ? a.d_out[1] : a.d_out[4], 0);
 }
 
-// fragment in ring slot q (the DMA de-interleaved it: every lane's hi 16 B, then every lane's lo)
-DEV Frag rfrag(const char* stg, int q, int lane) {
-  const char* b = stg + q * FB + lane * 16;
-  return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + 1024)};
-}
+// LDS image of one DMA'd 2 KiB fragment.  HS (dense): the first DMA instruction moves the
+// fragment's first KiB (lanes 0-31, hi | lo each), the second the second KiB, both as fully used
+// 64-byte segments, and each lands as [hi of its 32 lanes][lo of its 32 lanes]: lane l reads hi
+// at (l / 32) KiB + 16 (l % 32) and lo 512 bytes on (any 16 consecutive lanes read 256
+// contiguous bytes: conflict-free).  !HS: every lane's hi 16 B, then every lane's lo — each DMA
+// instruction then touches 16 of every 32 bytes of the whole 2 KiB.
+template <bool HS>
+DEV int frag_lane_off(int lane) { return HS ? (lane >> 5) * 1024 + (lane & 31) * 16 : lane * 16; }
+// per-lane byte offset into a fragment's global 2 KiB for the first of its two DMA instructions
+// (the second adds HS ? 1024 : 16 in the SGPR offset; its lo half is at HS ? 512 : 1024 in LDS)
+template <bool HS>
+DEV unsigned dma_lane_src(int lane) { return HS ? (unsigned)((lane & 31) * 32 + (lane >> 5) * 16) : (unsigned)lane * 32u; }
 
 typedef __attribute__((ext_vector_type(8))) float f32x8;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
@@ -295,17 +303,17 @@ DEV void static_for(F&& f) {
 // half's LDS reads are in flight while the first half's MFMAs run (left to itself hipcc reads each
 // fragment right before its 3 MFMAs and, at one wave per SIMD, exposes the LDS latency once per
 // fragment).  f(integral_constant<q>, fragment).
-template <unsigned MASK, int N, typename F>
+template <bool HS, unsigned MASK, int N, typename F>
 DEV void for_stage(const char* stg, int lane, F&& f) {
   constexpr int H = N / 2;
   Frag b[N];
   // one lane address per stage; every fragment then is an immediate offset (q * FB < 64 KiB)
-  const char* base = stg + lane * 16;
+  const char* base = stg + frag_lane_off<HS>(lane);
   auto rd = [&](auto qc) __attribute__((always_inline)) {
     constexpr int q = decltype(qc)::value;
     if constexpr ((MASK >> q) & 1u)
       b[q] = Frag{*reinterpret_cast<const bf16x8*>(base + q * FB),
-                  *reinterpret_cast<const bf16x8*>(base + q * FB + 1024)};
+                  *reinterpret_cast<const bf16x8*>(base + q * FB + (HS ? 512 : 1024))};
   };
   static_for<0, H>(rd);
   __builtin_amdgcn_sched_barrier(0);
@@ -336,7 +344,7 @@ DEV float gsum(float x) {
   return x;
 }
 
-template <int S>
+template <int S, bool HS>
 __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const int tid = threadIdx.x, lane = tid & 63;
@@ -371,8 +379,13 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rx =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x_buf), (short)0, 0x7fffffff, 0x00020000);
-  const unsigned vw = (unsigned)lane * 32u;
-  const unsigned vx = (unsigned)(((size_t)src_of(16 * wave + lr) * a.d_in[0] + 8 * lg) * sizeof(T));
+  const unsigned vw = dma_lane_src<HS>(lane);
+  // X fragment lane fl = (row fl & 15, k-group fl >> 4): with HS the first instruction moves
+  // fragment lanes 0-31 (k-groups 0, 1: 64 contiguous bytes of each of the 16 rows), the second
+  // k-groups 2, 3 (+64 bytes)
+  const unsigned vx =
+      HS ? (unsigned)((size_t)src_of(16 * wave + lr) * a.d_in[0] * sizeof(T) + 32 * ((lane >> 4) & 1) + 16 * (lane >> 5))
+         : (unsigned)(((size_t)src_of(16 * wave + lr) * a.d_in[0] + 8 * lg) * sizeof(T));
 
   // The stream's sources, computed once per workgroup and held in two VGPRs: lane l of cw0 packs
   // this wave's slot codes 4w, 4w+1 of step l, cw1 its slots 4w+2, 4w+3, 16 bits each — a weight
@@ -407,7 +420,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
       // (the instruction's immediate offset would move the LDS destination too: the hi | lo
       // 16-byte halves differ in the SGPR offset instead)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB, 16, vw, code * 2048u, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB + 1024, 16, vw, code * 2048u + 16u, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB + 1024, 16, vw, code * 2048u + (HS ? 1024u : 16u), 0, 0);
     }
   };
   // This wave's observation fragments (its 16 rows, 32 features of k-step ks) go to a private
@@ -420,17 +433,18 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
     const uint32_t xo = (uint32_t)fc1_ks(p, min(ks0, p.ks1 - 1), rot) * 128u;
     __attribute__((address_space(3))) char* d = (__attribute__((address_space(3))) char*)(xring + (ks0 & 1) * FB);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d, 16, vx, xo, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d + 1024, 16, vx, xo + 16u, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d + 1024, 16, vx, xo + (HS ? 64u : 16u), 0, 0);
   };
   // its fragment of k-step ks (the DMA landed: every vmcnt wait since covers it, in issue order);
   // read and waited in one asm statement (a plain LDS load would wait for the ring's DMA)
   auto read_x = [&](int ks0) __attribute__((always_inline)) {
     const uint32_t addr =
-        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(xring + (ks0 & 1) * FB) + lane * 16;
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(xring + (ks0 & 1) * FB) + frag_lane_off<HS>(lane);
     bf16x8 h, l;
-    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
+    const uint32_t addr_lo = addr + (uint32_t)(HS ? 512 : 1024);
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
                  : "=&v"(h), "=&v"(l)
-                 : "v"(addr)
+                 : "v"(addr), "v"(addr_lo)
                  : "memory");
     return Frag{h, l};
   };
@@ -507,7 +521,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
       if constexpr (sub == 0) xa = read_x(ks);
       // (sub 2: fragments f = 32..38 only; f >= 39 are not DMA'd)
       constexpr unsigned M1 = sub == 2 ? ((1u << (P1 + V1 - 32)) - 1u) : 0xffffu;
-      for_stage<M1, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      for_stage<HS, M1, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
         mma1(std::integral_constant<int, 16 * sub + decltype(qc)::value>{}, b);
       });
       if constexpr (sub == 0) {
@@ -598,7 +612,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   static_for<0, 10>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     stg = wait_step(nst);
-    for_stage<0x7f7fu, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    for_stage<HS, 0x7f7fu, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
       constexpr int i = 2 * j + (q >> 3);
       if constexpr (i < 4) acc2p[q & 7] = P::mma(acc2p[q & 7], q < 8 ? ah0 : ah1, b);
@@ -653,7 +667,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   }
   stg = wait_step(nst);
   f32x4 amu0 = f32x4{0.f, 0.f, 0.f, 0.f}, amu1 = amu0, av0 = amu0;
-  for_stage<0x0fffu, 12>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+  for_stage<HS, 0x0fffu, 12>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
     constexpr int q = decltype(qc)::value;
     if constexpr (q < 4) amu0 = P::mma(amu0, am[q], b);
     else if constexpr (q < 8) amu1 = P::mma(amu1, am[q - 4], b);
@@ -823,7 +837,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
     f32x4 dp[8], dv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) dp[q] = dv[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for_stage<0x7f7fu, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    for_stage<HS, 0x7f7fu, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
       if constexpr (q < 8) dp[q] = P::mma(f32x4{0.f, 0.f, 0.f, 0.f}, adp, b);
       else dv[q - 8] = P::mma(f32x4{0.f, 0.f, 0.f, 0.f}, adv, b);
@@ -873,7 +887,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) g[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     constexpr unsigned M2 = j == 1 ? 0x0fffu : 0xffffu;   // policy pair 3's tile 7 is padding
-    for_stage<M2, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    for_stage<HS, M2, 16>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
       constexpr int P_ = 2 * j + (q >> 3);
       const Frag& a2 = P_ < 4 ? a2p[q & 3] : a2v[q & 3];
@@ -905,12 +919,12 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   }
 }
 
-template <int S>
+template <int S, bool HS>
 void rs_launch(const MlpArgs& a, hipStream_t s) {
   const size_t lds = rs_lds_bytes<S>();
-  set_max_lds_once<mlp_train_rs_kernel<S>>(lds);
+  set_max_lds_once<mlp_train_rs_kernel<S, HS>>(lds);
   const int nblk = (a.M + ROWS - 1) / ROWS;
-  hipLaunchKernelGGL((mlp_train_rs_kernel<S>), dim3(nblk), dim3(NW * 64), lds, s, a);
+  hipLaunchKernelGGL((mlp_train_rs_kernel<S, HS>), dim3(nblk), dim3(NW * 64), lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
@@ -934,13 +948,20 @@ extern "C" size_t mlp_rs_lds_bytes() { return g_rs_stages == 2 ? rs_lds_bytes<2>
 static_assert(rs_lds_bytes<3>() <= 160 * 1024, "3-stage ring must fit LDS");
 
 extern "C" void launch_mlp_train_rs(const MlpArgs& a, hipStream_t s) {
-  if (g_rs_stages == 2) rs_launch<2>(a, s);
-  else rs_launch<3>(a, s);
+  if (g_rs_dense) {
+    if (g_rs_stages == 2) rs_launch<2, true>(a, s);
+    else rs_launch<3, true>(a, s);
+  } else {
+    if (g_rs_stages == 2) rs_launch<2, false>(a, s);
+    else rs_launch<3, false>(a, s);
+  }
 }
 
-extern "C" int s3_stream_state() { return g_rs_enable ? g_rs_stages : 0; }
+// 0 = off, else stages + 10 * dense-DMA layout
+extern "C" int s3_stream_state() { return g_rs_enable ? g_rs_stages + 10 * g_rs_dense : 0; }
 
-extern "C" void set_s3_stream(int enable, int stages) {
+extern "C" void set_s3_stream(int enable, int stages, int dense) {
   g_rs_enable = enable ? 1 : 0;
   if (stages == 2 || stages == 3) g_rs_stages = stages;
+  if (dense >= 0) g_rs_dense = dense ? 1 : 0;
 }

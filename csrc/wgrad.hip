@@ -110,7 +110,7 @@ constexpr size_t wgrad_lds_bytes() { return (size_t)S * WgSlots<W>::N * wgrad_fr
 int g_wgrad_stages = 4;
 
 
-template <int DT, int S, int C, int W>
+template <int DT, int S, int C, int W, bool HS>
 DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   using P = Prec<DT>;
   using T = typename P::T;
@@ -144,10 +144,13 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
     for (int q = 0; q < C; ++q)
 #pragma unroll
       for (int h = 0; h < NI; ++h) {
-        // split-bf16 fragments (32 B per lane: hi | lo) are de-interleaved by the DMA itself:
-        // instruction h moves every lane's h-th 16 bytes, so LDS holds the hi block, then the
-        // lo block, each read conflict-free at lane * 16
-        const size_t go = IsSplit<DT>::value ? (size_t)lane * 32 + h * 16 : (size_t)h * 1024 + lane * 16;
+        // split-bf16 fragments (32 B per lane: hi | lo) are de-interleaved by the DMA itself.
+        // HS (dense): instruction h moves the fragment's h-th KiB (lanes 32h .. 32h+31), landing
+        // as [their hi][their lo]; otherwise instruction h moves every lane's h-th 16 bytes (LDS:
+        // the hi block, then the lo block).  Both are read conflict-free.
+        const size_t go = IsSplit<DT>::value
+                              ? (HS ? (size_t)h * 1024 + (lane & 31) * 32 + (lane >> 5) * 16 : (size_t)lane * 32 + h * 16)
+                              : (size_t)h * 1024 + lane * 16;
         glds16(src[q] + (size_t)kk * FB + go, st + dst[q] + h * 1024);
       }
   };
@@ -169,8 +172,8 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
       Frag af[4], bf[4];
       auto lds_frag = [&](int f) {
         if constexpr (IsSplit<DT>::value) {
-          const char* b = st + f * FB + lane * 16;
-          return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + 1024)};
+          const char* b = st + f * FB + (HS ? (lane >> 5) * 1024 + (lane & 31) * 16 : lane * 16);
+          return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + (HS ? 512 : 1024))};
         } else {
           return P::load(reinterpret_cast<const T*>(st + f * FB) + lane * 8);
         }
@@ -200,23 +203,34 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
       for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * KE + col + 16 * j] = acc[i][j][q];
 }
 
-template <int DT, int S, int W>
+template <int DT, int S, int W, bool HS>
 __global__ __launch_bounds__(W * 64) void wgrad_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const WgradTask tk = a.tasks[blockIdx.x];
   if constexpr (W == 16) {
-    wgrad_lds_body<DT, S, 2, W>(a, tk, smem);    // 32 slots = 2 per wave
+    wgrad_lds_body<DT, S, 2, W, HS>(a, tk, smem);    // 32 slots = 2 per wave
   } else {
-    if (4 * (tk.nq + tk.kq) <= 2 * W) wgrad_lds_body<DT, S, 2, W>(a, tk, smem);
-    else wgrad_lds_body<DT, S, 3, W>(a, tk, smem);
+    if (4 * (tk.nq + tk.kq) <= 2 * W) wgrad_lds_body<DT, S, 2, W, HS>(a, tk, smem);
+    else wgrad_lds_body<DT, S, 3, W, HS>(a, tk, smem);
   }
+}
+
+template <int DT, int S, int W, bool HS>
+void launch_wgrad_lds_t(const WgradArgs& a, hipStream_t s) {
+  const size_t lds = wgrad_lds_bytes<DT, S, W>();
+  set_max_lds_once<wgrad_kernel<DT, S, W, HS>>(lds);
+  hipLaunchKernelGGL((wgrad_kernel<DT, S, W, HS>), dim3(a.ntasks), dim3(W * 64), lds, s, a);
 }
 
 template <int DT, int S, int W = 8>
 void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
-  const size_t lds = wgrad_lds_bytes<DT, S, W>();
-  set_max_lds_once<wgrad_kernel<DT, S, W>>(lds);
-  hipLaunchKernelGGL((wgrad_kernel<DT, S, W>), dim3(a.ntasks), dim3(W * 64), lds, s, a);
+  if constexpr (IsSplit<DT>::value) {
+    if (a.dense) {
+      launch_wgrad_lds_t<DT, S, W, true>(a, s);
+      return;
+    }
+  }
+  launch_wgrad_lds_t<DT, S, W, false>(a, s);
 }
 
 // With the partials pass (nred = A + 8 > 0):

@@ -58,6 +58,7 @@ def main():
     p, eng = build(dtype)
     ext = eng.ext
     state = ext.s3_stream_state()
+    wg_dense = ext.wgrad_dense()
     M = eng.mb
 
     def train():
@@ -99,8 +100,12 @@ def main():
     arms = {
         "s3w4": (waves(4), train), "s3w8": (waves(8), train),
         "wg_prop": (lambda: plan_mode(False), wgrad), "wg_aligned": (lambda: plan_mode(True), wgrad),
-        "rs2": (lambda: (ext.set_s3_stream(True, 2), eng.sync_tile()), train),
-        "rs3": (lambda: (ext.set_s3_stream(True, 3), eng.sync_tile()), train),
+        "rs2": (lambda: (ext.set_s3_stream(True, 2, 0), eng.sync_tile()), train),
+        "rs3": (lambda: (ext.set_s3_stream(True, 3, 0), eng.sync_tile()), train),
+        "rs3d": (lambda: (ext.set_s3_stream(True, 3, 1), eng.sync_tile()), train),
+        "rs2d": (lambda: (ext.set_s3_stream(True, 2, 1), eng.sync_tile()), train),
+        "wg_sparse": (lambda: ext.set_wgrad_dense(False), wgrad),
+        "wg_dense": (lambda: ext.set_wgrad_dense(True), wgrad),
         "tile32": (lambda: (ext.set_s3_stream(False, 3), eng.sync_tile()), train),
         "trainA": (lambda: use_ext("A"), lambda: train_with(ext_a)),
         "trainB": (lambda: use_ext("b"), lambda: train_with(variants["b"])),
@@ -126,8 +131,9 @@ def main():
             setup()
             res[k].append(timed(fn))
     use_ext("A")
-    ext.set_s3_stream(state > 0, state or 3)
+    ext.set_s3_stream(state > 0, (state % 10) or 3, state // 10 if state else -1)
     eng.sync_tile()
+    ext.set_wgrad_dense(wg_dense)
     plan_mode(False)
     ext.set_s3_train_waves(8)
     ext.set_train_ablation(0)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""rocprofv3 ``*_kernel_stats.csv`` -> markdown table (for profiles/).
+"""rocprofv3 ``*_kernel_stats.csv`` (or the ``*_results.db`` its default rocpd output writes)
+-> markdown table (for profiles/).
 
     python scripts/kernel_stats_md.py gpurun_out/prof/run_kernel_stats.csv "title" [notes] > profiles/x.md
 """
@@ -7,10 +8,23 @@ import csv
 import sys
 
 
+def from_db(path):
+    """the kernel_stats.csv columns from the rocpd sqlite database (its `kernels` view)"""
+    import sqlite3
+    con = sqlite3.connect(path)
+    q = ("select name, count(*), sum(end - start), min(end - start) from kernels group by name")
+    out = [dict(Name=n, Calls=c, TotalDurationNs=t, MinNs=m) for n, c, t, m in con.execute(q)]
+    tot = sum(r["TotalDurationNs"] for r in out) or 1
+    for r in out:
+        r["AverageNs"] = r["TotalDurationNs"] / r["Calls"]
+        r["Percentage"] = 100.0 * r["TotalDurationNs"] / tot
+    return out
+
+
 def main():
     path, title = sys.argv[1], sys.argv[2]
     notes = sys.argv[3] if len(sys.argv) > 3 else ""
-    rows = list(csv.DictReader(open(path)))
+    rows = from_db(path) if path.endswith(".db") else list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
     total = sum(float(r["TotalDurationNs"]) for r in rows)
     print(f"# {title}\n")

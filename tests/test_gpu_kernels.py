@@ -272,11 +272,36 @@ def test_fused_loss_backward_row_tiles(rows, env_name, mb):
         ext.set_mlp_rows(0)
 
 
-@pytest.mark.parametrize("env_name,mb,stages", [("Humanoid-v2", 512, 3), ("Humanoid-v2", 200, 2),
-                                               ("HalfCheetah-v2", 256, 3), ("Pendulum-v0", 64, 3)])
-def test_s3_streaming_update_matches_tile_kernel(env_name, mb, stages):
+def test_s3_wgrad_dense_dma_layout_is_bitwise_identical():
+    """split-bf16 wgrad (csrc/wgrad.hip): the dense-DMA fragment layout moves the same fragments
+    into a different LDS image and feeds the same MFMAs in the same order — the full gradient is
+    bitwise the sparse layout's."""
+    ext = _ext()
+    p = ppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 8,
+                   batch_size=512, dtype="bf16x3", ent_coeff=0.01)
+    eng, model, _, _ = _engine(p)
+    _fill_buffer(eng, model)
+    idx = torch.randperm(eng.N, generator=torch.Generator().manual_seed(5))[:512]
+    state = ext.wgrad_dense()
+    res = {}
+    try:
+        for on in (True, False):
+            ext.set_wgrad_dense(on)
+            eng.begin_update()
+            eng.grad(idx)
+            res[on] = eng.grad_flat.clone()
+    finally:
+        ext.set_wgrad_dense(state)
+    assert torch.equal(res[True], res[False])
+    assert res[True].abs().sum().item() > 0
+
+
+@pytest.mark.parametrize("env_name,mb,stages,dense", [
+    ("Humanoid-v2", 512, 3, 1), ("Humanoid-v2", 512, 3, 0), ("Humanoid-v2", 200, 2, 1),
+    ("Humanoid-v2", 200, 2, 0), ("HalfCheetah-v2", 256, 3, 1), ("Pendulum-v0", 64, 3, 0)])
+def test_s3_streaming_update_matches_tile_kernel(env_name, mb, stages, dense):
     """split-bf16: the row-stationary weight-streaming update (csrc/mlp_stream.hip, 64 rows per
-    workgroup, every ring depth) vs the 32-row tile kernel (mlp.hip) on the same minibatch —
+    workgroup, every ring depth, both DMA fragment layouts) vs the 32-row tile kernel (mlp.hip) on the same minibatch —
     gradients, loss terms and the wgrad operands both write (idx gather, ragged last tile, the
     in-kernel X^T path)."""
     ext = _ext()
@@ -289,14 +314,14 @@ def test_s3_streaming_update_matches_tile_kernel(env_name, mb, stages):
     state = ext.s3_stream_state()
     try:
         for on in (True, False):
-            ext.set_s3_stream(on, stages)
+            ext.set_s3_stream(on, stages, dense)
             eng.sync_tile()
             assert eng.train_rows == (64 if on else 32)
             eng.begin_update()
             eng.grad(idx)
             res[on] = (eng.grad_flat.clone(), eng.last_losses(), eng.g1vT.clone(), eng.h1pT.clone())
     finally:
-        ext.set_s3_stream(state > 0, state or 3)
+        ext.set_s3_stream(state > 0, (state % 10) or 3, state // 10 if state else -1)
         eng.sync_tile()
     g_rs, l_rs, g1_rs, h1_rs = res[True]
     g_t, l_t, g1_t, h1_t = res[False]
