@@ -512,12 +512,14 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
       acc1[t] = P::mma(acc1[t], xa, b);
     }
   };
-  int nstx = 0;
   for (int ks = 0; ks < p.ks1; ++ks) {
     // (sub 0 issues the X^T stores, if any, and — after its refill — the 2 X loads of ks + 2)
     static_for<0, 3>([&](auto sc) __attribute__((always_inline)) {
       constexpr int sub = decltype(sc)::value;
-      stg = sub == 1 ? wait_step(nstx, 2) : wait_step(0);
+      // (sub 1 waits with sub 0's 2 X loads outstanding; sub 0's X^T stores, when the rollout did
+      // not write X^T, are not counted — an undercount, so the wait also covers them — which
+      // keeps every fc1 wait count a compile-time constant)
+      stg = sub == 1 ? wait_step(0, 2) : wait_step(0);
       if constexpr (sub == 0) xa = read_x(ks);
       // (sub 2: fragments f = 32..38 only; f >= 39 are not DMA'd)
       constexpr unsigned M1 = sub == 2 ? ((1u << (P1 + V1 - 32)) - 1u) : 0xffffu;
@@ -525,7 +527,6 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
         mma1(std::integral_constant<int, 16 * sub + decltype(qc)::value>{}, b);
       });
       if constexpr (sub == 0) {
-        nstx = 0;
         if (want_xT) {
           // the rollout did not write this call's X^T: transpose the wave's 16 x 32 block here
           const f32x8 x = join8(xa);
@@ -534,7 +535,6 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
           w[1] = float4{x[4], x[5], x[6], x[7]};
           store_T8(a.xT, tp, SST, lane >> 1, lane & 1, 32 * fc1_ks(p, ks, rot) + (lane >> 1),
                    mw + 8 * (lane & 1), a.ldT);
-          nstx = 2;
         }
         refill();
         issue_x(ks + 2);   // into the slot X[ks] just left
@@ -548,7 +548,6 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   // ---------------- fc2: h1 = tanh(fc1) chained two tiles (one k-step) at a time ----------------
   // Software-pipelined: step j's MFMAs and step j+1's two operands (tanh, the h1^T stores, the
   // LDS transposes) share one scheduling region, so the VALU work fills the MFMA shadow.
-  const bool no_T = (a.ablate & 1) != 0;
   const int n1p = a.n_out[0], n1v = a.n_out[3], n2p = a.n_out[1], n2v = a.n_out[4];
   f32x4 acc2p[8], acc2v[8];
 #pragma unroll
@@ -588,21 +587,14 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
       const int c0 = 32 * ks + lr;
       __bf16* oT = pol ? bh1p : bh1v;
       float* tt = u == 0 ? tp : tp2;
-      if constexpr (!last) {
-        if (!no_T) {
-          store_Tt(oT, 2 * ks, tsb, h0);
-          store_Tt(oT, 2 * ks + 1, tsb, h1);
-          nst += 4;
-        }
-        tp_put(tt, h0, h1, lane);
-      } else {
-        if (!no_T) {
-          if (c0 < nr) store_Tt(oT, 2 * ks, tsb, h0);
-          if (c0 + 16 < nr) store_Tt(oT, 2 * ks + 1, tsb, h1);
-          nst += (32 * ks < nr ? 2 : 0) + (32 * ks + 16 < nr ? 2 : 0);
-        }
-        tp_put(tt, bias_col(h0, c0, nr), bias_col(h1, c0 + 16, nr), lane);
-      }
+      // (the last k-step's features >= nr are the bias column (1) and zero padding: stored
+      // as such, rewriting the operand's constant bias row with its own value, so every lane
+      // stores and the step's store count is a compile-time constant)
+      const f32x4 s0 = last ? bias_col(h0, c0, nr) : h0, s1 = last ? bias_col(h1, c0 + 16, nr) : h1;
+      store_Tt(oT, 2 * ks, tsb, s0);
+      store_Tt(oT, 2 * ks + 1, tsb, s1);
+      nst += 4;
+      tp_put(tt, s0, s1, lane);
     });
     tp_get2A(tp, tp2, lane, fa, fb);
     return nst;
@@ -629,9 +621,9 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
         acc2p[q] = act_tanh4<DT_S3>(acc2p[q]);
         acc2v[q] = act_tanh4<DT_S3>(acc2v[q]);
         const int c = 16 * q + lr;
-        if (!no_T && c < n2p) store_Tt(bh2p, q, tsb, acc2p[q]);
-        if (!no_T && c < n2v) store_Tt(bh2v, q, tsb, acc2v[q]);
-        if (!no_T) nst += (16 * q < n2p ? 2 : 0) + (16 * q < n2v ? 2 : 0);
+        store_Tt(bh2p, q, tsb, bias_col(acc2p[q], c, n2p));   // (bias row 1, padding 0)
+        store_Tt(bh2v, q, tsb, bias_col(acc2v[q], c, n2v));
+        nst += 4;
       }
     }
     refill();
@@ -848,9 +840,10 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
       const int c = 16 * q + lr;
       dp[q] = c < n2p ? dp[q] * (1.0f - acc2p[q] * acc2p[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
       dv[q] = c < n2v ? dv[q] * (1.0f - acc2v[q] * acc2v[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
-      if (!no_T && c < n2p) store_Tt(bg2p, q, tsb, dp[q]);
-      if (!no_T && c < n2v) store_Tt(bg2v, q, tsb, dv[q]);
-      if (!no_T) nst += (16 * q < n2p ? 2 : 0) + (16 * q < n2v ? 2 : 0);
+      // (dY^T rows past the layer's width: zeros; wgrad's output rows there are never gathered)
+      store_Tt(bg2p, q, tsb, dp[q]);
+      store_Tt(bg2v, q, tsb, dv[q]);
+      nst += 4;
     }
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -873,12 +866,11 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
     const bool pol = P_ < 4;
     const int jj = pol ? P_ : P_ - 4;
     const int t0 = pol ? 2 * jj : 8 + 2 * jj;
-    const int nr = pol ? n1p : n1v;
     __bf16* oT = pol ? bg1p : bg1v;
-    const int c0 = 32 * jj + lr;
-    if (c0 < nr) store_Tt(oT, 2 * jj, tsb, g0 * (1.0f - acc1[t0] * acc1[t0]));
-    if (c0 + 16 < nr) store_Tt(oT, 2 * jj + 1, tsb, g1 * (1.0f - acc1[t0 + 1] * acc1[t0 + 1]));
-    return (32 * jj < nr ? 2 : 0) + (32 * jj + 16 < nr ? 2 : 0);
+    // (rows past the width carry don't-care values: wgrad's output rows there are never gathered)
+    store_Tt(oT, 2 * jj, tsb, g0 * (1.0f - acc1[t0] * acc1[t0]));
+    store_Tt(oT, 2 * jj + 1, tsb, g1 * (1.0f - acc1[t0 + 1] * acc1[t0 + 1]));
+    return 4;
   };
   static_for<0, 10>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;

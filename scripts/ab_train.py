@@ -115,7 +115,7 @@ def main():
         "grad": (waves(8), lambda: eng.grad(None)), "values": (waves(8), eng.values),
         "rollout": (waves(8), eng.rollout),
         "abl0": (lambda: ext.set_train_ablation(0), train), "abl1": (lambda: ext.set_train_ablation(1), train),
-        "abl2": (lambda: ext.set_train_ablation(2), train), "abl4": (lambda: ext.set_train_ablation(4), train),
+        "abl2": (lambda: ext.set_train_ablation(2), train), "abl4": (lambda: ext.set_train_ablation(4), train), "abl3": (lambda: ext.set_train_ablation(3), train),
         "abl8": (lambda: ext.set_train_ablation(8), train), "abl16": (lambda: ext.set_train_ablation(16), train),
         "abl7": (lambda: ext.set_train_ablation(7), train),
         "val4": (lambda: ext.set_s3_value_waves(4), eng.values),
