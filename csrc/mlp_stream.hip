@@ -407,6 +407,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   const uint32_t cw1 = code16(lane, SPW * wave + 2) | (code16(lane, SPW * wave + 3) << 16);
 
   const bool abl_dma = (a.ablate & 2) != 0;   // diagnostics only (phase_timeline TIMELINE_ABLATE=2)
+  const bool abl_x = (a.ablate & 8) != 0;     // diagnostics only: no observation DMA (stale X)
   auto issue = [&](int st, int stage) __attribute__((always_inline)) {
     if (abl_dma) return;
     const int l = min(st, MAX_STEPS - 1);
@@ -429,7 +430,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_train_rs_kernel(MlpArgs a) {
   // (dead until fc3).
   char* xring = reinterpret_cast<char*>(scr + 2 * TILE_F);
   auto issue_x = [&](int ks0) __attribute__((always_inline)) {
-    if (abl_dma) return;
+    if (abl_dma || abl_x) return;
     const uint32_t xo = (uint32_t)fc1_ks(p, min(ks0, p.ks1 - 1), rot) * 128u;
     __attribute__((address_space(3))) char* d = (__attribute__((address_space(3))) char*)(xring + (ks0 & 1) * FB);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d, 16, vx, xo, 0, 0);
