@@ -1,0 +1,54 @@
+"""bench.py output contract (the driver parses this line): one JSON line from rank 0 with the
+BASELINE metric, the whole-job value over all ranks, and the timing fields — at a tiny geometry,
+on one GPU and as 2 torchrun ranks sharing it (gloo; RCCL refuses two ranks on one device, the
+driver's N-GPU runs use RCCL through the same code path)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = ["--num-envs", "64", "--rollout-len", "4", "--num-epoch", "2", "--steps", "2", "--warmup", "1"]
+
+
+def _json_line(out: str) -> dict:
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def _check(d: dict, n: int, variants: list) -> None:
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert d["metric"] == base["metric"]
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    assert d["dtype"] == "fp32_3xbf16" and d["unit"] == "env_steps/s"
+    rows = 64 * 4
+    assert d["config"]["global_batch"] == rows * n and d["config"]["parallelism"] == f"dp{n}"
+    # value = total env steps of all ranks / the max-over-ranks elapsed time
+    assert d["value"] == pytest.approx(rows * n * 2 / (d["ms_per_step"] * 2 / 1e3), rel=1e-6)
+    assert d["vs_baseline"] == pytest.approx(d["value"] / 1.6e3)
+    assert sorted(d["variants"]) == sorted(variants)
+
+
+def test_bench_json_line_one_gpu():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", *TINY, "--variants", "bf16"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check(_json_line(r.stdout), 1, ["bf16"])
+
+
+def test_bench_json_line_two_ranks():
+    env = dict(os.environ, DPPO_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29681", "bench.py", "--gpus", "2", *TINY,
+                        "--variants", "", "--verify-sync"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check(_json_line(r.stdout), 2, [])
+    assert "replicas_in_sync True" in r.stderr
