@@ -8,7 +8,10 @@ Arms, interleaved, each timed over `reps` back-to-back launches with HIP events:
   adam         the no-clip Adam alone (reads grad_flat; images written)
   adam_noimg   the no-clip Adam alone without image stores
 
-    python scripts/ab_gather.py [dtype] [reps]
+    python scripts/ab_gather.py [dtype] [reps] [variant]
+
+With a variant name (an extension built from another source tree, ops/_build.py --variant) the
+fused and gather arms are also timed through that build, interleaved: a same-box A/B.
 """
 import json
 import os
@@ -70,6 +73,21 @@ def main():
 
     arms = {"fused": fused(eng.w_map), "no_images": fused(neg), "gather": gather, "adam": adam(eng.w_map),
             "adam_noimg": adam(neg)}
+    if len(sys.argv) > 3:
+        from pytorch_dppo_amd.ops import native
+
+        def with_ext(e, fn):     # the arms' closures read `ext` at call time
+            def f():
+                nonlocal ext
+                old, ext = ext, e
+                try:
+                    fn()
+                finally:
+                    ext = old
+            return f
+        v = native.load_variant(sys.argv[3])
+        arms[f"fused_{sys.argv[3]}"] = with_ext(v, fused(eng.w_map))
+        arms[f"gather_{sys.argv[3]}"] = with_ext(v, gather)
     res = {k: [] for k in arms}
     for _ in range(3):
         for k, fn in arms.items():
