@@ -335,32 +335,58 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
     } else {
       // item = (row r, dim pair p), consecutive threads on consecutive pairs of one row: the
       // 16 x S/2 items spread evenly over the threads (one Box-Muller pair per item) and the
-      // per-dim constants come from LDS tables filled once per launch
+      // per-dim constants come from LDS tables filled once per launch.  Two items per turn with
+      // every LDS read of both issued before any state store (items never share a state slot),
+      // so the second item's loads, hashes and transcendentals overlap the first's instead of
+      // waiting behind its stores; the reset / step choice is a select, not a branch.
       const int np = (S + 1) >> 1;
       int r = tid / np, p = tid - r * np;
       const int sr = NTHR / np, sp = NTHR - sr * np;
-      while (r < ROWS) {
-        const int d0 = 2 * p, d1 = d0 + 1;
-        const bool has1 = d1 < S;
-        float n0, n1;
-        if (done_s[r] > 0.5f) {
-          const float2 g = gauss_pair(kes[2 * ROWS + r], (uint32_t)p);
+      struct In { float st0, st1, a0, a1, w0, w1; uint32_t key; bool done, has1; int d0; };
+      auto load = [&](int rr, int pp) {
+        In q;
+        q.d0 = 2 * pp;
+        q.has1 = q.d0 + 1 < S;
+        const int d1 = q.has1 ? q.d0 + 1 : q.d0;
+        q.done = done_s[rr] > 0.5f;
+        q.key = q.done ? kes[2 * ROWS + rr] : kes[ROWS + rr];
+        q.st0 = st[rr * S + q.d0];
+        q.st1 = st[rr * S + d1];
+        q.a0 = act[rr * A + jdx[q.d0]];
+        q.a1 = act[rr * A + jdx[d1]];
+        q.w0 = wdrv[q.d0];
+        q.w1 = wdrv[d1];
+        return q;
+      };
+      auto step_item = [&](const In& q, int pp, float& n0, float& n1) {
+        const float2 g = gauss_pair(q.key, (uint32_t)pp);
+        if (q.done) {
           n0 = SYN_RESET * g.x;
           n1 = SYN_RESET * g.y;
         } else {
-          const float2 g = gauss_pair(kes[ROWS + r], (uint32_t)p);
-          const float a0 = fminf(fmaxf(act[r * A + jdx[d0]], -1.f), 1.f);
-          n0 = SYN_DECAY * st[r * S + d0] + SYN_DRIVE * fast_tanh(wdrv[d0] * a0) + SYN_NOISE * g.x;
-          n1 = 0.f;
-          if (has1) {
-            const float a1 = fminf(fmaxf(act[r * A + jdx[d1]], -1.f), 1.f);
-            n1 = SYN_DECAY * st[r * S + d1] + SYN_DRIVE * fast_tanh(wdrv[d1] * a1) + SYN_NOISE * g.y;
-          }
+          const float a0 = fminf(fmaxf(q.a0, -1.f), 1.f);
+          const float a1 = fminf(fmaxf(q.a1, -1.f), 1.f);
+          n0 = SYN_DECAY * q.st0 + SYN_DRIVE * fast_tanh(q.w0 * a0) + SYN_NOISE * g.x;
+          n1 = SYN_DECAY * q.st1 + SYN_DRIVE * fast_tanh(q.w1 * a1) + SYN_NOISE * g.y;
         }
-        st[r * S + d0] = n0;
-        if (has1) st[r * S + d1] = n1;
-        r += sr;
-        p += sp;
+      };
+      while (r < ROWS) {
+        int r2 = r + sr, p2 = p + sp;
+        if (p2 >= np) { p2 -= np; ++r2; }
+        const bool v2 = r2 < ROWS;
+        const In q1 = load(r, p);
+        const In q2 = load(v2 ? r2 : r, v2 ? p2 : p);   // past the end: re-read item 1 (unused)
+        float n10, n11, n20, n21;
+        step_item(q1, p, n10, n11);
+        step_item(q2, v2 ? p2 : p, n20, n21);
+        st[r * S + q1.d0] = n10;
+        if (q1.has1) st[r * S + q1.d0 + 1] = n11;
+        if (v2) {
+          st[r2 * S + q2.d0] = n20;
+          if (q2.has1) st[r2 * S + q2.d0 + 1] = n21;
+        }
+        r = r2 + sr;
+        p = p2 + sp;
         if (p >= np) { p -= np; ++r; }
       }
     }
