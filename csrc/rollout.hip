@@ -69,6 +69,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   uint32_t* kes = cv.take<uint32_t>(3 * ROWS);   // per-env key prefixes of this step: action, env, reset
   float* wdrv = cv.take<float>(S);                // synthetic dynamics: drive weight of state dim d
   int* jdx = cv.take<int>(S);                     //                     action index driving dim d
+  float* lsg = cv.take<float>(2 * A);             // per action dim: log sigma [0, A), sigma [A, 2A)
   // fp8: the MFMA tile is e4m3 but the buffer rows are bf16 — a bf16 staging tile lets them
   // leave as 16-byte row chunks (element stores strided by the row length were 2.6x the bf16
   // kernel's time)
@@ -98,6 +99,14 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   for (int d = tid; d < S; d += NTHR) {   // per-dim constants once per launch (no per-step modulo)
     wdrv[d] = 0.5f + (float)(d % 7) / 7.0f;
     jdx[d] = d % A;
+  }
+  // log_std is fixed during a rollout: log sigma and sigma once per launch, not a global load
+  // (and an exp) per sampled dim and step
+  for (int j = tid; j < A; j += NTHR) {
+    const float ls = a.log_std[j];
+    const float lsig = a.std_var ? 0.5f * ls : ls;
+    lsg[j] = lsig;
+    lsg[A + j] = __expf(lsig);
   }
   if (tid < ROWS) {
     int e = e0 + tid;
@@ -239,10 +248,8 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
       for (int h = 0; h < 2; ++h) {
         const int j = 2 * q + h;
         if (j < A) {
-          const float ls = a.log_std[j];
-          const float lsig = a.std_var ? 0.5f * ls : ls;
           const float eps = h ? g.y : g.x;
-          const float av = mu[r * A + j] + __expf(lsig) * eps;
+          const float av = mu[r * A + j] + lsg[A + j] * eps;
           act[r * A + j] = av;
           epsb[r * A + j] = eps;
           if (r < nvalid) a.actions[((size_t)tb * a.buf_E + e0 + r) * A + j] = av;
@@ -260,10 +267,8 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
       float lp = 0.f, err = 0.f;
       const int na = min(A, O);
       for (int j = l; j < A; j += LPE) {
-        const float ls = a.log_std[j];
-        const float lsig = a.std_var ? 0.5f * ls : ls;
         const float ep = epsb[r * A + j];
-        lp += -0.5f * ep * ep - lsig;
+        lp += -0.5f * ep * ep - lsg[j];
         if (a.kind != 1 && j < na) {
           const float ac = fminf(fmaxf(act[r * A + j], -1.f), 1.f);
           const float d = ac - fast_tanh(st[r * S + j]);
@@ -429,6 +434,7 @@ size_t rollout_lds(const RolloutArgs& a) {
   b += al(sizeof(float) * ROWS) + al(sizeof(int) * ROWS) + al(sizeof(float) * ROWS) + al(sizeof(float) * 2 * ROWS);
   b += al(sizeof(uint32_t) * 3 * ROWS);
   b += al(sizeof(float) * a.S) + al(sizeof(int) * a.S);
+  b += al(sizeof(float) * 2 * a.A);
   if (DT == DT_FP8) b += al(sizeof(__bf16) * ROWS * a.d1);   // bf16 staging tile of the buffer rows
   return b;
 }
