@@ -94,6 +94,11 @@ def main():
             eng.wgrad_aligned = aligned
             eng._build_wgrad_plan(eng.model)
 
+    def plan_wgs(n):   # wgrad task count of the plan (engine_hip WGRAD_TARGET_WGS)
+        if getattr(eng, "_ab_wgs", None) != n:
+            eng._ab_wgs = n
+            eng._build_wgrad_plan(eng.model, target_wgs=n)
+
     def waves(n):
         return lambda: (ext.set_s3_train_waves(n), eng.sync_tile())
 
@@ -124,6 +129,8 @@ def main():
         "roll4": (lambda: ext.set_rollout_waves(4), eng.rollout),
         "roll8": (lambda: ext.set_rollout_waves(8), eng.rollout),
     }
+    for n in (192, 224, 240, 256, 272, 288, 320, 384, 448, 512):
+        arms[f"wgs{n}"] = ((lambda n=n: plan_wgs(n)), wgrad)
     res = {k: [] for k in want}
     for _ in range(5):
         for k in want:
@@ -135,6 +142,7 @@ def main():
     eng.sync_tile()
     ext.set_wgrad_dense(wg_dense)
     plan_mode(False)
+    plan_wgs(0)
     ext.set_s3_train_waves(8)
     ext.set_train_ablation(0)
     out = {k: {"median_us": sorted(v)[len(v) // 2], "all_us": [round(x, 1) for x in v]} for k, v in res.items()}
