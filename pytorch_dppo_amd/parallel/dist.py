@@ -73,19 +73,27 @@ class DistContext:
             dist.broadcast(t, src=src)
 
     def allreduce_obs_moments(self, count: float, s1: torch.Tensor, s2: torch.Tensor,
-                              count_uniform: bool = False):
+                              count_uniform: bool = False, extra: Optional[torch.Tensor] = None):
         """global (count, S1, S2) about a shift every rank shares — exact merge (R2).
 
         ``count_uniform``: every rank contributed the same (host-known) count, so the global
-        count is count * world_size and no device->host read is needed (the hot path)."""
+        count is count * world_size and no device->host read is needed (the hot path).
+        ``extra`` (count_uniform only): a small fp64 device tensor summed over ranks in the SAME
+        all-reduce and written back in place — the iteration's episode [return sum, count] (R5)
+        ride along with the moments instead of costing a second collective."""
         if not self.collective:
             return count, s1, s2
         O = s1.numel()
         if count_uniform:
-            buf = torch.cat([s1.reshape(-1).to(self.device, torch.float64),
-                             s2.reshape(-1).to(self.device, torch.float64)])
+            parts = [s1.reshape(-1).to(self.device, torch.float64), s2.reshape(-1).to(self.device, torch.float64)]
+            if extra is not None:
+                parts.append(extra.reshape(-1).to(self.device, torch.float64))
+            buf = torch.cat(parts)
             dist.all_reduce(buf, op=dist.ReduceOp.SUM)
-            return count * self.world_size, buf[:O], buf[O:]
+            if extra is not None:
+                extra.copy_(buf[2 * O:].view(extra.shape))
+            return count * self.world_size, buf[:O], buf[O:2 * O]
+        assert extra is None, "extra rides only on the count-uniform all-reduce"
         buf = torch.empty(1 + 2 * O, dtype=torch.float64, device=self.device)
         buf[0] = count
         buf[1:1 + O] = s1.reshape(-1).to(self.device, torch.float64)

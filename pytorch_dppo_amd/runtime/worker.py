@@ -92,8 +92,8 @@ class DPPOWorker:
             self._stats_stream = torch.cuda.Stream(device=self.device)
 
     # ---------------------------------------------------------------------------------------
-    def _merge_stats(self, count, s1, s2, shift, count_uniform: bool = False) -> None:
-        count, s1, s2 = self.ctx.allreduce_obs_moments(count, s1, s2, count_uniform=count_uniform)
+    def _merge_stats(self, count, s1, s2, shift, count_uniform: bool = False, extra=None) -> None:
+        count, s1, s2 = self.ctx.allreduce_obs_moments(count, s1, s2, count_uniform=count_uniform, extra=extra)
         self.stats.merge_moments(count, s1, s2, shift)
 
     def init_stats(self) -> None:
@@ -140,15 +140,19 @@ class DPPOWorker:
         tm.start("obs_stats")
         # every rank collects exactly T*E steps -> the global count is host-known (no sync)
         stats_done = None
+        # the episode [return sum, count] of a device rollout join the moments' all-reduce (R5)
+        ep2 = ro.get("ep2")
+        ep_extra = ep2 if (torch.is_tensor(ep2) and ep2.dtype == torch.float64 and ep2.device == self.device) else None
+        ro["ep2_reduced"] = ep_extra is not None
         if side is not None:
             # rollout-mode stats feed only the NEXT rollout's normalisation: the reduce, the RCCL
             # all-reduce and the Chan merge run on a side stream, overlapping values/GAE/update
             with torch.cuda.stream(side):
-                self._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"], count_uniform=True)
+                self._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"], count_uniform=True, extra=ep_extra)
                 stats_done = torch.cuda.Event()
                 stats_done.record(side)
         else:
-            self._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"], count_uniform=True)
+            self._merge_stats(ro["count"], ro["s1"], ro["s2"], ro["shift"], count_uniform=True, extra=ep_extra)
         if p.obs_norm_update == "step" and hasattr(eng, "after_stats_merge"):
             eng.after_stats_merge()
         tm.stop("obs_stats")
@@ -234,9 +238,10 @@ class DPPOWorker:
         ep2 = ro.get("ep2")
         flat = None
         if ep2 is not None and hasattr(eng, "pack_metrics") and getattr(eng, "_loss_dev", None) is not None:
-            # GPU engine: all-reduce the [return sum, count] pair in place (R5), then one launch
-            # packs it with the loss sums and the gradient norm
-            flat = eng.pack_metrics(self.ctx.allreduce_tensor_(ep2))
+            # GPU engine: the [return sum, count] pair (R5) was summed over ranks with the
+            # observation moments (or is all-reduced here), then one launch packs it with the
+            # loss sums and the gradient norm
+            flat = eng.pack_metrics(ep2 if ro.get("ep2_reduced") else self.ctx.allreduce_tensor_(ep2))
         if flat is not None:
             loss_dev = flat
         else:

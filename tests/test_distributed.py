@@ -110,6 +110,29 @@ def test_obs_stats_merge_equals_single_process_on_concatenated_stream(tmp_path):
         assert torch.allclose(s["md"], ref.mean_diff, rtol=1e-9)
 
 
+def _worker_moments_extra(rank, world, port, out_dir):
+    ctx = _init(rank, world, port)
+    g = torch.Generator().manual_seed(7 + rank)
+    s1, s2 = torch.randn(5, generator=g, dtype=torch.float64), torch.rand(5, generator=g, dtype=torch.float64)
+    ep = torch.tensor([10.0 * (rank + 1), float(rank + 2)], dtype=torch.float64)
+    c, r1, r2 = ctx.allreduce_obs_moments(64.0, s1, s2, count_uniform=True, extra=ep)
+    torch.save({"s1": s1, "s2": s2, "c": c, "r1": r1, "r2": r2, "ep": ep}, os.path.join(out_dir, f"m{rank}.pt"))
+    ctx.destroy()
+
+
+def test_episode_stats_ride_on_the_moment_allreduce(tmp_path):
+    """R2 + R5 in ONE collective: the episode [return sum, count] appended to the moment
+    all-reduce come back summed over ranks, in place, and the moments are unchanged by it."""
+    assert _join(_spawn(_worker_moments_extra, 3, str(tmp_path)), 120) == [0, 0, 0]
+    ms = [torch.load(tmp_path / f"m{r}.pt", weights_only=True) for r in range(3)]
+    s1 = sum(m["s1"] for m in ms)
+    s2 = sum(m["s2"] for m in ms)
+    for m in ms:
+        assert m["c"] == 64.0 * 3
+        assert torch.allclose(m["r1"], s1) and torch.allclose(m["r2"], s2)
+        assert torch.equal(m["ep"], torch.tensor([60.0, 9.0], dtype=torch.float64))
+
+
 def _worker_fault(rank, world, port, out_dir):
     ctx = _init(rank, world, port, timeout=20.0)
     if rank == 1:

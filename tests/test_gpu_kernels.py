@@ -534,6 +534,14 @@ def test_rccl_world1_allreduce_and_training_step():
         m = w.iteration_step()
         assert m["replicas_in_sync"] is True
         assert math.isfinite(m["loss"]) and m["updates"] == 4
+        # the episode [return sum, count] rode on the moments' RCCL all-reduce (identity at
+        # world 1): the packed metrics hold exactly the rollout's sums
+        m = w.iteration_step()
+        ep = w.engine.ep_sum.tolist()
+        assert torch.equal(w.engine.metrics_buf[:2], w.engine.ep_sum)
+        assert m["ep_count"] == ep[1]
+        if ep[1] > 0:
+            assert m["mean_ep_return"] == pytest.approx(ep[0] / ep[1])
     finally:
         dist.destroy_process_group()
 
