@@ -4,6 +4,10 @@ source tree (ops/_build.py --variant NAME --src DIR), interleaved in one process
 geometry (Humanoid dims, 4096 envs x 16 steps).  Diagnostics.
 
     python scripts/ab_rollout.py VARIANT [dtype] [reps]
+
+Before timing, one rollout from the same env state through each build: every buffer it writes
+(observation rows, x^T operand, actions, log-probs, rewards, dones, moments, episode stats, env
+state) must be bitwise identical ("bitwise_equal" in the output) for a layout-only change.
 """
 import json
 import os
@@ -31,6 +35,16 @@ def main():
     w.iteration_step()
     eng = w.engine
     exts = {"cur": eng.ext, var: native.load_variant(var)}
+    sd = eng.env.state_dict()
+    outs = {}
+    for k, e in exts.items():
+        eng.ext = e
+        eng.env.load_state_dict(sd)
+        eng.rollout()
+        torch.cuda.synchronize()
+        outs[k] = [t.clone() for t in (eng.x_buf, eng.xT, eng.actions, eng.logp, eng.rewards, eng.dones, eng.mom,
+                                       eng.epstat, eng.env.state, eng.env.ep_len, eng.env.ep_ret)]
+    same = all(torch.equal(a, b) for a, b in zip(outs["cur"], outs[var]))
     res = {k: [] for k in exts}
     for _ in range(3):
         for k, e in exts.items():
@@ -45,7 +59,7 @@ def main():
             torch.cuda.synchronize()
             res[k].append(s.elapsed_time(t) / reps * 1e3)
     eng.ext = exts["cur"]
-    print(json.dumps({"dtype": dtype, **{k: min(v) for k, v in res.items()}, "all": res}))
+    print(json.dumps({"dtype": dtype, "bitwise_equal": same, **{k: min(v) for k, v in res.items()}, "all": res}))
 
 
 if __name__ == "__main__":
