@@ -217,6 +217,18 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
       }
     }
     if (last) break;
+    // (env, step) key prefixes of the sample / env phases, shared by every dim of the step:
+    // hashed by the last wave's lanes (idle in the narrow policy layers) before fc1, so the
+    // layers' barriers publish them and the sample phase needs no barrier of its own (the
+    // previous step's env phase, their last reader, ended in a barrier)
+    const uint32_t kstep = a.t0 + (uint32_t)step;
+    if (tid >= NTHR - ROWS) {
+      const int r = tid - (NTHR - ROWS);
+      const uint32_t e = (uint32_t)(e0 + r);
+      kes[r] = key_es(a.key_action, e, kstep);
+      kes[ROWS + r] = key_es(a.key_env, e, kstep);
+      kes[2 * ROWS + r] = key_es(a.key_reset, e, kstep);
+    }
     PH(0);   // (a) observe -> after its barrier
     // ---- (b) policy MLP ----
     layer_gemm<DT, ROWS, NW, EPI_TANH, true>(xs, ld1, a.d1, W1, a.n1, h1, ld2, sc1, wave, lane, nullptr, 0, 0, 0, &pf);
@@ -232,14 +244,6 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
     __syncthreads();
     PH(3);   // fc1, fc2, fc3 (each incl. barrier)
     // ---- (c) sample a = mu + sigma * eps (one Box-Muller pair -> two action dims) ----
-    const uint32_t kstep = a.t0 + (uint32_t)step;
-    if (tid < ROWS) {   // (env, step) key prefixes, shared by every dim of the step
-      const uint32_t e = (uint32_t)(e0 + tid);
-      kes[tid] = key_es(a.key_action, e, kstep);
-      kes[ROWS + tid] = key_es(a.key_env, e, kstep);
-      kes[2 * ROWS + tid] = key_es(a.key_reset, e, kstep);
-    }
-    __syncthreads();
     const int npa = (A + 1) >> 1;
     for (int i = tid; i < ROWS * npa; i += NTHR) {
       const int r = i / npa, q = i - r * npa;
