@@ -37,16 +37,19 @@ def _check(d: dict, n: int, variants: list) -> None:
 
 
 def test_bench_json_line_one_gpu():
-    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", *TINY, "--variants", "bf16"], cwd=ROOT,
+    from pytorch_dppo_amd.runtime.launcher import free_port
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))   # its world-1 RCCL group
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", *TINY, "--variants", "bf16"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     _check(_json_line(r.stdout), 1, ["bf16"])
 
 
 def test_bench_json_line_two_ranks():
+    from pytorch_dppo_amd.runtime.launcher import free_port
     env = dict(os.environ, DPPO_DIST_BACKEND="gloo")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29681", "bench.py", "--gpus", "2", *TINY,
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", *TINY,
                         "--variants", "", "--verify-sync"], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
