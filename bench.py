@@ -5,6 +5,11 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Both forms run N ranks: without a torchrun world (no WORLD_SIZE) and N > 1 the first form
+starts the N ranks itself as a child torch.distributed.run tree and exits with its status; under
+torchrun WORLD_SIZE must equal --gpus and every local rank needs its own GPU (RCCL), else the
+bench exits non-zero instead of reporting a different world as N GPUs.
+
 One DPPO worker per GPU (one process per GPU, RCCL over xGMI).  A *step* is one full DPPO
 iteration of the reference algorithm on every worker (train.py:60-178 + chief.py):
 rollout of T x E = 16 x 4096 = 65,536 env steps (Humanoid-v2 dims: obs 376, act 17, synthetic
@@ -27,6 +32,8 @@ samples it): it is diagnostics, and each timed event record idles the GPU ~10 us
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -45,6 +52,43 @@ METRIC = "env steps/sec (whole node), MuJoCo Humanoid-v2, 8 DPPO workers"
 BASELINE_VALUE = 1.6e3
 # JSON "dtype" labels: bf16x3 IS fp32-accurate compute (split-bf16 operands, fp32 accumulate)
 DTYPE_LABEL = {"bf16x3": "fp32_3xbf16", "fp32": "fp32", "bf16": "bf16", "fp8": "fp8_e4m3_fwd+bf16_update"}
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``python bench.py --gpus N`` without a torchrun world: start the N ranks as ONE child
+    process tree (torch.distributed.run, rendezvous on 127.0.0.1) and return its exit status.
+    Runs before this process touches the GPU (no HIP call, no exec: the parent only waits), the
+    way the reference's main.py:68-71 spawns its N workers."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # RCCL over dmabuf IPC on this host driver
+    print(f"bench: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
+def check_world(gpus: int) -> None:
+    """a torchrun world must be the one --gpus names, with a device per local rank (RCCL: one
+    process per GPU).  ``DPPO_DIST_BACKEND=gloo`` (diagnostics: ranks sharing one GPU) skips the
+    device count."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {gpus}: refusing to report a "
+                         f"{world}-rank run as {gpus} GPUs")
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    ndev = torch.cuda.device_count()
+    if os.environ.get("DPPO_DIST_BACKEND", "nccl") == "nccl" and ndev < local:
+        raise SystemExit(f"bench: {local} local ranks but only {ndev} visible GPU(s) (RCCL needs one "
+                         f"process per GPU)")
 
 
 def main():
@@ -79,6 +123,14 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the N-GPU node run from a plain `python bench.py --gpus N`: N child ranks, this process
+        # exits with their status (it never initialises the GPU itself)
+        ndev = torch.cuda.device_count()
+        if os.environ.get("DPPO_DIST_BACKEND", "nccl") == "nccl" and ndev < args.gpus:
+            raise SystemExit(f"bench: --gpus {args.gpus} but only {ndev} visible GPU(s)")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    check_world(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         ctx = init_distributed("gpu")
@@ -149,6 +201,9 @@ def main():
                           "global_batch": rows * ctx.world_size, "seq_len": T,
                           "parallelism": f"dp{ctx.world_size}", "env": args.env_name,
                           "dppo_workers": ctx.world_size, "workers_per_gpu": 1, "num_envs_per_gpu": E,
+                          "dist_backend": ctx.backend,
+                          "rccl_world_size": (dist.get_world_size() if dist.is_initialized()
+                                              and ctx.backend == "nccl" else 0),
                           "rollout_len": T, "num_epoch": args.num_epoch,
                           "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout, "graphs": args.graphs,
                           "grad_buckets": bucketed,

@@ -226,6 +226,7 @@ MlpArgs base_mlp(int dt, const Layout& L, const std::vector<double>& scales, tor
     TORCH_CHECK(row0 >= 0 && row0 + M <= limit, "row range out of x_buf / per-row arrays");
   }
   a.x_buf = x_buf.data_ptr();
+  a.x_bytes = (int64_t)x_buf.numel() * (int64_t)x_buf.element_size();
   a.row0 = (int)row0;
   a.M = (int)M;
   a.W = wimg.data_ptr();
@@ -323,11 +324,12 @@ int64_t train_lds_bytes(int64_t dt, std::vector<int64_t> layout, int64_t A) {
   return train_lds_bytes_impl((int)dt, parse_layout(layout), A);
 }
 
-int64_t train_rows(int64_t dt, std::vector<int64_t> layout, int64_t A) {
+int64_t train_rows(int64_t dt, std::vector<int64_t> layout, int64_t A, int64_t x_bytes) {
   const Layout L = parse_layout(layout);
   MlpArgs a{};
   for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
   a.A = (int)A;
+  a.x_bytes = x_bytes;   // the row tile depends on which kernel the buffer admits
   return mlp_train_rows((int)dt, a);
 }
 

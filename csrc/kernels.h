@@ -86,6 +86,7 @@ struct MlpArgs {
                           // transposed stores, bit1 skip v_fc1, bit2 skip dgrad chain, bit3 skip loss,
                           // bit4 skip the observation loads (zero X tile)
   int x_stream;           // 1: non-temporal observation-row loads (A/B knob; 0 default: cached)
+  int64_t x_bytes;        // bytes of x_buf (kernels with 32-bit buffer offsets refuse >= 2 GiB)
   float* part;            // [nblk][NPART] per-workgroup partial sums (loss terms, dlog_std)
   int npart;
   // DIAGNOSTIC ONLY (scripts/phase_timeline.py; null in every real run): per-wave s_memtime

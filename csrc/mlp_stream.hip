@@ -929,6 +929,10 @@ void rs_launch(const MlpArgs& a, hipStream_t s) {
 // shape runs the 32-row tile kernel
 extern "C" int mlp_rs_applies(const MlpArgs& a) {
   if (!g_rs_enable) return 0;
+  // the observation gather uses a raw buffer resource with 32-bit per-lane byte offsets: an
+  // x_buf of 2 GiB or more (e.g. > 1.4 M Humanoid rows at split-bf16) takes the tile kernel,
+  // whose row loads use 64-bit addresses
+  if (a.x_bytes >= ((int64_t)1 << 31)) return 0;
   return a.d_in[0] <= 384 && a.d_in[0] == a.d_in[3] && (a.n_out[0] + 15) / 16 == P1 &&
          (a.n_out[3] + 15) / 16 == V1 && a.d_in[1] == 128 && a.d_in[4] == 512 && a.d_in[2] == 128 &&
          a.d_in[5] == 128 && a.d_out[1] == 128 && a.d_out[4] == 128 && a.d_out[2] == 32 && a.d_out[5] == 32 &&

@@ -12,20 +12,33 @@ namespace {
 // 64-thread workgroups (E/64 of them, spread over more CUs than E/256), and the loads of 8
 // steps are issued before their part of the recurrence (same arithmetic in the same order): the
 // step-at-a-time loop was a chain of T dependent load round trips per lane.
-// seg > 0: the reference's segment length num_steps (train.py:82) — after every seg steps the
-// recursion restarts (A_{t+1} masked) while the not-done bootstrap V_{t+1} stays in delta.
+// seg > 0: the reference's segment length num_steps (train.py:82-106): a segment ends at a done
+// or after seg steps, and the next one starts fresh — so after the last done t_d before t the
+// segments are [t_d+1, t_d+1+seg), ...  A segment that ends by length without a done restarts the
+// recursion (A_{t+1} masked) while the not-done bootstrap V_{t+1} stays in delta.  The cut flags
+// depend on the dones BEFORE t, so a forward pass over the env's dones writes them into adv (as
+// scratch: each element is read back by the same thread before the reverse pass overwrites it).
+DEV bool seg_cut(int t, int td, int seg, float d) { return d == 0.f && (t - td) % seg == 0; }
 __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ rew, const float* __restrict__ val,
                                                  const float* __restrict__ done, float* __restrict__ adv,
                                                  float* __restrict__ ret, int T, int E, float gamma, float lam,
                                                  int seg) {
   const int e = blockIdx.x * 64 + threadIdx.x;
   if (e >= E) return;
+  if (seg > 0) {
+    int td = -1;
+    for (int t = 0; t < T; ++t) {
+      const size_t o = (size_t)t * E + e;
+      const float d = done[o];
+      adv[o] = seg_cut(t, td, seg, d) ? 0.f : 1.f;   // continuation factor of A_{t+1}
+      if (d != 0.f) td = t;
+    }
+  }
   float nxt = 0.f;
   float vnext = val[(size_t)T * E + e];
-  auto step = [&](int t, size_t o, float r, float v, float d) {
+  auto step = [&](size_t o, float r, float v, float d, float cont) {
     const float nt = 1.f - d;
     const float delta = r + gamma * vnext * nt - v;
-    const float cont = (seg > 0 && (t + 1) % seg == 0) ? 0.f : 1.f;
     nxt = delta + gamma * lam * nt * cont * nxt;
     adv[o] = nxt;
     ret[o] = nxt + v;
@@ -33,20 +46,21 @@ __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ rew, 
   };
   int t = T - 1;
   for (; t >= 7; t -= 8) {
-    float r[8], v[8], d[8];
+    float r[8], v[8], d[8], c[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const size_t o = (size_t)(t - k) * E + e;
       r[k] = rew[o];
       v[k] = val[o];
       d[k] = done[o];
+      c[k] = seg > 0 ? adv[o] : 1.f;
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) step(t - k, (size_t)(t - k) * E + e, r[k], v[k], d[k]);
+    for (int k = 0; k < 8; ++k) step((size_t)(t - k) * E + e, r[k], v[k], d[k], c[k]);
   }
   for (; t >= 0; --t) {
     const size_t o = (size_t)t * E + e;
-    step(t, o, rew[o], val[o], done[o]);
+    step(o, rew[o], val[o], done[o], seg > 0 ? adv[o] : 1.f);
   }
 }
 
@@ -63,14 +77,37 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float* __restrict__
                                                        float* __restrict__ ret, int T, int E, float gamma,
                                                        float lam, int seg) {
   __shared__ float sD[256], sC[256];
+  __shared__ int sT[256];
   const int e = blockIdx.x, j = threadIdx.x;
   const int chunk = (T + 255) / 256;
   const int t0 = min(T, j * chunk), t1 = min(T, t0 + chunk);
+  if (seg > 0) {
+    // the last done before this chunk: an exclusive max-scan of the chunks' last dones, then a
+    // forward pass over the chunk writes its cut flags into adv (scratch, see seg_cut)
+    int last = -1;
+    for (int t = t0; t < t1; ++t)
+      if (done[(size_t)t * E + e] != 0.f) last = t;
+    sT[j] = last;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+      const int o = j >= off ? sT[j - off] : -1;
+      __syncthreads();
+      sT[j] = max(sT[j], o);
+      __syncthreads();
+    }
+    int td = j > 0 ? sT[j - 1] : -1;
+    for (int t = t0; t < t1; ++t) {
+      const size_t o = (size_t)t * E + e;
+      const float d = done[o];
+      adv[o] = seg_cut(t, td, seg, d) ? 0.f : 1.f;
+      if (d != 0.f) td = t;
+    }
+  }
   auto delta_c = [&](int t, float& delta, float& c) {
     const size_t o = (size_t)t * E + e;
     const float nt = 1.f - done[o];
     delta = rew[o] + gamma * val[o + E] * nt - val[o];
-    c = (seg > 0 && (t + 1) % seg == 0) ? 0.f : gamma * lam * nt;
+    c = gamma * lam * nt * (seg > 0 ? adv[o] : 1.f);
   };
   float D = 0.f, C = 1.f;
   for (int t = t1 - 1; t >= t0; --t) {

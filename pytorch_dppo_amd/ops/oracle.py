@@ -43,19 +43,29 @@ def gae(rewards: torch.Tensor, values: torch.Tensor, dones: torch.Tensor, gamma:
 
     ``values`` is [T+1,E] (row T = bootstrap V(s_T)); ``dones[t]`` = episode ended at step t
     (so V_{t+1} and A_{t+1} are masked, which is the reference's segment break + R=0).
-    ``segment`` > 0 (the reference's ``num_steps``, train.py:82 / ppo.py:87): a segment also
-    ends after every ``segment`` steps — there the recursion restarts (A_{t+1} masked) while
-    the bootstrap V_{t+1} of the not-done state is kept (train.py:109-112 per segment).
+    ``segment`` > 0 (the reference's ``num_steps``, train.py:82-106 / ppo.py:87): a segment
+    ends at a done OR after ``segment`` steps, and the next segment starts fresh (its step count
+    restarts after a done).  Where a segment ends by length without a done the recursion
+    restarts (A_{t+1} masked) while the bootstrap V_{t+1} of the not-done state is kept
+    (train.py:109-112 per segment).
     Returns (advantages [T,E], returns [T,E]) with returns = A + V.
     """
     T = rewards.shape[0]
+    cont = torch.ones_like(rewards)
+    if segment > 0:
+        # forward: steps since the current segment started, per env (train.py:82 `for step`)
+        s = torch.zeros_like(rewards[0], dtype=torch.int64)
+        for t in range(T):
+            d = dones[t] != 0
+            end_len = (s + 1 == segment) & ~d
+            cont[t] = torch.where(end_len, torch.zeros_like(cont[t]), cont[t])
+            s = torch.where(d | (s + 1 == segment), torch.zeros_like(s), s + 1)
     adv = torch.zeros_like(rewards)
     nxt = torch.zeros_like(rewards[0])
     for t in range(T - 1, -1, -1):
         nonterm = 1.0 - dones[t].to(rewards.dtype)
         delta = rewards[t] + gamma * values[t + 1] * nonterm - values[t]
-        cont = 0.0 if (segment > 0 and (t + 1) % segment == 0) else 1.0
-        nxt = delta + gamma * lam * nonterm * cont * nxt
+        nxt = delta + gamma * lam * nonterm * cont[t] * nxt
         adv[t] = nxt
     return adv, adv + values[:T]
 

@@ -354,7 +354,8 @@ class HipEngine:
     def sync_tile(self) -> None:
         """Row tile of the fused update kernel (64 rows when the layer set fits LDS, else 32;
         16 at fp32) and the partial-sum rows it produces; re-query after ext.set_mlp_rows."""
-        self.train_rows = int(self.ext.train_rows(self.dt, self.layout, self.A))
+        xb = self.x_buf.numel() * self.x_buf.element_size()
+        self.train_rows = int(self.ext.train_rows(self.dt, self.layout, self.A, xb))
         self.ntrain_blk = self.ldT // self.train_rows
 
     def params_changed(self) -> None:
@@ -399,6 +400,10 @@ class HipEngine:
 
     def load_env_state(self, d: Dict) -> None:
         self.env.load_state_dict(d)
+        if self.host_env:
+            # the host envs were restored (and reset): the next rollout acts on their observation,
+            # not on the one the constructor's reset left (TorchEngine.load_env_state does the same)
+            self._host_obs = self.env.observe().to(self.device, torch.float32)
 
     # ------------------------------------------------------------------------------------------
     def _launch_rollout(self, T: int, t_base: int, t0: int, norm: RunningObsStats, shift: torch.Tensor,
@@ -479,10 +484,17 @@ class HipEngine:
         one-launch moment/episode-stat reduce runs there, ordered after the rollout kernel, so
         it (and the caller's merge, issued on the same stream) overlaps the value forward and
         the update; the caller orders its stream after that work before reading the stats."""
+        # fp8: the weights changed during the previous update (Adam rewrites only the bf16 image);
+        # before either path, so values() / GAE of a host-env rollout see the current weights too
+        self.refresh_fwd_image()
         if self.host_env:
-            return self._rollout_host()
+            ro = self._rollout_host()
+            if stats_stream is not None:
+                # the caller merges the moments on stats_stream: order it after the host rollout's
+                # device work, which produced them (and reads the stats the merge overwrites)
+                stats_stream.wait_stream(torch.cuda.current_stream(self.device))
+            return ro
         p = self.p
-        self.refresh_fwd_image()   # fp8: weights changed during the previous update
         if p.obs_norm_update == "rollout":
             # the shift IS the fp32 mean, no snapshot copy: its readers are the rollout kernel
             # and obs_merge, which reads shift[d] before writing mean_f32[d] in the same thread

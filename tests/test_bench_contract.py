@@ -1,7 +1,9 @@
 """bench.py output contract (the driver parses this line): one JSON line from rank 0 with the
 BASELINE metric, the whole-job value over all ranks, and the timing fields — at a tiny geometry,
-on one GPU and as 2 torchrun ranks sharing it (gloo; RCCL refuses two ranks on one device, the
-driver's N-GPU runs use RCCL through the same code path)."""
+on one GPU and as 2 ranks sharing it (gloo; RCCL refuses two ranks on one device, the driver's
+N-GPU runs use RCCL through the same code path), launched by torchrun AND by a plain
+``python bench.py --gpus 2`` (bench.py starts the ranks itself).  The world checks (WORLD_SIZE
+must equal --gpus, one GPU per RCCL rank) run before any GPU call, so they are tested on CPU."""
 import json
 import os
 import subprocess
@@ -9,7 +11,6 @@ import sys
 
 import pytest
 
-pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TINY = ["--num-envs", "64", "--rollout-len", "4", "--num-epoch", "2", "--steps", "2", "--warmup", "1"]
@@ -36,6 +37,7 @@ def _check(d: dict, n: int, variants: list) -> None:
     assert sorted(d["variants"]) == sorted(variants)
 
 
+@pytest.mark.gpu
 def test_bench_json_line_one_gpu():
     from pytorch_dppo_amd.runtime.launcher import free_port
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))   # its world-1 RCCL group
@@ -45,6 +47,7 @@ def test_bench_json_line_one_gpu():
     _check(_json_line(r.stdout), 1, ["bf16"])
 
 
+@pytest.mark.gpu
 def test_bench_json_line_two_ranks():
     from pytorch_dppo_amd.runtime.launcher import free_port
     env = dict(os.environ, DPPO_DIST_BACKEND="gloo")
@@ -55,3 +58,58 @@ def test_bench_json_line_two_ranks():
     assert r.returncode == 0, r.stderr[-3000:]
     _check(_json_line(r.stdout), 2, [])
     assert "replicas_in_sync True" in r.stderr
+
+
+@pytest.mark.gpu
+def test_plain_bench_gpus_two_launches_two_ranks():
+    """the driver's form `python bench.py --gpus N` (no torchrun): bench.py starts N ranks itself"""
+    env = dict(os.environ, DPPO_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY, "--variants", "", "--verify-sync"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    _check(d, 2, [])
+    assert d["config"]["dist_backend"] == "gloo"
+    assert "replicas_in_sync True" in r.stderr
+    assert "launching 2 ranks" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_one_gpu_reports_rccl_world():
+    from pytorch_dppo_amd.runtime.launcher import free_port
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    r = subprocess.run([sys.executable, "bench.py", *TINY, "--variants", ""], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 1 and d["config"]["rccl_world_size"] == 1 and d["config"]["dist_backend"] == "nccl"
+
+
+def _bench_fails(args, extra_env):
+    env = dict(os.environ, **extra_env)
+    r = subprocess.run([sys.executable, "bench.py", *args, *TINY], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")], "no JSON line on a refused run"
+    return r.stderr
+
+
+def test_bench_refuses_world_size_mismatch():
+    """a torchrun world of 2 launched as --gpus 4 must not be reported as 4 GPUs (CPU: the check
+    runs before any GPU call)"""
+    err = _bench_fails(["--gpus", "4"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0",
+                                         "LOCAL_WORLD_SIZE": "2"})
+    assert "WORLD_SIZE=2 but --gpus 4" in err
+
+
+def test_bench_refuses_more_rccl_ranks_than_gpus():
+    """RCCL needs one GPU per local rank: on a box with fewer visible GPUs, plain --gpus N and a
+    torchrun world both exit non-zero before starting anything"""
+    import torch
+    n = max(2, torch.cuda.device_count() + 1)
+    err = _bench_fails(["--gpus", str(n)], {"DPPO_DIST_BACKEND": "nccl"})
+    assert f"--gpus {n} but only" in err
+    err = _bench_fails(["--gpus", str(n)], {"DPPO_DIST_BACKEND": "nccl", "WORLD_SIZE": str(n), "RANK": "0",
+                                            "LOCAL_RANK": "0", "LOCAL_WORLD_SIZE": str(n)})
+    assert "visible GPU" in err

@@ -138,3 +138,45 @@ def test_hip_engine_host_env_path_matches_torch_engine(dtype):
     w = DPPOWorker(p, DistContext(device=dev))
     m = w.iteration_step()
     assert math.isfinite(m["loss"]) and m["updates"] == 2
+
+
+@pytest.mark.gpu
+def test_hip_engine_host_env_fp8_refreshes_forward_image():
+    """fp8 + host env: Adam rewrites only the bf16 image, so the rollout must refresh the e4m3
+    forward image (and its scales) before the host path too — values() / GAE then use the current
+    weights."""
+    from pytorch_dppo_amd.parallel.dist import DistContext
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    dev = torch.device("cuda", 0)
+    p = dppo_preset(device="gpu", env_backend="gym", env_name="FakeGym-v0", num_envs=16, exploration_size=16 * 8,
+                    batch_size=16 * 8, num_epoch=2, dtype="fp8", seed=3)
+    w = DPPOWorker(p, DistContext(device=dev))
+    w.iteration_step()
+    eng = w.engine
+    eng.rollout()
+    img, q = eng.wimg_fwd.clone(), eng.qscale.clone()
+    eng.refresh_fwd_image()
+    assert torch.equal(img, eng.wimg_fwd) and torch.equal(q, eng.qscale)
+
+
+@pytest.mark.gpu
+def test_hip_engine_host_env_resume_refreshes_observation():
+    """after load_env_state the next host rollout acts on the restored envs' observation"""
+    from pytorch_dppo_amd.models.actor_critic import ActorCritic
+    from pytorch_dppo_amd.runtime.engine_hip import HipEngine
+    from pytorch_dppo_amd.utils.obs_stats import RunningObsStats
+    dev = torch.device("cuda", 0)
+    p = dppo_preset(device="gpu", env_backend="gym", env_name="FakeGym-v0", num_envs=16, exploration_size=16 * 4,
+                    batch_size=16 * 4, num_epoch=1, dtype="bf16x3", seed=3)
+    engs = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        env = make_vec_env(None, p.num_envs, seed=p.seed, backend="gym", name="FakeGym-v0")
+        st = RunningObsStats(5, dev)
+        eng = HipEngine(p, ActorCritic(5, 2).to(dev), env, st, dev, 0)
+        st.observes(eng.current_obs())
+        engs.append(eng)
+    a, b = engs
+    a.rollout()
+    b.load_env_state(a.env_state())
+    assert torch.equal(b.current_obs().cpu(), b.env.observe().float())

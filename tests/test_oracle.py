@@ -56,16 +56,22 @@ def test_gae_segment_length_matches_reference_num_steps_segments(seg):
     d[7, 0] = d[22, 0] = d[39, 1] = d[0, 2] = d[11, 2] = 1.0
     adv, ret = oracle.gae(r, v, d, 0.99, 0.95, segment=seg)
     for e in range(E):
+        # the reference's segment loop literally (train.py:69-106): `for step in range(num_steps)`
+        # with a `break` at done, then the next segment starts fresh
         start = 0
-        for t in range(T):
-            if d[t, e] > 0 or t == T - 1 or (t + 1) % seg == 0:
-                end = t + 1
-                boot = 0.0 if d[t, e] > 0 else float(v[end, e])
-                a_ref, r_ref = _gae_reference_loop(r[start:end, e].tolist(), v[start:end, e].tolist() + [boot],
-                                                   0.99, 0.95)
-                assert torch.allclose(adv[start:end, e], torch.tensor(a_ref, dtype=torch.float64))
-                assert torch.allclose(ret[start:end, e], torch.tensor(r_ref, dtype=torch.float64))
-                start = end
+        while start < T:
+            t = start
+            for step in range(seg):
+                t = start + step
+                if t == T - 1 or d[t, e] > 0:
+                    break
+            end = t + 1
+            boot = 0.0 if d[t, e] > 0 else float(v[end, e])
+            a_ref, r_ref = _gae_reference_loop(r[start:end, e].tolist(), v[start:end, e].tolist() + [boot],
+                                               0.99, 0.95)
+            assert torch.allclose(adv[start:end, e], torch.tensor(a_ref, dtype=torch.float64))
+            assert torch.allclose(ret[start:end, e], torch.tensor(r_ref, dtype=torch.float64))
+            start = end
 
 
 def test_inert_reference_knobs_warn():
