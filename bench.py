@@ -108,11 +108,9 @@ def main():
                          "(reported under 'variants'; '' = none)")
     ap.add_argument("--batch-size", type=int, default=0, help="0 = full buffer (reference DPPO)")
     ap.add_argument("--overlap-rollout", action="store_true",
-                    help="overlap the final gradient all-reduce with the next rollout (1-update lag)")
+                    help="the last value-head all-reduce + Adam overlap the next rollout (exact: the rollout reads only the policy)")
     ap.add_argument("--graphs", action="store_true",
                     help="replay the per-minibatch launch chains as hipGraphs (use_graphs)")
-    ap.add_argument("--grad-buckets", default="off", choices=["auto", "on", "off"],
-                    help="bucketed gradient all-reduce overlapping the wgrad (auto: multi-rank)")
     ap.add_argument("--force-collectives", action="store_true",
                     help="diagnostics: run the hot-path RCCL collectives even at world size 1")
     ap.add_argument("--phase-timing", type=int, default=0,
@@ -147,7 +145,7 @@ def main():
         p = dppo_preset(device="gpu", env_name=args.env_name, num_envs=E, exploration_size=rows,
                         batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=dtype,
                         num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
-                        use_graphs=args.graphs, grad_buckets=args.grad_buckets,
+                        use_graphs=args.graphs,
                         phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
         w = DPPOWorker(p, ctx)
         m = {}
@@ -183,7 +181,7 @@ def main():
     elapsed, p, w, m = run(args.dtype)
     total_steps = rows * ctx.world_size * args.steps
     value = total_steps / elapsed
-    bucketed = bool(w.bucketed)
+    heads = bool(getattr(w.engine, "heads", False))
     del w
     variants = {}
     for dt in [d for d in args.variants.split(",") if d and d != args.dtype]:
@@ -206,7 +204,7 @@ def main():
                                               and ctx.backend == "nccl" else 0),
                           "rollout_len": T, "num_epoch": args.num_epoch,
                           "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout, "graphs": args.graphs,
-                          "grad_buckets": bucketed,
+                          "per_head_chains": heads,
                           "note": ("value = total env steps/s of all n_gpus workers (one DPPO worker per GPU); "
                                    "the 8-worker node figure of the metric is the n_gpus=8 run; vs_baseline "
                                    "divides by the reference's derived 8-worker CPU node estimate (BASELINE.md)"),

@@ -265,7 +265,10 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   check(actions, "actions", at::kFloat, A);
   const int64_t nrows = actions.numel() / A;
   MlpArgs a = base_mlp((int)dt, L, scales, x_buf, idx, row0, M, wimg, flat, A, check_idx, nrows);
-  TORCH_CHECK(opts.size() == 5, "opts: loss_kind, value_loss, std_var, first_step, npart");
+  TORCH_CHECK(opts.size() == 5 || opts.size() == 6, "opts: loss_kind, value_loss, std_var, first_step, npart[, head]");
+  // head >= 0: one head's per-head streaming kernel (csrc/mlp_head.hip; 0 policy, 1 value)
+  const int head = opts.size() == 6 ? (int)opts[5] : -1;
+  TORCH_CHECK(head >= -1 && head <= 1, "head: -1 (both heads, one kernel), 0 policy, 1 value");
   TORCH_CHECK(fopts.size() == 2, "fopts: clip, ent_coeff");
   TORCH_CHECK(tbufs.size() == 11, "11 transposed buffers");
   check(logp_old, "logp_old", at::kFloat, nrows);
@@ -275,8 +278,10 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   check(mu_prev, "mu_prev", at::kFloat, nrows * A);
   check(v_prev, "v_prev", at::kFloat, nrows);
   check(log_std_old, "log_std_old", at::kFloat, A);
-  const int ROWS = mlp_train_rows((int)dt, a);
-  TORCH_CHECK(train_lds_bytes_impl((int)dt, L, A) <= 160 * 1024, "mlp_train tile does not fit LDS");
+  if (head >= 0)
+    TORCH_CHECK(dt == 3 && mlp_head_applies(a), "the per-head kernels cover split-bf16 and the reference network only");
+  const int ROWS = head >= 0 ? mlp_head_rows() : mlp_train_rows((int)dt, a);
+  TORCH_CHECK(head >= 0 || train_lds_bytes_impl((int)dt, L, A) <= 160 * 1024, "mlp_train tile does not fit LDS");
   const int64_t Mpad = ((M + ROWS - 1) / ROWS) * ROWS;
   TORCH_CHECK(ldT >= Mpad && ldT % 32 == 0, "ldT must cover M padded to the row tile and be a multiple of 32");
   // rows each transposed buffer must hold (writer side)
@@ -284,7 +289,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
                             L.n_out[0], L.n_out[1], L.n_out[2], L.n_out[3], L.n_out[4], L.n_out[5]};
   for (int i = 0; i < 11; ++i) check(tbufs[i], "transposed buffer", storage_type((int)dt), need[i] * ldT);
   const int npart = (int)opts[4];
-  TORCH_CHECK(npart >= 8 + A, "npart too small");
+  TORCH_CHECK(npart >= (head == 1 ? 8 : 8 + A), "npart too small");
   const int nblk = (int)(Mpad / ROWS);
   check(part, "part", at::kFloat, (int64_t)nblk * npart);
   a.log_std_old = log_std_old.data_ptr<float>();
@@ -310,14 +315,27 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   a.xT_ready = xT_ready ? 1 : 0;
   a.ablate = g_train_ablate;
   if (g_tstamp != nullptr) {
-    const int64_t nw = mlp_train_waves((int)dt, a);
+    const int64_t nw = head >= 0 ? 4 : mlp_train_waves((int)dt, a);
     TORCH_CHECK(g_tstamp_numel >= ((nblk + g_tstamp_every - 1) / g_tstamp_every) * nw * 16, "tstamp buffer too small");
     a.tstamp = g_tstamp;
     a.tstamp_every = g_tstamp_every;
   }
   a.part = part.data_ptr<float>();
-  launch_mlp_train((int)dt, a, cur_stream());
+  if (head >= 0) {
+    launch_mlp_head(head, a, cur_stream());
+  } else {
+    launch_mlp_train((int)dt, a, cur_stream());
+  }
   after_launch(__func__);
+}
+
+// the per-head kernels cover this (dtype, network); x_bytes is irrelevant to them (64-bit rows)
+bool head_applies(int64_t dt, std::vector<int64_t> layout, int64_t A) {
+  const Layout L = parse_layout(layout);
+  MlpArgs a{};
+  for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
+  a.A = (int)A;
+  return dt == 3 && mlp_head_applies(a) != 0;
 }
 
 int64_t train_lds_bytes(int64_t dt, std::vector<int64_t> layout, int64_t A) {
@@ -395,26 +413,32 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
 }
 
 // i_lo/i_hi: flat parameter range gathered from the slabs (-1, -1: [A, n)); with_partials: also
-// the log_std gradients and the loss sums (the range must then start at or after A)
+// the first nlog gradients (log_std) and the loss sums of the columns in loss_mask from the
+// per-workgroup partials (the slab range must then start at or after nlog).  grad / src_off /
+// src_meta may be one head's slice of the flat vectors.
 void grad_gather(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_meta, torch::Tensor part,
                  int64_t nblk, int64_t npart, int64_t A, double scale, torch::Tensor grad, torch::Tensor loss_out,
-                 int64_t i_lo, int64_t i_hi, bool with_partials) {
+                 int64_t i_lo, int64_t i_hi, bool with_partials, int64_t nlog, int64_t loss_mask) {
   const int64_t n = grad.numel();
-  if (i_lo < 0) i_lo = A;
+  if (nlog < 0) nlog = A;
+  if (i_lo < 0) i_lo = nlog;
   if (i_hi < 0) i_hi = n;
-  TORCH_CHECK(A <= i_lo && i_lo <= i_hi && i_hi <= n, "gather range must lie in [A, n)");
+  TORCH_CHECK(0 <= nlog && nlog <= A && (!with_partials || nlog <= i_lo) && i_lo <= i_hi && i_hi <= n,
+              "gather range must lie in [nlog, n)");
+  TORCH_CHECK(loss_mask >= 0 && loss_mask <= 255, "loss_mask");
   check(grad, "grad", at::kFloat, n);
   check(src_off, "src_off", at::kInt, n);
   check(src_meta, "src_meta", at::kInt, n);
   check(slab, "slab", at::kFloat, 1);
   check(part, "part", at::kFloat, nblk * npart);
   check(loss_out, "loss_out", at::kFloat, 8);
-  TORCH_CHECK(npart >= 8 + A, "npart");
+  TORCH_CHECK(npart >= 8 + (with_partials ? nlog : 0), "npart");
   // the (offset, chunks x stride) of every element lies inside its bucket's slab by
   // construction (HipEngine._build_wgrad_plan asserts it once; no per-epoch device sync here)
   launch_grad_gather(slab.data_ptr<float>(), src_off.data_ptr<int>(), src_meta.data_ptr<int>(),
-                     part.data_ptr<float>(), (int)nblk, (int)npart, (int)A, (float)scale, grad.data_ptr<float>(),
-                     (int)i_lo, (int)i_hi, with_partials ? 1 : 0, loss_out.data_ptr<float>(), cur_stream());
+                     part.data_ptr<float>(), (int)nblk, (int)npart, (int)nlog, (int)loss_mask, (float)scale,
+                     grad.data_ptr<float>(), (int)i_lo, (int)i_hi, with_partials ? 1 : 0, loss_out.data_ptr<float>(),
+                     cur_stream());
   after_launch(__func__);
 }
 
@@ -497,13 +521,17 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, do
   after_launch(__func__);
 }
 
-// grad_gather (partials pass + [A, n)) and the no-clip Adam step in one launch (world size 1:
-// nothing runs between them).  Bit-identical parameters to grad_gather -> adam(host_step).
+// grad_gather (partials pass + [nlog, n)) and the no-clip Adam step in one launch (world size 1:
+// nothing runs between them).  Bit-identical parameters to grad_gather -> adam(host_step).  The
+// flat tensors may be one head's slice (nlog = A for the policy slice that starts with log_std,
+// 0 for the value slice; loss_mask = the loss columns that head owns).
 void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_meta, torch::Tensor part,
                  int64_t npblk, int64_t npart, int64_t A, double scale, torch::Tensor loss_out, torch::Tensor g,
                  torch::Tensor p, torch::Tensor m, torch::Tensor v, double lr, double b1, double b2, double eps,
                  int64_t step, torch::Tensor state, torch::Tensor norm_part, torch::Tensor wimg, torch::Tensor w_map,
-                 torch::Tensor wt_map, int64_t dt, torch::Tensor qmul) {
+                 torch::Tensor wt_map, int64_t dt, torch::Tensor qmul, int64_t nlog, int64_t loss_mask) {
+  if (nlog < 0) nlog = A;
+  TORCH_CHECK(0 <= nlog && nlog <= A && loss_mask >= 0 && loss_mask <= 255, "nlog / loss_mask");
   const int64_t n = p.numel();
   check(p, "p", at::kFloat, n);
   check(g, "g", at::kFloat, n);
@@ -518,15 +546,16 @@ void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
   check(w_map, "w_map", at::kInt, n);
   check(wt_map, "wt_map", at::kInt, n);
   check(wimg, "wimg", storage_type((int)dt), 1);
-  TORCH_CHECK(npart >= 8 + A && A < n, "npart / A");
+  TORCH_CHECK(npart >= 8 + nlog && nlog < n, "npart / nlog");
   TORCH_CHECK(step >= 1, "gather_adam needs the host step number (eager launches only)");
   const int nblk = (int)norm_part.numel();
   check(norm_part, "norm_part", at::kFloat, nblk);
-  TORCH_CHECK(nblk > A + 8 && nblk <= 4096, "norm_part must hold more than A + 8 blocks");
+  TORCH_CHECK(nblk > nlog + 8 && nblk <= 4096, "norm_part must hold more than nlog + 8 blocks");
   const float* q = nullptr;
   if (qmul.defined() && qmul.numel() > 0) { check(qmul, "qmul", at::kFloat, n); q = qmul.data_ptr<float>(); }
   launch_gather_adam(slab.data_ptr<float>(), src_off.data_ptr<int>(), src_meta.data_ptr<int>(),
-                     part.data_ptr<float>(), (int)npblk, (int)npart, (int)A, (float)scale, loss_out.data_ptr<float>(),
+                     part.data_ptr<float>(), (int)npblk, (int)npart, (int)nlog, (int)loss_mask, (float)scale,
+                     loss_out.data_ptr<float>(),
                      g.data_ptr<float>(), p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (int)n,
                      (float)lr, (float)b1, (float)b2, (float)eps, (int)step, state.data_ptr<float>(),
                      norm_part.data_ptr<float>(), nblk, wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(),
@@ -576,6 +605,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rollout", &rollout);
   m.def("mlp_value", &mlp_value);
   m.def("mlp_train", &mlp_train);
+  m.def("head_applies", &head_applies);
+  m.def("head_rows", []() { return (int64_t)mlp_head_rows(); });
+  m.def("set_head_kernels", [](bool on) { set_head_kernels(on ? 1 : 0); });
+  m.def("head_kernels_enabled", []() { return head_kernels_enabled() != 0; });
   m.def("train_lds_bytes", &train_lds_bytes);
   m.def("train_rows", &train_rows);
   m.def("train_waves", &train_waves);

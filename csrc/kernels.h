@@ -98,6 +98,12 @@ struct MlpArgs {
 // row-stationary weight-streaming split-bf16 update (mlp_stream.hip): the default mlp_train
 // kernel for DT_S3 whenever the shapes fit its register tiles
 extern "C" int mlp_rs_applies(const MlpArgs& a);
+// per-head streaming update (csrc/mlp_head.hip): head 0 = policy, 1 = value; 128 rows per workgroup
+extern "C" int mlp_head_applies(const MlpArgs& a);
+extern "C" int mlp_head_rows();
+extern "C" void launch_mlp_head(int head, const MlpArgs& a, hipStream_t s);
+extern "C" void set_head_kernels(int enable);
+extern "C" int head_kernels_enabled();
 extern "C" size_t mlp_rs_lds_bytes();
 extern "C" void launch_mlp_train_rs(const MlpArgs& a, hipStream_t s);
 extern "C" void set_s3_stream(int enable, int stages, int dense);   // dense < 0: unchanged
@@ -143,8 +149,8 @@ void set_wgrad_stages(int st);                 // bf16 wgrad DMA ring depth 3 / 
 // grad[i] for i in [i_lo, i_hi) from the slabs (src_off / src_meta: see grad_gather_kernel);
 // with_partials: also log_std grads [0, A) and the 8 loss sums from the per-workgroup partials
 void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part, int nblk,
-                        int npart, int A, float scale, float* grad, int i_lo, int i_hi, int with_partials,
-                        float* loss_out, hipStream_t s);
+                        int npart, int nlog, int loss_mask, float scale, float* grad, int i_lo, int i_hi,
+                        int with_partials, float* loss_out, hipStream_t s);
 void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
                 int T, int E, float gamma, float lam, int mode, int seg, hipStream_t s);
 void set_adam_fused(int on);
@@ -155,7 +161,8 @@ void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, 
 // grad_gather (with the partials pass, range [A, n)) + no-clip Adam fused: world size 1 only
 // (no all-reduce between them); nblk = norm_part size, must exceed A + 8
 void launch_gather_adam(const float* slab, const int* src_off, const int* src_meta, const float* part, int npblk,
-                        int npart, int A, float scale, float* loss_out, float* g, float* p, float* m, float* v,
+                        int npart, int nlog, int loss_mask, float scale, float* loss_out, float* g, float* p,
+                        float* m, float* v,
                         int n, float lr, float b1, float b2, float eps, int step, float* state, float* norm_part,
                         int nblk, void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale,
                         hipStream_t s);

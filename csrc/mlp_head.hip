@@ -1,0 +1,895 @@
+// Per-head, row-stationary, weight-streaming fused PPO update (split-bf16, the fp32-accurate
+// headline precision).  SURVEY K4, K5, K8, K10, K11; loss = corrected ppo.py:148-167 or the
+// reference DPPO loss train.py:142-161; the backward of model.py:35-45 through one head.
+//
+// The actor-critic's two heads share only their input rows: the policy loss (clip + entropy,
+// log_std) reads p_fc1 -> p_fc2 -> mu, the value loss v_fc1 -> v_fc2 -> v.  So the update runs
+// as TWO kernels, one per head, instead of mlp_stream.hip's one:
+//  * each head's whole gradient chain (kernel -> wgrad -> gather -> [all-reduce] -> Adam) is
+//    independent of the other head's, so at world size > 1 one head's RCCL all-reduce overlaps
+//    the other head's kernels (runtime/engine_hip.py), the reference's chief sum
+//    (chief.py:13-20) off the critical path;
+//  * a head alone needs half the registers of both, so a wave owns TWO 16-row blocks (32 rows,
+//    128 per 4-wave workgroup): every weight fragment a workgroup pulls from L2 into its LDS
+//    ring feeds 128 rows instead of 64 — half the L2->CU weight bytes per row, the bound of the
+//    64-row kernel (docs/ARCHITECTURE.md: ~20 B/clk per CU of LDS-DMA), and each fragment read
+//    from LDS feeds 6 MFMAs instead of 3.
+// The observation rows are read once per head (2 x 100 MB per epoch at the bench geometry).
+//
+// Structure per workgroup (4 waves, one per SIMD, up to 512 VGPRs each; wave w owns rows
+// 32w .. 32w+31 of the workgroup's 128 through the whole chain, activations in registers in the
+// MFMA C layout):
+//   fc1      X (gathered rows, per-wave LDS ring, LDS-DMA with 64-bit per-lane row addresses —
+//            any buffer size) x W1: value 2 stages per k-step (32 output tiles), policy 2 k-steps
+//            per stage (7 tiles each)
+//   fc2      2 k-steps per stage; the next k-step's A operand (tanh, h1^T stores, LDS transpose)
+//            is prepared between the two k-steps' MFMAs
+//   fc3 + loss + dgrad fc3   one stage (fc3 slots 0-7, dgrad fc3 slots 8-14)
+//   dgrad fc2  4 output tiles x 4 k-steps per stage; a stage's dtanh epilogue runs in the next
+// Weights stream through an S-stage LDS ring (16 split-bf16 fragments = 32 KiB per stage, wave w
+// DMAs slots 4w..4w+3 by buffer_load ... lds with the fragment codes of every step held in two
+// VGPRs' lanes); counted vmcnt waits + a raw s_barrier per step (the bookkeeping of
+// mlp_stream.hip: vector-memory operations retire in issue order).
+#include <type_traits>
+
+#include "kernels.h"
+#include "mlp_core.h"
+
+namespace {
+
+using P = Prec<DT_S3>;
+using T = P::T;
+using Frag = P::Frag;
+
+constexpr float HD_LOG_2PI = 1.8378770664093453f;
+constexpr int NPF = 8;                      // fixed loss-term columns of a partial row
+constexpr int NW = 4, RB = 2;               // waves; 16-row blocks per wave
+constexpr int WROWS = 16 * RB, ROWS = NW * WROWS;   // 32 rows per wave, 128 per workgroup
+constexpr int FB = 2048;                    // bytes of one split-bf16 fragment (512 slots x 4 B)
+constexpr int NSLOT = 16, SPW = NSLOT / NW, SB = NSLOT * FB, GL = 2 * SPW;
+constexpr int SST = 36, TILE_F = 16 * SST;  // [16][SST] fp32 transpose tile (conflict-free)
+constexpr int MAX_STEPS = 64;
+constexpr int XDMA = 2 * RB;                // DMA instructions of one wave's X fragments of a k-step
+
+template <int HEAD> struct HeadCfg;
+template <> struct HeadCfg<0> {   // policy: p_fc1 -> p_fc2 -> mu
+  static constexpr int L1 = 0, L2 = 1, L3 = 2;
+  static constexpr int N1 = 8, N1R = 7;     // fc1 tiles held / real (100 features + the bias column)
+  static constexpr int K2 = 4;              // fc2 k-steps (fc1 output padded to 128)
+  static constexpr int N3 = 2;              // fc3 output tiles (A <= 32)
+  static constexpr int XS = 4;              // X ring slots (k-steps): 2 per stage, 2 ahead
+  static constexpr int S = 2;               // weight ring stages
+  static constexpr int NS4 = 2;             // dgrad fc2 stages (4 output tiles each)
+};
+template <> struct HeadCfg<1> {   // value: v_fc1 -> v_fc2 -> v
+  static constexpr int L1 = 3, L2 = 4, L3 = 5;
+  static constexpr int N1 = 32, N1R = 32;   // 500 features + the bias column: 32 tiles
+  static constexpr int K2 = 16;
+  static constexpr int N3 = 1;
+  static constexpr int XS = 2;              // 1 k-step per 2 stages, 1 k-step ahead
+  static constexpr int S = 3;
+  static constexpr int NS4 = 8;
+};
+
+template <int HEAD>
+constexpr int xr_floats() { return HeadCfg<HEAD>::XS * RB * FB / 4; }
+template <int HEAD>
+constexpr int ws_floats() { return xr_floats<HEAD>() + RB * TILE_F; }
+template <int HEAD>
+constexpr size_t head_lds_bytes() {
+  return (size_t)HeadCfg<HEAD>::S * SB + (size_t)NW * ws_floats<HEAD>() * sizeof(float);
+}
+static_assert(head_lds_bytes<0>() <= 160 * 1024 && head_lds_bytes<1>() <= 160 * 1024, "LDS");
+// loss scratch (after fc1, in the X ring): dL/dmu | dL/dv [32][SST], then the wave's partials
+static_assert(WROWS * SST + NPF + 32 <= xr_floats<1>(), "loss scratch fits the X ring");
+static_assert(WROWS * 32 <= RB * TILE_F, "mu tile fits the transpose tiles");
+
+template <int HEAD>
+DEV int fc1_stages(int ks1) { return HEAD == 0 ? (ks1 + 1) >> 1 : 2 * ks1; }
+
+DEV int rot_ks(int ks, int rot, int ks1) {
+  const int k = ks + rot;
+  return k >= ks1 ? k - ks1 : k;
+}
+
+// Ring slot q of stream step st: element offset of a weight fragment, or -1 (a slot no MFMA
+// reads; its DMA re-loads slot 0's fragment so every wave issues GL DMAs per step)
+template <int HEAD>
+DEV int step_src(const MlpArgs& a, int st, int q, int rot, int ks1) {
+  using C = HeadCfg<HEAD>;
+  const int ns1 = fc1_stages<HEAD>(ks1), ns2 = C::K2 / 2;
+  const int s_fc3 = ns1 + ns2, s_dg2 = s_fc3 + 1, s_end = s_dg2 + C::NS4;
+  if (st >= s_end) st = s_end - 1;
+  if (st < ns1) {
+    int ks, t;
+    if constexpr (HEAD == 0) {
+      ks = 2 * st + (q >> 3);
+      t = q & 7;
+      if (t >= C::N1R || ks >= ks1) return -1;
+    } else {
+      ks = st >> 1;
+      t = 16 * (st & 1) + q;
+    }
+    return a.off_w[C::L1] + (int)fm_frag(t, rot_ks(ks, rot, ks1), a.d_in[C::L1], 0);
+  }
+  if (st < s_fc3) {
+    const int i = 2 * (st - ns1) + (q >> 3), t = q & 7;
+    if (t == 7) return -1;   // output tile 7 (features 112-127) is padding
+    return a.off_w[C::L2] + (int)fm_frag(t, i, a.d_in[C::L2], 0);
+  }
+  if (st == s_fc3) {
+    if (q < 8) {
+      if (q >= 4 * C::N3) return -1;
+      return a.off_w[C::L3] + (int)fm_frag(q >> 2, q & 3, a.d_in[C::L3], 0);
+    }
+    if (q == 15) return -1;
+    return a.off_wt[C::L3] + (int)fm_frag(q - 8, 0, a.d_out[C::L3], 0);
+  }
+  const int t = 4 * (st - s_dg2) + (q >> 2), ks = q & 3;
+  if (t >= C::N1R) return -1;
+  return a.off_wt[C::L2] + (int)fm_frag(t, ks, a.d_out[C::L2], 0);
+}
+
+// dense LDS image of a DMA'd fragment (mlp_stream.hip frag_lane_off<true>): lane l reads hi at
+// (l / 32) KiB + 16 (l % 32), lo 512 bytes on
+DEV int lane_off(int lane) { return (lane >> 5) * 1024 + (lane & 31) * 16; }
+
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+
+DEV Frag split8(const f32x8& x) {
+  const bf16x8 h = __builtin_convertvector(x, bf16x8);
+  const bf16x8 l = __builtin_convertvector(x - __builtin_convertvector(h, f32x8), bf16x8);
+  return Frag{h, l};
+}
+
+DEV f32x8 join8(const Frag& f) {
+  return __builtin_convertvector(f.h, f32x8) + __builtin_convertvector(f.l, f32x8);
+}
+
+// C-layout tiles of features c0..c0+15 (v0) and c0+16..c0+31 (v1) -> [16][SST] fp32
+DEV void tp_put(float* tp, const f32x4& v0, const f32x4& v1, int lane) {
+  const int lr = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    tp[(4 * lg + i) * SST + lr] = v0[i];
+    tp[(4 * lg + i) * SST + 16 + lr] = v1[i];
+  }
+}
+
+// A operand (row lane & 15, k = 8 (lane >> 4) .. +7) of a [16][SST] tile, split; reads + wait in
+// one asm statement (a plain LDS load would wait vmcnt(0) for the ring's LDS-DMA)
+DEV Frag tp_getA(const float* tp, int lane) {
+  const float* r = tp + (lane & 15) * SST + 8 * (lane >> 4);
+  const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)r;
+  float4 x0, x1;
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(x0), "=&v"(x1)
+               : "v"(addr)
+               : "memory");
+  return split8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
+}
+
+DEV f32x4 bias_col(const f32x4& v, int c, int nb) {
+  const float o = c == nb ? 1.f : 0.f;
+  return c < nb ? v : f32x4{o, o, o, o};
+}
+
+// 4 consecutive m of feature 16 t + (lane & 15) -> the FM wgrad operand from the lane's base
+DEV void store_Tt(__bf16* lane_base, int t, size_t tsb, const f32x4& v) {
+  const bf16x4v hv = __builtin_convertvector(v, bf16x4v);
+  const bf16x4v lv = __builtin_convertvector(v - __builtin_convertvector(hv, f32x4), bf16x4v);
+  char* p = reinterpret_cast<char*>(lane_base) + (size_t)t * tsb;
+  opnd_store(*reinterpret_cast<const u32x2*>(&hv), reinterpret_cast<u32x2*>(p));
+  opnd_store(*reinterpret_cast<const u32x2*>(&lv), reinterpret_cast<u32x2*>(p + 16));
+}
+
+// 8 consecutive m (rows 8h..8h+7) of column col of a [rows][ld] fp32 tile -> one FM group
+DEV void store_T8(void* outT, const float* tile, int ld, int col, int h, int feat, int m, int ldT) {
+  f32x8 x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = tile[(8 * h + j) * ld + col];
+  const Frag s = split8(x);
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+  u32x4* o = reinterpret_cast<u32x4*>(P::hi_ptr(reinterpret_cast<T*>(outT), fm_index(feat, m, ldT)));
+  opnd_store(*reinterpret_cast<const u32x4*>(&s.h), o);
+  opnd_store(*reinterpret_cast<const u32x4*>(&s.l), o + 1);
+}
+
+// s_waitcnt vmcnt(BASE + extra) with a compile-time immediate (mlp_stream.hip wait_vm):
+// undercounting `extra` is safe (the wait is longer), overcounting is not
+template <int BASE, int E = 0>
+DEV void wait_vm(int extra) {
+  if constexpr (BASE + E >= 63) {
+    WAIT_VMCNT(63);
+  } else {
+    if (extra <= E) WAIT_VMCNT(BASE + E);
+    else wait_vm<BASE, E + 1>(extra);
+  }
+}
+
+template <int B, int E, typename F>
+DEV void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// Fragments q in [Q0, Q1) of a stage with bit q of MASK set, read in groups of G: group g + 1's
+// LDS reads are in flight while group g's MFMAs run.  f(integral_constant<q>, fragment).
+template <unsigned MASK, int Q0, int Q1, int G, typename F>
+DEV void for_slots(const char* stg, int lane, F&& f) {
+  constexpr int NG = (Q1 - Q0 + G - 1) / G;
+  Frag b[2][G];
+  const char* base = stg + lane_off(lane);
+  auto rd = [&](auto gc) __attribute__((always_inline)) {
+    constexpr int g = decltype(gc)::value;
+    static_for<0, G>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int q = Q0 + g * G + decltype(ic)::value;
+      if constexpr (q < Q1 && ((MASK >> q) & 1u))
+        b[g & 1][decltype(ic)::value] = Frag{*reinterpret_cast<const bf16x8*>(base + q * FB),
+                                             *reinterpret_cast<const bf16x8*>(base + q * FB + 512)};
+    });
+  };
+  rd(std::integral_constant<int, 0>{});
+  static_for<0, NG>([&](auto gc) __attribute__((always_inline)) {
+    constexpr int g = decltype(gc)::value;
+    if constexpr (g + 1 < NG) rd(std::integral_constant<int, g + 1>{});
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, G>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int q = Q0 + g * G + decltype(ic)::value;
+      if constexpr (q < Q1 && ((MASK >> q) & 1u)) f(std::integral_constant<int, q>{}, b[g & 1][decltype(ic)::value]);
+    });
+  });
+}
+
+template <int G>
+DEV float xsum(float x) {   // sum over the lanes that differ only in the bits of G (xor tree)
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1)
+    if (G & o) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+// phase timeline (diagnostics, scripts/head_timeline.py): lane 0 of each wave of every
+// tstamp_every-th workgroup records the shader clock at the phase boundaries (a vector store the
+// wait bookkeeping does not count: an undercount, safe)
+#define HD_STAMP(i)                                                                               \
+  do {                                                                                            \
+    if (a.tstamp != nullptr && (blockIdx.x % a.tstamp_every) == 0 && lane == 0)                   \
+      a.tstamp[((size_t)(blockIdx.x / a.tstamp_every) * NW + wave) * 16 + (i)] =                  \
+          __builtin_amdgcn_s_memtime();                                                           \
+  } while (0)
+
+template <int HEAD>
+__global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
+  using C = HeadCfg<HEAD>;
+  constexpr int S = C::S, XS = C::XS;
+  constexpr int WS_F = ws_floats<HEAD>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int m0 = blockIdx.x * ROWS;
+  const int A = a.A;
+  const int ks1 = a.d_in[0] >> 5;
+  const int ns1 = fc1_stages<HEAD>(ks1);
+  char* ring = smem;
+  float* scr = reinterpret_cast<float*>(smem + (size_t)S * SB) + wave * WS_F;
+  char* xring = reinterpret_cast<char*>(scr);
+  float* tpb = scr + xr_floats<HEAD>();   // RB transpose tiles [16][SST]
+  float* dml = scr;                        // (after fc1) dL/dmu [32][SST] | dL/dv column 32
+  float* wpart = scr + WROWS * SST;        // (after fc1) [8 loss terms | 32 dlog_std]
+  float* mus = tpb;                        // (loss) mu [32][32] | v [32]
+
+  auto src_of = [&](int r) __attribute__((always_inline)) {
+    const int rr = (m0 + r < a.M) ? m0 + r : m0;   // rows past M re-read row m0 (zero gradient)
+    return a.idx ? a.idx[rr] : a.row0 + rr;
+  };
+  const int mw = m0 + WROWS * wave;
+  // the loss's row and sub-lane: policy 2 lanes per row (32 rows), value lanes 0-31 one row each
+  const int lrow = HEAD == 0 ? lane >> 1 : lane & 31;
+  const int lsub = HEAD == 0 ? lane & 1 : lane >> 5;
+  const bool lvalid = mw + lrow < a.M;
+  const int lsrc = src_of(WROWS * wave + lrow);
+
+  // loss inputs of this lane's row, loaded before any DMA: older than every ring batch, they never
+  // hold up a counted wait (policy: 4 x 16 registers, held through fc1 / fc2)
+  const bool ref_loss = a.loss_kind != 0;
+  constexpr int JM = HEAD == 0 ? 16 : 1;   // action dims per lane (policy: j = lsub + 2 q, A <= 32)
+  float actv[JM], lsv[JM], lsov[JM], mupv[JM];
+  float l_adv = 0.f, l_ret = 0.f, l_lpo = 0.f, l_vold = 0.f, l_vprev = 0.f;
+  if constexpr (HEAD == 0) {
+#pragma unroll
+    for (int q = 0; q < JM; ++q) {
+      const int j = lsub + 2 * q;
+      actv[q] = j < A ? a.actions[(size_t)lsrc * A + j] : 0.f;
+      lsv[q] = j < A ? a.log_std[j] : 0.f;
+      lsov[q] = (ref_loss && j < A) ? a.log_std_old[j] : 0.f;
+      mupv[q] = (ref_loss && j < A) ? a.mu_prev[(size_t)lsrc * A + j] : 0.f;
+    }
+    l_adv = a.adv[lsrc];
+    l_lpo = !ref_loss ? a.logp_old[lsrc] : 0.f;
+  } else {
+    l_ret = a.ret[lsrc];
+    l_vold = !ref_loss ? a.v_old[lsrc] : 0.f;
+    l_vprev = ref_loss ? a.v_prev[lsrc] : 0.f;
+  }
+
+  // ---- DMA sources ----
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), (short)0, 0x7fffffff, 0x00020000);
+  const unsigned vw = (unsigned)((lane & 31) * 32 + (lane >> 5) * 16);
+  // observation rows: 64-bit per-lane addresses (global_load_lds), so a buffer of any size works;
+  // instruction h of a row block moves k-groups 2h, 2h+1 (64 contiguous bytes of each row)
+  const char* xsrc[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+    xsrc[rb] = reinterpret_cast<const char*>(a.x_buf) +
+               (size_t)src_of(WROWS * wave + 16 * rb + lr) * (size_t)a.d_in[0] * sizeof(T) + 32 * ((lane >> 4) & 1) +
+               16 * (lane >> 5);
+  const int rot = (int)(blockIdx.x % (unsigned)ks1);
+  auto code16 = [&](int st, int q) __attribute__((always_inline)) {
+    int c = step_src<HEAD>(a, st, q, rot, ks1);
+    if (c < 0) c = step_src<HEAD>(a, st, 0, rot, ks1);
+    if (c < 0) c = a.off_w[C::L1];
+    return (uint32_t)(c >> 9);
+  };
+  const uint32_t cw0 = code16(lane, SPW * wave) | (code16(lane, SPW * wave + 1) << 16);
+  const uint32_t cw1 = code16(lane, SPW * wave + 2) | (code16(lane, SPW * wave + 3) << 16);
+
+  // diagnostics only (scripts/head_timeline.py ablations; 0 in every real run): bit 1 no weight
+  // DMA, bit 3 no observation DMA, bit 5 no fc1 MFMAs
+  const int abl = a.ablate;
+  auto issue = [&](int st, int stage) __attribute__((always_inline)) {
+    if (abl & 2) return;
+    const int l = min(st, MAX_STEPS - 1);
+    const uint32_t w01 = __builtin_amdgcn_readlane(cw0, l);
+    const uint32_t w23 = __builtin_amdgcn_readlane(cw1, l);
+    __attribute__((address_space(3))) char* stg =
+        (__attribute__((address_space(3))) char*)(ring + stage * SB) + SPW * wave * FB;
+#pragma unroll
+    for (int u = 0; u < SPW; ++u) {
+      const uint32_t code = ((u < 2 ? w01 : w23) >> (16 * (u & 1))) & 0xffffu;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB, 16, vw, code * 2048u, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB + 1024, 16, vw, code * 2048u + 1024u, 0, 0);
+    }
+  };
+  // this wave's RB observation fragments of fc1 k-step ks into X ring slot ks % XS
+  auto issue_x = [&](int ks) __attribute__((always_inline)) {
+    if (abl & 8) return;
+    const size_t xo = (size_t)rot_ks(min(ks, ks1 - 1), rot, ks1) * 128u;
+    char* d = xring + (ks & (XS - 1)) * (RB * FB);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      glds16(xsrc[rb] + xo, d + rb * FB);
+      glds16(xsrc[rb] + xo + 64, d + rb * FB + 1024);
+    }
+  };
+  auto read_x = [&](int ks, int rb) __attribute__((always_inline)) {
+    const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(
+                              xring + (ks & (XS - 1)) * (RB * FB) + rb * FB) + lane_off(lane);
+    bf16x8 h, l;
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:512\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(h), "=&v"(l)
+                 : "v"(addr)
+                 : "memory");
+    return Frag{h, l};
+  };
+
+  // Ring bookkeeping.  Every step: wait for its stage (this wave's DMAs by count, every wave's by
+  // the barrier, which also retires every wave's reads of the previous step's stage), then at
+  // once refill that previous stage with step cur + S - 1, then compute.  Vector-memory
+  // operations retire in issue order (loads, stores, LDS-DMA together), so the wait for step c's
+  // batch — issued at the start of step c - S + 1 — may leave outstanding everything younger:
+  // the S - 2 later refills and every store / X load issued since (`younger` = those of the
+  // previous step; undercounting is safe, overcounting is not).
+  int cst = 0, cur = 0;
+  constexpr int NH = S - 1;
+  int hist[NH];
+#pragma unroll
+  for (int i = 0; i < NH; ++i) hist[i] = 0;
+  auto wait_step = [&](int younger) __attribute__((always_inline)) -> const char* {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = NH - 1; i > 0; --i) hist[i] = hist[i - 1];
+    hist[0] = younger;
+    int extra = 0;
+#pragma unroll
+    for (int i = 0; i < NH; ++i) extra += hist[i];
+    wait_vm<GL * (S - 2)>(extra);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* stg = ring + cst * SB;
+    issue(cur + S - 1, cst == 0 ? S - 1 : cst - 1);
+    cst = cst + 1 == S ? 0 : cst + 1;
+    ++cur;
+    return stg;
+  };
+
+  HD_STAMP(0);
+  // ---- prime: the first X k-steps, then ring stages 0 .. S-2 ----
+#pragma unroll
+  for (int k = 0; k < XS; ++k) issue_x(k);
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st) issue(st, st);
+
+  const size_t tsb = (size_t)a.ldT * 64;   // bytes of one 16-feature row block of an FM operand
+  auto lane_base = [&](void* buf, int rb) __attribute__((always_inline)) {
+    return P::hi_ptr(reinterpret_cast<T*>(buf), fm_index(lr, mw + 16 * rb + 4 * lg, a.ldT));
+  };
+  void* const h1T = HEAD == 0 ? a.h1pT : a.h1vT;
+  void* const h2T = HEAD == 0 ? a.h2pT : a.h2vT;
+  void* const g2T = HEAD == 0 ? a.g2pT : a.g2vT;
+  void* const g1T = HEAD == 0 ? a.g1pT : a.g1vT;
+
+  // ---------------- fc1 ----------------
+  f32x4 acc1[RB][C::N1];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int t = 0; t < C::N1; ++t) acc1[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool want_xT = HEAD == 0 && !a.xT_ready;
+  const char* stg;
+  // (the policy kernel writes the x^T wgrad operand when the rollout did not: the wave's 16 x 32
+  // block of k-step ks of row block rb, transposed through its tile)
+  auto put_xT = [&](const Frag& x, int ks, int rb) __attribute__((always_inline)) {
+    float* tp = tpb + rb * TILE_F;
+    const f32x8 v = join8(x);
+    float4* w = reinterpret_cast<float4*>(tp + lr * SST + 8 * lg);
+    w[0] = float4{v[0], v[1], v[2], v[3]};
+    w[1] = float4{v[4], v[5], v[6], v[7]};
+    store_T8(a.xT, tp, SST, lane >> 1, lane & 1, 32 * rot_ks(ks, rot, ks1) + (lane >> 1),
+             mw + 16 * rb + 8 * (lane & 1), a.ldT);
+  };
+  if constexpr (HEAD == 1) {
+    Frag xa[RB];
+    for (int ks = 0; ks < ks1; ++ks) {
+      static_for<0, 2>([&](auto sc) __attribute__((always_inline)) {
+        constexpr int sub = decltype(sc)::value;
+        stg = wait_step(sub == 1 ? XDMA : 0);
+        if constexpr (sub == 0) {
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb) xa[rb] = read_x(ks, rb);
+        }
+        if (!(abl & 32))
+          for_slots<0xffffu, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+            constexpr int t = 16 * sub + decltype(qc)::value;
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) acc1[rb][t] = P::mma(acc1[rb][t], xa[rb], b);
+          });
+        if constexpr (sub == 0) issue_x(ks + 2);   // into the slot X[ks] just left
+      });
+      if (ks == 1) HD_STAMP(8);
+      if (ks == 5) HD_STAMP(9);
+    }
+  } else {
+    for (int st = 0; st < ns1; ++st) {
+      stg = wait_step(st > 0 ? 2 * XDMA : 0);
+      const int ka = 2 * st, kb = 2 * st + 1;
+      const bool two = kb < ks1;
+      Frag xa[RB], xb[RB];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        xa[rb] = read_x(ka, rb);
+        xb[rb] = read_x(kb, rb);
+      }
+      for_slots<0x7f7fu, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+        constexpr int q = decltype(qc)::value;
+        if constexpr (q < 8) {
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb) acc1[rb][q] = P::mma(acc1[rb][q], xa[rb], b);
+        } else {
+          if (two) {
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) acc1[rb][q - 8] = P::mma(acc1[rb][q - 8], xb[rb], b);
+          }
+        }
+      });
+      if (want_xT) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          put_xT(xa[rb], ka, rb);
+          if (two) put_xT(xb[rb], kb, rb);
+        }
+      }
+      issue_x(ka + 4);   // into the slots X[ka], X[kb] just left
+      issue_x(kb + 4);
+      if (st == 0) HD_STAMP(8);
+      if (st == 3) HD_STAMP(9);
+    }
+  }
+  HD_STAMP(1);
+  // ---------------- fc2: h1 = tanh(fc1), one k-step's A operand prepared at a time ----------------
+  const int n1 = a.n_out[C::L1], n2 = a.n_out[C::L2];
+  __bf16* bh1[RB];
+  __bf16* bh2[RB];
+  __bf16* bg2[RB];
+  __bf16* bg1[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    bh1[rb] = lane_base(h1T, rb);
+    bh2[rb] = lane_base(h2T, rb);
+    bg2[rb] = lane_base(g2T, rb);
+    bg1[rb] = lane_base(g1T, rb);
+  }
+  // A operand of fc2 k-step I (h1 features 32 I .. 32 I + 31) for both row blocks: tanh in place,
+  // the h1^T stores, the transposes; returns the number of stores
+  auto prep = [&](auto Ic, Frag (&fa)[RB]) __attribute__((always_inline)) -> int {
+    constexpr int I = decltype(Ic)::value;
+    constexpr bool last = I == C::K2 - 1;
+    const int c0 = 32 * I + lr;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const f32x4 h0 = act_tanh4<DT_S3>(acc1[rb][2 * I]), h1 = act_tanh4<DT_S3>(acc1[rb][2 * I + 1]);
+      acc1[rb][2 * I] = h0;
+      acc1[rb][2 * I + 1] = h1;
+      // (the last k-step holds the bias column (1) and zero padding: stored as such)
+      const f32x4 s0 = last ? bias_col(h0, c0, n1) : h0, s1 = last ? bias_col(h1, c0 + 16, n1) : h1;
+      store_Tt(bh1[rb], 2 * I, tsb, s0);
+      store_Tt(bh1[rb], 2 * I + 1, tsb, s1);
+      tp_put(tpb + rb * TILE_F, s0, s1, lane);
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) fa[rb] = tp_getA(tpb + rb * TILE_F, lane);
+    return 4 * RB;
+  };
+  f32x4 acc2[RB][8];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc2[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag a0[RB], a1[RB];
+  // (+ the X loads of the last fc1 step: policy past-the-end re-loads)
+  int nst = prep(std::integral_constant<int, 0>{}, a0) + (HEAD == 0 ? 2 * XDMA : 0);
+  static_for<0, C::K2 / 2>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    stg = wait_step(nst);
+    for_slots<0x7fu, 0, 8, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      constexpr int t = decltype(qc)::value;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a0[rb], b);
+    });
+    nst = prep(std::integral_constant<int, 2 * j + 1>{}, a1);
+    for_slots<0x7f00u, 8, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      constexpr int t = decltype(qc)::value - 8;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a1[rb], b);
+    });
+    if constexpr (2 * j + 2 < C::K2) {
+      nst += prep(std::integral_constant<int, 2 * j + 2>{}, a0);
+    } else {
+      // h2 = tanh(fc2) (kept for dgrad fc3); its stores belong to this step
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          acc2[rb][t] = act_tanh4<DT_S3>(acc2[rb][t]);
+          store_Tt(bh2[rb], t, tsb, bias_col(acc2[rb][t], 16 * t + lr, n2));   // (bias row 1, padding 0)
+        }
+      nst += 16 * RB;
+    }
+  });
+
+  HD_STAMP(2);
+  // ---------------- fc3 + loss + dgrad fc3: one stage ----------------
+  stg = wait_step(nst);
+  HD_STAMP(3);
+  f32x4 a3[RB][C::N3];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int t = 0; t < C::N3; ++t) a3[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fc3 k-step by k-step: the A operand (h2 features 32 ks .. +31, bias column, padding) and the
+  // fragments of that k-step (slot 4 t + ks)
+  static_for<0, 4>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int ks = decltype(kc)::value;
+    const int c0 = 32 * ks + lr;
+    Frag am[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      tp_put(tpb + rb * TILE_F, bias_col(acc2[rb][2 * ks], c0, n2), bias_col(acc2[rb][2 * ks + 1], c0 + 16, n2), lane);
+      am[rb] = tp_getA(tpb + rb * TILE_F, lane);
+    }
+    constexpr unsigned M3 = C::N3 == 2 ? ((1u << ks) | (1u << (4 + ks))) : (1u << ks);
+    for_slots<M3, 0, 8, 8>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      constexpr int t = decltype(qc)::value >> 2;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) a3[rb][t] = P::mma(a3[rb][t], am[rb], b);
+    });
+  });
+  // (the transpose tiles hold mu / v from here: every wave's own)
+  float dls[JM], lt[6];
+#pragma unroll
+  for (int q = 0; q < JM; ++q) dls[q] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) lt[k] = 0.f;
+  Frag ad[RB];   // the A operand of dgrad fc3: dL/dmu (policy) | dL/dv in column 0 (value)
+  if constexpr (HEAD == 0) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * rb + 4 * lg + i;
+        if (lr < A) mus[r * 32 + lr] = a3[rb][0][i];
+        if (16 + lr < A) mus[r * 32 + 16 + lr] = a3[rb][1][i];
+      }
+    {
+      // zero the wave's dL/dmu tile (columns >= A are the padded K of dgrad fc3)
+      float4* z = reinterpret_cast<float4*>(dml + (lane >> 1) * SST + 16 * (lane & 1));
+      z[0] = z[1] = z[2] = z[3] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int r = lrow, sub = lsub;
+    const bool valid = lvalid;
+    const float cvar = a.std_var ? 0.5f : 1.f;
+    float lclip = 0.f, lent = 0.f, kl = 0.f, cf = 0.f;
+    if (a.loss_kind == 0) {
+      // ---- corrected PPO (ppo.py:148-167) ----
+      float logp = 0.f;
+#pragma unroll
+      for (int q = 0; q < JM; ++q) {
+        const int j = sub + 2 * q;
+        if (j >= A) break;
+        const float lsig = cvar * lsv[q];
+        const float z = (actv[q] - mus[r * 32 + j]) * __expf(-lsig);
+        logp += -0.5f * z * z - 0.5f * HD_LOG_2PI - lsig;
+      }
+      logp += __shfl_xor(logp, 1, 64);
+      const float lrat = logp - l_lpo;
+      const float ratio = __expf(lrat);
+      const float s1 = ratio * l_adv;
+      const float s2 = fminf(fmaxf(ratio, 1.f - a.clip), 1.f + a.clip) * l_adv;
+      lclip = -fminf(s1, s2);
+      const float dlogp = (s1 <= s2) ? -l_adv * ratio : 0.f;
+      kl = (ratio - 1.f) - lrat;
+      cf = (fabsf(ratio - 1.f) > a.clip) ? 1.f : 0.f;
+#pragma unroll
+      for (int q = 0; q < JM; ++q) {
+        const int j = sub + 2 * q;
+        if (j >= A) break;
+        const float lsig = cvar * lsv[q];
+        const float isig = __expf(-lsig);
+        const float z = (actv[q] - mus[r * 32 + j]) * isig;
+        dml[r * SST + j] = valid ? dlogp * z * isig : 0.f;
+        dls[q] = valid ? (dlogp * (z * z - 1.f) - a.ent_coeff) * cvar : 0.f;
+        lent += -a.ent_coeff * (0.5f + 0.5f * HD_LOG_2PI + lsig);
+      }
+      lent += __shfl_xor(lent, 1, 64);
+    } else {
+      // ---- reference DPPO loss (train.py:142-161): per-dim pdf ratio, variance convention ----
+      const float invA = 1.f / (float)A;
+      const bool first = a.first_step != 0;
+#pragma unroll
+      for (int q = 0; q < JM; ++q) {
+        const int j = sub + 2 * q;
+        if (j >= A) break;
+        const float mu = mus[r * 32 + j];
+        const float var = __expf(lsv[q]);
+        const float mu_o = first ? mu : mupv[q];
+        const float var_o = first ? var : __expf(lsov[q]);
+        const float x = actv[q];
+        const float pd = __expf(-(x - mu) * (x - mu) / (2.f * var)) * rsqrtf(2.f * var * 3.14159265358979f);
+        const float po = __expf(-(x - mu_o) * (x - mu_o) / (2.f * var_o)) * rsqrtf(2.f * var_o * 3.14159265358979f);
+        const float ratio = pd / (1e-10f + po);
+        const float s1 = ratio * l_adv;
+        const float s2 = fminf(fmaxf(ratio, 1.f - a.clip), 1.f + a.clip) * l_adv;
+        lclip += -fminf(s1, s2) * invA;
+        const float dratio = (s1 <= s2) ? -l_adv * invA : 0.f;
+        float dp = dratio / (1e-10f + po);
+        const float lgp = logf(pd + 1e-5f);
+        lent += -a.ent_coeff * pd * lgp * invA;
+        dp += -a.ent_coeff * invA * (lgp + pd / (pd + 1e-5f));
+        dml[r * SST + j] = valid ? dp * pd * (x - mu) / var : 0.f;
+        dls[q] = valid ? dp * pd * ((x - mu) * (x - mu) / (2.f * var) - 0.5f) : 0.f;
+        cf += (fabsf(ratio - 1.f) > a.clip) ? invA : 0.f;
+        if (valid) a.mu_prev[(size_t)lsrc * A + j] = mu;   // train.py:164 model_old <- model
+      }
+      lclip += __shfl_xor(lclip, 1, 64);
+      lent += __shfl_xor(lent, 1, 64);
+      cf += __shfl_xor(cf, 1, 64);
+    }
+    if (sub == 0) {
+      const float vm = valid ? 1.f : 0.f;
+      lt[0] = lclip * vm; lt[2] = lent * vm; lt[3] = kl * vm; lt[4] = cf * vm; lt[5] = vm;
+    }
+    // the wave's partial sums over its 32 rows (lanes of one sub-lane: xor over lane bits 1-5)
+#pragma unroll
+    for (int q = 0; q < JM; ++q) dls[q] = xsum<62>(dls[q]);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) lt[k] = xsum<62>(lt[k]);
+    if (lane < 2) {
+#pragma unroll
+      for (int q = 0; q < JM; ++q)
+        if (lane + 2 * q < A) wpart[NPF + lane + 2 * q] = dls[q];
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) wpart[k] = lt[k];
+        wpart[6] = wpart[7] = 0.f;
+      }
+    }
+    // dY^T of mu: item = (feature, 8-row group) of the wave's 32 rows
+    for (int it = lane; it < 4 * A; it += 64)
+      store_T8(a.g3pT, dml, SST, it >> 2, it & 3, it >> 2, mw + 8 * (it & 3), a.ldT);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) ad[rb] = tp_getA(dml + 16 * rb * SST, lane);
+  } else {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (lr == 0) mus[16 * rb + 4 * lg + i] = a3[rb][0][i];
+    float dv = 0.f;
+    if (lsub == 0) {
+      const float v = mus[lrow];
+      const bool valid = lvalid;
+      const bool first = a.first_step != 0;
+      const float vold = ref_loss ? (first ? v : l_vprev) : l_vold;
+      float lv;
+      if (a.value_loss == 0) {
+        const float d = v - l_ret;
+        lv = d * d;
+        dv = 2.f * d;
+      } else {
+        const float d1 = v - l_ret;
+        const float dd = v - vold;
+        const float vc = vold + fminf(fmaxf(dd, -a.clip), a.clip);
+        const float d2 = vc - l_ret;
+        const float f1 = d1 * d1, f2 = d2 * d2;
+        const float inr = (dd >= -a.clip && dd <= a.clip) ? 1.f : 0.f;
+        lv = 0.5f * fmaxf(f1, f2);
+        if (f1 > f2) dv = d1;
+        else if (f2 > f1) dv = d2 * inr;
+        else dv = 0.5f * d1 + 0.5f * d2 * inr;
+      }
+      if (ref_loss && valid) a.v_prev[lsrc] = v;
+      dv = valid ? dv : 0.f;
+      const float vm = valid ? 1.f : 0.f;
+      lt[1] = lv * vm;
+      lt[5] = vm;
+      dml[lrow] = dv;   // dL/dv of the wave's 32 rows
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) lt[k] = xsum<31>(lt[k]);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) wpart[k] = lt[k];
+      wpart[6] = wpart[7] = 0.f;
+    }
+    // dY^T of v (feature 0) in 8-row groups, and the A operand of dgrad fc3 (K = 32, only k = 0)
+    float dvr[RB];
+    {
+      const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)dml;
+      float d0, d1;
+      asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:64\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(d0), "=&v"(d1)
+                   : "v"(base + 4u * lr)
+                   : "memory");
+      dvr[0] = d0;
+      dvr[1] = d1;
+    }
+    if (lane < 4) store_T8(a.g3vT, dml, 1, 0, lane, 0, mw + 8 * lane, a.ldT);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) ad[rb] = split8(f32x8{lg == 0 ? dvr[rb] : 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
+  }
+
+  HD_STAMP(4);
+  // dgrad fc3: dpre2 = (dY W3) * (1 - h2^2) -> g2^T stores and the A operands of dgrad fc2
+  f32x4 d2[RB][8];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) d2[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for_slots<0x7f00u, 8, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    constexpr int t = decltype(qc)::value - 8;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) d2[rb][t] = P::mma(d2[rb][t], ad[rb], b);
+  });
+  nst = 0;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int c = 16 * t + lr;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      d2[rb][t] = c < n2 ? d2[rb][t] * (1.0f - acc2[rb][t] * acc2[rb][t]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      store_Tt(bg2[rb], t, tsb, d2[rb][t]);
+    }
+  }
+  nst += 16 * RB;
+  Frag a2[4][RB];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      tp_put(tpb + rb * TILE_F, d2[rb][2 * ks], d2[rb][2 * ks + 1], lane);
+      a2[ks][rb] = tp_getA(tpb + rb * TILE_F, lane);
+    }
+  // (the loss's dY^T stores are not counted: an undercount, the next waits cover them)
+
+  HD_STAMP(5);
+  // ---------------- dgrad fc2: g1 = (dpre2 W2) * (1 - h1^2), only the wgrad operand ----------------
+  f32x4 gq[4][RB];
+  auto epi = [&](auto sc) __attribute__((always_inline)) -> int {
+    constexpr int s = decltype(sc)::value;
+    int n = 0;
+    static_for<0, 4>([&](auto uc) __attribute__((always_inline)) {
+      constexpr int tt = 4 * s + decltype(uc)::value;
+      if constexpr (tt < C::N1R) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          const f32x4 h = acc1[rb][tt];
+          store_Tt(bg1[rb], tt, tsb, gq[decltype(uc)::value][rb] * (1.0f - h * h));
+        }
+        n += 2 * RB;
+      }
+    });
+    return n;
+  };
+  static_for<0, C::NS4>([&](auto sc) __attribute__((always_inline)) {
+    constexpr int s = decltype(sc)::value;
+    stg = wait_step(nst);
+    f32x4 g[4][RB];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) g[u][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr unsigned M4 = (4 * s + 3 < C::N1R) ? 0xffffu : ((1u << (4 * ((C::N1R - 4 * s) & 3))) - 1u);
+    for_slots<M4, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) g[q >> 2][rb] = P::mma(g[q >> 2][rb], a2[q & 3][rb], b);
+    });
+    if constexpr (s > 0) nst = epi(std::integral_constant<int, s - 1>{});
+    else nst = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) gq[u][rb] = g[u][rb];
+  });
+  epi(std::integral_constant<int, C::NS4 - 1>{});
+  HD_STAMP(6);
+
+  // ---------------- per-workgroup partials (deterministic fixed order) ----------------
+  WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
+  __syncthreads();
+  const float* sc0 = reinterpret_cast<const float*>(smem + (size_t)S * SB);
+  const int np = HEAD == 0 ? NPF + A : NPF;
+  for (int q = tid; q < np; q += NW * 64) {
+    float s = 0.f;
+    for (int w = 0; w < NW; ++w) s += sc0[w * WS_F + WROWS * SST + q];
+    a.part[(size_t)blockIdx.x * a.npart + q] = s;
+  }
+  HD_STAMP(7);
+}
+
+template <int HEAD>
+void head_launch(const MlpArgs& a, hipStream_t s) {
+  const size_t lds = head_lds_bytes<HEAD>();
+  set_max_lds_once<mlp_head_kernel<HEAD>>(lds);
+  const int nblk = (a.M + ROWS - 1) / ROWS;
+  hipLaunchKernelGGL((mlp_head_kernel<HEAD>), dim3(nblk), dim3(NW * 64), lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
+int g_head_enable = 1;
+
+}  // namespace
+
+// shapes the per-head kernels cover (the reference network: policy 100-100, value 500-100; any
+// observation width <= 383 and action width <= 32); anything else runs the generic kernels
+extern "C" int mlp_head_applies(const MlpArgs& a) {
+  if (!g_head_enable) return 0;
+  return a.d_in[0] <= 384 && a.d_in[0] >= 32 && a.d_in[0] == a.d_in[3] && (a.n_out[0] + 15) / 16 == 7 &&
+         (a.n_out[3] + 15) / 16 == 32 && a.d_in[1] == 128 && a.d_in[4] == 512 && a.d_in[2] == 128 &&
+         a.d_in[5] == 128 && a.d_out[1] == 128 && a.d_out[4] == 128 && a.d_out[2] == 32 && a.d_out[5] == 32 &&
+         a.n_out[1] > 96 && a.n_out[1] <= 112 && a.n_out[4] > 96 && a.n_out[4] <= 112 && a.A >= 1 && a.A <= 32;
+}
+
+extern "C" int mlp_head_rows() { return ROWS; }
+
+extern "C" void launch_mlp_head(int head, const MlpArgs& a, hipStream_t s) {
+  if (head == 0) head_launch<0>(a, s);
+  else head_launch<1>(a, s);
+}
+
+extern "C" void set_head_kernels(int enable) { g_head_enable = enable ? 1 : 0; }
+extern "C" int head_kernels_enabled() { return g_head_enable; }

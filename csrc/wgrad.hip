@@ -233,10 +233,11 @@ void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
   launch_wgrad_lds_t<DT, S, W, false>(a, s);
 }
 
-// With the partials pass (nred = A + 8 > 0):
-//   Workgroups [0, A): grad[j] = scale * sum_b part[b*npart + 8 + j]  (log_std, one WG per dim,
-//                      strided partial sums + LDS tree: fixed order, deterministic)
-//   Workgroups [A, A+8): loss_out[q] = sum_b part[b*npart + q] (loss-term sums for logging).
+// With the partials pass (nred = nlog + 8 > 0):
+//   Workgroups [0, nlog): grad[j] = scale * sum_b part[b*npart + 8 + j]  (log_std, one WG per
+//                      dim, strided partial sums + LDS tree: fixed order, deterministic)
+//   Workgroups [nlog, nlog+8): loss_out[q] = sum_b part[b*npart + q] (loss-term sums for
+//                      logging; only the columns in loss_mask: a per-head gather owns its terms).
 // Workgroups [nred, grid): grad[i] = scale * sum_{c < nch} slab[src_off[i] + c * stride],
 //                    i in [i_lo, i_hi), with (nch, stride) of i's output tile packed in
 //                    src_meta[i] = nch * 16 + stride / 4096 (each tile has its own batch-chunk
@@ -247,13 +248,14 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
                                                           const int* __restrict__ src_off,
                                                           const int* __restrict__ src_meta,
                                                           const float* __restrict__ part,
-                                                          int nblk, int npart, int A, float scale,
-                                                          float* __restrict__ grad, int i_lo, int i_hi,
-                                                          int nred, float* __restrict__ loss_out) {
+                                                          int nblk, int npart, int nlog, int loss_mask,
+                                                          float scale, float* __restrict__ grad, int i_lo,
+                                                          int i_hi, int nred, float* __restrict__ loss_out) {
   if ((int)blockIdx.x < nred) {
     __shared__ float red[256];
     const int j = blockIdx.x;
-    const int col = j < A ? 8 + j : j - A;
+    const int col = j < nlog ? 8 + j : j - nlog;
+    if (j >= nlog && !((loss_mask >> (j - nlog)) & 1)) return;
     float s = 0.f;
     for (int b = threadIdx.x; b < nblk; b += 256) s += part[(size_t)b * npart + col];
     red[threadIdx.x] = s;
@@ -263,8 +265,8 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
       __syncthreads();
     }
     if (threadIdx.x == 0) {
-      if (j < A) grad[j] = red[0] * scale;
-      else loss_out[j - A] = red[0];
+      if (j < nlog) grad[j] = red[0] * scale;
+      else loss_out[j - nlog] = red[0];
     }
     return;
   }
@@ -307,14 +309,14 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
 }
 
 extern "C" void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part,
-                                   int nblk, int npart, int A, float scale, float* grad, int i_lo, int i_hi,
-                                   int with_partials, float* loss_out, hipStream_t s) {
+                                   int nblk, int npart, int nlog, int loss_mask, float scale, float* grad, int i_lo,
+                                   int i_hi, int with_partials, float* loss_out, hipStream_t s) {
   int grid = (i_hi - i_lo + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
-  const int nred = with_partials ? A + 8 : 0;
+  const int nred = with_partials ? nlog + 8 : 0;
   grid += nred;
   hipLaunchKernelGGL(grad_gather_kernel, dim3(grid), dim3(256), 0, s, slab, src_off, src_meta, part, nblk, npart,
-                     A, scale, grad, i_lo, i_hi, nred, loss_out);
+                     nlog, loss_mask, scale, grad, i_lo, i_hi, nred, loss_out);
   HIP_CHECK_LAUNCH();
 }

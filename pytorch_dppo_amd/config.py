@@ -69,13 +69,11 @@ class Params:
     resume: str = ""
     log_jsonl: str = ""
     log_every: int = 1
-    overlap_rollout: bool = False        # SURVEY §5.8 option (b)
+    # the last gradient all-reduce overlaps the next rollout.  GPU engine: the value
+    # head's last step stays pending until after the next rollout (which reads only the policy:
+    # exact); CPU engine: the whole last step (option b, a 1-update policy lag)
+    overlap_rollout: bool = False
     use_graphs: bool = False             # replay the per-minibatch launch chains as hipGraphs (GPU engine)
-    # bucketed gradient all-reduce overlapping the policy-side wgrad: off | on | auto (on when
-    # multi-rank).  Off by default: at world size 1 with forced RCCL calls it measured 3.96 vs
-    # 3.11 ms per iteration (two extra launches, a 128-workgroup policy wgrad, and the two
-    # collectives' fixed costs exceed the ~40 us/epoch they can hide); multi-GPU unmeasured.
-    grad_buckets: str = "off"
     dist_timeout_s: float = 300.0
     verify_sync_every: int = 0           # debug param-checksum all-reduce period
     adam_betas: tuple = (0.9, 0.999)
@@ -115,8 +113,6 @@ class Params:
             raise ValueError(f"value_loss must be mse|clipped_half, got {self.value_loss}")
         if self.std_convention not in ("std", "var"):
             raise ValueError("std_convention must be std|var")
-        if self.grad_buckets not in ("auto", "on", "off"):
-            raise ValueError("grad_buckets must be auto|on|off")
         if self.grad_reduce not in ("sum", "mean"):
             raise ValueError("grad_reduce must be sum|mean")
         if self.loss == "dppo_ref":

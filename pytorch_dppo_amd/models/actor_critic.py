@@ -7,9 +7,10 @@ Architecture = reference ``Model`` (``model.py:8-45``):
 * a state-independent ``log_std [1, A]`` initialised to 0 (``model.py:21``),
 * Linear weights with torch's default init, biases zeroed (``model.py:24-27``).
 
-Every parameter is a view into ``self.flat`` (one contiguous fp32 tensor) laid out in the
-reference's ``named_parameters`` order (``log_std`` first — root parameters precede
-sub-modules).  That single buffer is what the RCCL gradient all-reduce, the fused Adam kernel
+Every parameter is a view into ``self.flat`` (one contiguous fp32 tensor): ``log_std`` and
+the policy head, then the value head (each head one contiguous range); ``state_dict()`` and
+``named_parameters_ref()`` keep the reference's ``named_parameters`` order (``log_std`` first —
+root parameters precede sub-modules).  That single buffer is what the RCCL gradient all-reduce, the fused Adam kernel
 and checkpointing operate on.  ``state_dict()`` returns exactly the
 reference keys/shapes so ``model.pt`` loads into the reference ``Model`` with
 ``strict=True``.
@@ -67,13 +68,22 @@ class ActorCritic(nn.Module):
             ls = self.layer(name)
             order += [(f"{name}.weight", (ls.fan_out, ls.fan_in)), (f"{name}.bias", (ls.fan_out,))]
         self.param_shapes: "OrderedDict[str, Tuple[int, ...]]" = OrderedDict(order)
+        # memory order of the flat buffer: log_std and the policy head first, then the value head,
+        # so each head's parameters (and gradient, and Adam state) are ONE contiguous range — the
+        # HIP engine updates and all-reduces the two heads as independent chains.  state_dict()
+        # keeps the reference key order regardless (it is built from views).
+        mem = ["log_std"] + [f"{n}.{s}" for n in ("p_fc1", "p_fc2", "mu", "v_fc1", "v_fc2", "v")
+                             for s in ("weight", "bias")]
         self.offsets: Dict[str, Tuple[int, int]] = {}
         off = 0
-        for k, shp in self.param_shapes.items():
-            n = math.prod(shp)
+        for k in mem:
+            n = math.prod(self.param_shapes[k])
             self.offsets[k] = (off, n)
             off += n
         self.num_params = off
+        # [lo, hi) of each head in the flat buffer (log_std belongs to the policy)
+        self.head_ranges: Dict[str, Tuple[int, int]] = {"policy": (0, self.offsets["v_fc1.weight"][0]),
+                                                        "value": (self.offsets["v_fc1.weight"][0], off)}
         self.flat = nn.Parameter(torch.zeros(off, dtype=torch.float32))
         self.reset_parameters()
 

@@ -6,10 +6,14 @@ Per iteration (all device work on the current HIP stream, no host sync until the
                                          log-prob, env physics) -> [T][E] buffer in HBM
   values    1 launch  csrc/mlp.hip       V(s) for all (T+1)*E rows (value head on MFMA)
   gae       1 launch  csrc/optim.hip     one lane per env reverse scan
-  per minibatch (= one synchronous global step, train.py:133-175 / chief.py:13-20):
-    grad    3 launches  mlp_train (fwd+loss+dgrad) -> wgrad (grouped split-K) -> grad_gather
-    [RCCL all-reduce of the flat fp32 gradient — done by the worker between grad and apply]
-    apply   2 launches  sumsq + fused Adam/clip that also refreshes the packed weight images
+  per minibatch (= one synchronous global step, train.py:133-175 / chief.py:13-20), step():
+    split-bf16 + the reference network (the headline): the two heads are independent chains,
+      per head  mlp_head (fwd+loss+dgrad, csrc/mlp_head.hip) -> wgrad (its layers) -> gather+Adam
+      world size > 1: gather -> async RCCL all-reduce of the head's flat range -> Adam, with each
+      head's all-reduce in flight while the other head's kernels run (policy step e's beside
+      value step e's kernels, value step e's beside policy step e+1's)
+    otherwise: mlp_train (both heads) -> wgrad -> grad_gather [-> all-reduce] -> Adam
+    with clipping (ppo preset): gathers -> all-reduce -> sumsq + Adam over the whole vector
 
 The packed weight images (PackedLayout) hold every layer as [d_out][d_in] and its transpose
 in the MFMA operand precision (fp32 / bf16), the bias folded into column K.
@@ -134,11 +138,23 @@ class HipEngine:
         self.ep_sum = torch.zeros(2, dtype=torch.float64, device=device)
         # ---- update geometry ----
         self.mb = params.minibatch_rows()
-        self.ldT = _r(self.mb, 64)      # wgrad consumes k-steps in pairs (csrc/wgrad.hip)
+        # per-head streaming kernels (csrc/mlp_head.hip, 128 rows per workgroup): split-bf16 and
+        # the reference network; DPPO_HEADS=1 selects them (A/B while they are tuned)
+        self.heads = (os.environ.get("DPPO_HEADS", "0") != "0"
+                      and bool(self.ext.head_applies(self.dt, self.layout, A)))
+        # operand rows: a multiple of the update kernel's row tile (every row it writes has a
+        # column) and of 64 (wgrad consumes k-steps in pairs, csrc/wgrad.hip)
+        self.ldT = _r(self.mb, 128 if self.heads else 64)
         self.npart = NPART_FIXED + A
         # per-workgroup partials, sized for the smallest row tile (16) so a tile change
         # (set_mlp_rows, A/B diagnostics) never outgrows it
         self.part = torch.zeros(self.ldT // 16, self.npart, **f32)
+        # per-head partial rows (one per 128-row workgroup): policy [8 loss terms | A dlog_std],
+        # value [8 loss terms]; the loss columns each head's gather owns
+        self.nhead_blk = self.ldT // 128
+        self.part_h = [torch.zeros(self.nhead_blk, 8 + A, **f32), torch.zeros(self.nhead_blk, 8, **f32)]
+        self.loss_mask = [0b111101, 0b000010]
+        self.head_range = [model.head_ranges["policy"], model.head_ranges["value"]]
         if os.environ.get("DPPO_MLP_ROWS"):     # diagnostics: force the fused-kernel row tile
             self.ext.set_mlp_rows(int(os.environ["DPPO_MLP_ROWS"]))
         self.sync_tile()
@@ -165,15 +181,12 @@ class HipEngine:
         for buf, r in ((self.h1pT, lp1.fan_out), (self.h2pT, lp2.fan_out), (self.h1vT, lv1.fan_out),
                        (self.h2vT, lv2.fan_out)):
             storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), 1.0, self.dt)
-        self.split_grad = False          # bucketed gradient (enable_bucketed_grad, multi-rank)
         # wgrad workgroup waves: 8 (A/B: 16-wave workgroups with up to 16-quadrant tiles stream
         # fewer operand rows — 1,792 vs 2,304 per step for v_fc1 — but took 243 vs 226 us per
         # grad call; bf16 only, env DPPO_WGRAD_WAVES=16)
         self.wgrad_waves = int(os.environ.get("DPPO_WGRAD_WAVES", 8))
         if self.dt not in (1, 3):
             self.wgrad_waves = 8
-        self._pending_reduce = []        # async all-reduce works of the current step's buckets
-        self._reduce_stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None
         self._build_wgrad_plan(model)
         # ---- optimizer state ----
         n = model.num_params
@@ -186,7 +199,17 @@ class HipEngine:
         # launch uses one block per entry: A + 8 reduction blocks plus one per 256 elements
         # launch (one element per thread: a grid-stride second pass would double the load latency
         # chain of the blocks that take it) needs A + 8 reduction blocks plus one per 256 elements
-        self.norm_part = torch.zeros(min(4096, (n - self.A + 255) // 256 + self.A + 8), **f32)
+        n_whole = min(4096, (n - self.A + 255) // 256 + self.A + 8)
+        # per-head regions (fixed: every head launch writes each block of its region): policy
+        # [0, np_), value [np_, np_ + nv_)
+        (plo, phi), (vlo, vhi) = self.head_range
+        np_ = min(4096, self.A + 8 + (phi - self.A + 255) // 256)
+        nv_ = min(4096, 8 + (vhi - vlo + 255) // 256)
+        self.norm_regions = [(0, np_), (np_, np_ + nv_)]
+        self.norm_part = torch.zeros(max(n_whole, np_ + nv_), **f32)
+        self.norm_n_whole = n_whole
+        self._norm_n = n_whole       # entries the last Adam path wrote (metrics_pack sums them)
+        self._pending_value = None   # (all-reduce work, step, mean) of a value step not yet applied
         # world-size-1 fast path: grad_gather + no-clip Adam in one launch (DPPO_FUSED_APPLY=0: off)
         self.fused_apply = os.environ.get("DPPO_FUSED_APPLY", "1") != "0"
         self.idx_dev = torch.zeros(self.ldT, dtype=torch.int32, **dev)
@@ -220,34 +243,34 @@ class HipEngine:
 
     # ------------------------------------------------------------------------------------------
     def _build_wgrad_plan(self, model: ActorCritic, target_wgs: Optional[int] = None,
-                          split: Optional[bool] = None, chunks_override: Optional[int] = None) -> None:
+                          chunks_override: Optional[int] = None) -> None:
         """Task lists of the grouped split-K wgrad launches: (layer, output tile, batch chunk),
         output tiles from wgrad_tiles().
 
-        One *bucket* = one wgrad launch + one grad_gather launch over a contiguous flat range of
-        the gradient.  Unbucketed (default): every layer in one bucket.  ``split`` (bucketed
-        gradient, multi-rank): bucket 0 = v_fc1, v_fc2, mu, v (flat [v_fc1.weight, n): 83 % of
-        the parameters, all-reduced asynchronously while) bucket 1 = p_fc1, p_fc2 + log_std +
-        loss sums (flat [0, v_fc1.weight)) computes — each bucket chunked for ~target_wgs
-        workgroups, with its own fp32 partial slab.  ``target_wgs`` defaults to
-        WGRAD_TARGET_WGS (env DPPO_WGRAD_WGS)."""
+        One *bucket* = one wgrad launch + one gather launch over a contiguous flat range of the
+        gradient.  Per-head kernels: bucket 0 = the policy layers (p_fc1, p_fc2, mu; flat
+        [A, v_fc1.weight) — log_std and the policy loss terms come from the policy kernel's
+        partials), bucket 1 = the value layers (v_fc1, v_fc2, v; flat [v_fc1.weight, n)), so
+        each head's chain gathers (and all-reduces) its own range.  One-kernel path: every layer
+        in one bucket.  Each bucket is chunked for ~target_wgs workgroups (default
+        WGRAD_TARGET_WGS, env DPPO_WGRAD_WGS) with its own fp32 partial slab."""
         if target_wgs is None:
             target_wgs = int(os.environ.get("DPPO_WGRAD_WGS", WGRAD_TARGET_WGS))
         if target_wgs <= 0:
             target_wgs = (torch.cuda.get_device_properties(self.device).multi_processor_count
                           if self.device.type == "cuda" else 256)
-        if split is None:
-            split = self.split_grad
         ls = self.L.layers
         names = [l.name for l in ls]
-        if split:
-            groups = [[names.index(n) for n in ("v_fc1", "v_fc2", "mu", "v")],
-                      [names.index(n) for n in ("p_fc1", "p_fc2")]]
-            cut = model.offsets["v_fc1.weight"][0]
-            ranges = [(cut, model.num_params), (self.A, cut)]
+        if self.heads:
+            groups = [[names.index(n) for n in ("p_fc1", "p_fc2", "mu")],
+                      [names.index(n) for n in ("v_fc1", "v_fc2", "v")]]
+            (_, phi), (vlo, vhi) = self.head_range
+            ranges = [(self.A, phi), (vlo, vhi)]
+            partials = [True, False]
         else:
             groups = [list(range(len(ls)))]
             ranges = [(self.A, model.num_params)]
+            partials = [True]
         src = torch.full((model.num_params,), -1, dtype=torch.int64)
         meta = torch.zeros(model.num_params, dtype=torch.int64)
         self.buckets = []
@@ -330,7 +353,7 @@ class HipEngine:
             self.buckets.append({
                 "tasks_host": tasks_host, "tasks": tasks_host.to(self.device),
                 "slab": torch.zeros(base, device=self.device, dtype=torch.float32),
-                "lo": lo, "hi": hi, "partials": bi == len(groups) - 1})
+                "lo": lo, "hi": hi, "partials": partials[bi]})
         src[src < 0] = 0  # log_std entries (handled from the partials)
         self.src_off = src.to(torch.int32).to(self.device)
         self.src_meta = meta.to(torch.int32).to(self.device)
@@ -569,43 +592,12 @@ class HipEngine:
         self._first_step = True
 
     # ------------------------------------------------------------------------------------------
-    @torch.no_grad()
-    def enable_bucketed_grad(self, on: bool = True) -> bool:
-        """Bucketed gradient (multi-rank): the value-side range's all-reduce runs on RCCL's stream
-        while the policy range's wgrad computes (grad(idx, reducer)).  Not with hipGraph replay
-        (a collective cannot sit inside the captured chain).  Returns whether it is on."""
-        on = bool(on) and not self.use_graphs
-        if on != self.split_grad:
-            self.split_grad = on
-            self._build_wgrad_plan(self.model)
-        return on
-
-    def wait_reduce(self) -> None:
-        """order the compute stream after every bucket all-reduce of the last grad() call."""
-        for w in self._pending_reduce:
-            if w is not None:
-                w.wait()
-        self._pending_reduce = []
-
-    def can_fuse_apply(self, extra_grad: float = 0.0) -> bool:
-        """grad(idx, apply=True) is available: one gradient range, no clipping (the Adam step
-        needs no global norm first), eager launches (the host knows the step number), and no
-        all-reduce between the gradient and the update (the caller checks that: world size 1)."""
-        p = self.p
-        clip = p.max_grad_norm is not None and p.max_grad_norm > 0
-        return (self.fused_apply and not self.use_graphs and not extra_grad and not clip
-                and len(self.buckets) == 1 and self.buckets[0]["partials"])
-
-    def grad(self, idx: Optional[torch.Tensor], reducer=None, apply: bool = False) -> None:
-        """one minibatch gradient into grad_flat.  ``reducer(t) -> work`` (bucketed mode): called
-        on each bucket's flat range as soon as it is gathered (async all-reduce); finish with
-        wait_reduce() before apply().  ``apply=True`` (only when can_fuse_apply()): the gather
-        and the Adam step run as ONE launch — the same update as grad() then apply()."""
-        p = self.p
+    def _minibatch(self, idx: Optional[torch.Tensor]):
+        """(index tensor, row0, first-step flag, x^T-ready flag) of one minibatch call"""
         M = self.mb
         if idx is None:
-            idx_t, row0 = self.empty, 0
             assert M == self.N, "full-batch call needs minibatch == buffer"
+            idx_t = self.empty
         else:
             idx = idx.reshape(-1)
             if idx.numel() != M:
@@ -614,66 +606,188 @@ class HipEngine:
             if lo < 0 or hi >= self.N:   # host-side range check (the launch skips the device check)
                 raise IndexError(f"minibatch indices out of range [0, {self.N}): {lo}..{hi}")
             self.idx_dev[:M].copy_(idx.to(torch.int32), non_blocking=True)
-            idx_t, row0 = self.idx_dev, 0
+            idx_t = self.idx_dev
         first, xt_ready = bool(self._first_step), bool(idx is None and self._xT_valid)
-        if apply:
-            assert reducer is None and self.can_fuse_apply(), "fused gather + Adam is not available here"
-            self._launch_grad(idx_t, row0, first, xt_ready, fused_apply=True)
-            self.adam_step += 1
-        elif reducer is not None:
-            assert not self.use_graphs, "bucketed all-reduce cannot run inside a captured graph"
-            self._launch_grad(idx_t, row0, first, xt_ready, reducer)
-        else:
-            self._launch(("grad", idx is None, first, xt_ready),
-                         lambda: self._launch_grad(idx_t, row0, first, xt_ready))
         self._first_step = False
         self._loss_dev = self.loss_sums
+        return idx_t, first, xt_ready
+
+    def can_fuse_apply(self, extra_grad: float = 0.0) -> bool:
+        """the one-kernel path's grad(idx, apply=True): one gradient range, no clipping (the Adam
+        step needs no global norm first), eager launches (the host knows the step number), and
+        no all-reduce between the gradient and the update (the caller checks: world size 1)."""
+        p = self.p
+        clip = p.max_grad_norm is not None and p.max_grad_norm > 0
+        return (self.fused_apply and not self.use_graphs and not extra_grad and not clip
+                and (self.heads or (len(self.buckets) == 1 and self.buckets[0]["partials"])))
+
+    def step(self, idx: Optional[torch.Tensor], extra_grad: float = 0.0, allreduce=None,
+             mean: bool = False) -> None:
+        """ONE synchronous global step (train.py:133-175 + chief.py:13-20): the minibatch
+        gradient, its sum (``mean``: average) over ranks, and the Adam step.  ``allreduce(t)``
+        returns an async work handle (the worker's collective), None at world size 1.
+
+        Per-head kernels: each head is its own chain (kernel -> wgrad -> gather -> Adam).  At
+        world size 1 the gather and the Adam step are one launch per head.  With a collective,
+        the policy range's all-reduce is issued as soon as it is gathered and runs while the value
+        head's kernels compute; the value range's all-reduce runs while the policy Adam and the
+        NEXT step's policy kernels compute — its Adam is applied just before the value kernel of
+        the next step (or by finish_steps()).  Each head's Adam step e still precedes that head's
+        kernel of step e+1, so the parameters are exactly the synchronous ones.  Clipping (a
+        global norm over both heads), the Q1 extra gradient and hipGraph replay take the
+        whole-vector path."""
+        p = self.p
+        clip = p.max_grad_norm is not None and p.max_grad_norm > 0
+        if allreduce is None and self.can_fuse_apply(extra_grad):
+            self.grad(idx, apply=True)          # world size 1: gather + Adam in one launch (per head)
+            return
+        if not self.heads:
+            self.grad(idx)
+            if allreduce is not None:
+                self._reduce_wait(allreduce(self.grad_flat), self.grad_flat, mean)
+            self.apply(extra_grad)
+            return
+        idx_t, first, xt_ready = self._minibatch(idx)
+        if clip or extra_grad or self.use_graphs:
+            self._flush_value()
+            self._heads_grad(idx_t, first, xt_ready)
+            if allreduce is not None:
+                self._reduce_wait(allreduce(self.grad_flat), self.grad_flat, mean)
+            self.apply(extra_grad)
+            return
+        if allreduce is None:                   # (DPPO_FUSED_APPLY=0: the two-launch chains, no collective)
+            allreduce = lambda t: None          # noqa: E731
+        step_no = self.adam_step + 1
+        (plo, phi), (vlo, vhi) = self.head_range
+        self._head_chain(0, idx_t, first, xt_ready)
+        wp = allreduce(self.grad_flat[plo:phi])
+        self._flush_value()
+        self._head_chain(1, idx_t, first, xt_ready)
+        self._pending_value = (allreduce(self.grad_flat[vlo:vhi]), step_no, mean)
+        self._reduce_wait(wp, self.grad_flat[plo:phi], mean)
+        self._head_adam(0, step_no)
+        self.adam_step += 1
+        self._norm_n = self.norm_regions[1][1]
+
+    def finish_steps(self) -> None:
+        """apply a value-head step still waiting for its all-reduce (end of the epochs)"""
+        self._flush_value()
+
+    def _flush_value(self) -> None:
+        pend, self._pending_value = self._pending_value, None
+        if pend is None:
+            return
+        work, step_no, mean = pend
+        vlo, vhi = self.head_range[1]
+        self._reduce_wait(work, self.grad_flat[vlo:vhi], mean)
+        self._head_adam(1, step_no)
+
+    def _reduce_wait(self, work, t: torch.Tensor, mean: bool) -> None:
+        if work is not None:
+            work.wait()          # orders the compute stream after RCCL's (no host block on GPU)
+        if mean:
+            t.mul_(1.0 / torch.distributed.get_world_size())
+
+    def _heads_grad(self, idx_t, first: bool, xt_ready: bool) -> None:
+        for h in (0, 1):
+            self._head_chain(h, idx_t, first, xt_ready)
+
+    def _head_chain(self, h: int, idx_t, first: bool, xt_ready: bool, adam_step: int = 0) -> None:
+        """head h's kernel -> its wgrad -> its gather (+ the Adam step when adam_step > 0)."""
+        p, M = self.p, self.mb
+        opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
+                1 if p.std_convention == "var" else 0, 1 if first else 0, self.part_h[h].shape[1], h]
+        self.ext.mlp_train(self.dt, self.x_buf, idx_t, 0, M, self.wimg, self.layout, self.scales,
+                           self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
+                           self.ret, self.values_buf, self.mu_prev, self.v_prev, opts,
+                           [float(p.clip), float(p.ent_coeff)], self.tbufs, self.ldT, self.part_h[h], False,
+                           xt_ready)
+        if h == 0 and p.loss == "dppo_ref":
+            self.log_std_old.copy_(self.model.flat.data[:self.A])   # train.py:164, before Adam moves it
+        b = self.buckets[h]
+        self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
+                       b["tasks_host"], b["slab"], self.wgrad_waves)
+        lo, hi = self.head_range[h]
+        nlog = self.A if h == 0 else 0
+        part = self.part_h[h]
+        if adam_step > 0:
+            b1, b2 = p.adam_betas
+            r0, r1 = self.norm_regions[h]
+            self.ext.gather_adam(b["slab"], self.src_off[lo:hi], self.src_meta[lo:hi], part, self.nhead_blk,
+                                 part.shape[1], self.A, 1.0 / M, self.loss_sums, self.grad_flat[lo:hi],
+                                 self.model.flat.data[lo:hi], self.adam_m[lo:hi], self.adam_v[lo:hi], float(p.lr),
+                                 float(b1), float(b2), float(p.adam_eps), adam_step, self.adam_state,
+                                 self.norm_part[r0:r1], self.wimg, self.w_map[lo:hi], self.wt_map[lo:hi], self.dt,
+                                 self.no_q, nlog, self.loss_mask[h])
+        else:
+            self.ext.grad_gather(b["slab"], self.src_off[lo:hi], self.src_meta[lo:hi], part, self.nhead_blk,
+                                 part.shape[1], self.A, 1.0 / M, self.grad_flat[lo:hi], self.loss_sums, -1, -1,
+                                 True, nlog, self.loss_mask[h])
+
+    def _head_adam(self, h: int, step_no: int) -> None:
+        """no-clip Adam over head h's flat range (after its all-reduce); its norm region"""
+        p = self.p
+        lo, hi = self.head_range[h]
+        r0, r1 = self.norm_regions[h]
+        b1, b2 = p.adam_betas
+        self.ext.adam(self.model.flat.data[lo:hi], self.grad_flat[lo:hi], self.adam_m[lo:hi], self.adam_v[lo:hi],
+                      float(p.lr), float(b1), float(b2), float(p.adam_eps), 0.0, self.adam_state,
+                      self.norm_part[r0:r1], self.wimg, self.w_map[lo:hi], self.wt_map[lo:hi], self.dt, self.no_q,
+                      step_no)
+
+    def grad(self, idx: Optional[torch.Tensor], apply: bool = False) -> None:
+        """one minibatch gradient into grad_flat (no optimizer step; tests / the whole-vector
+        path).  ``apply=True`` (one-kernel path, only when can_fuse_apply()): the gather and the
+        Adam step run as ONE launch — the same update as grad() then apply()."""
+        if self.heads:
+            self._flush_value()
+            idx_t, first, xt_ready = self._minibatch(idx)
+            if apply:
+                assert self.can_fuse_apply(), "fused gather + Adam is not available here"
+                step_no = self.adam_step + 1
+                for h in (0, 1):
+                    self._head_chain(h, idx_t, first, xt_ready, adam_step=step_no)
+                self.adam_step += 1
+                self._norm_n = self.norm_regions[1][1]
+            else:
+                self._heads_grad(idx_t, first, xt_ready)
+            return None
+        idx_t, first, xt_ready = self._minibatch(idx)
+        if apply:
+            assert self.can_fuse_apply(), "fused gather + Adam is not available here"
+            self._launch_grad(idx_t, first, xt_ready, fused_apply=True)
+            self.adam_step += 1
+            self._norm_n = self.norm_n_whole
+        else:
+            self._launch(("grad", idx is None, first, xt_ready),
+                         lambda: self._launch_grad(idx_t, first, xt_ready))
         return None
 
-    def _launch_grad(self, idx_t: torch.Tensor, row0: int, first: bool, xt_ready: bool, reducer=None,
-                     fused_apply: bool = False) -> None:
+    def _launch_grad(self, idx_t: torch.Tensor, first: bool, xt_ready: bool, fused_apply: bool = False) -> None:
         p, M = self.p, self.mb
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
                 1 if p.std_convention == "var" else 0, 1 if first else 0, self.npart]
         fopts = [float(p.clip), float(p.ent_coeff)]
-        self.ext.mlp_train(self.dt, self.x_buf, idx_t, row0, M, self.wimg, self.layout, self.scales,
+        self.ext.mlp_train(self.dt, self.x_buf, idx_t, 0, M, self.wimg, self.layout, self.scales,
                            self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
                            self.ret, self.values_buf, self.mu_prev, self.v_prev, opts, fopts, self.tbufs,
                            self.ldT, self.part, False, xt_ready)
-        ready = []
-        for bi, b in enumerate(self.buckets):
-            self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                           b["tasks_host"], b["slab"], self.wgrad_waves)
-            if fused_apply:
-                if p.loss == "dppo_ref":   # train.py:164: the pre-update log_std, before Adam moves it
-                    self.log_std_old.copy_(self.model.flat.data[:self.A])
-                b1, b2 = p.adam_betas
-                self.ext.gather_adam(b["slab"], self.src_off, self.src_meta, self.part, self.ntrain_blk,
-                                     self.npart, self.A, 1.0 / M, self.loss_sums, self.grad_flat,
-                                     self.model.flat.data, self.adam_m, self.adam_v, float(p.lr), float(b1),
-                                     float(b2), float(p.adam_eps), self.adam_step + 1, self.adam_state,
-                                     self.norm_part, self.wimg, self.w_map, self.wt_map, self.dt, self.no_q)
-                return
-            self.ext.grad_gather(b["slab"], self.src_off, self.src_meta, self.part,
-                                 self.ntrain_blk, self.npart, self.A, 1.0 / M, self.grad_flat, self.loss_sums,
-                                 b["lo"], b["hi"], b["partials"])
-            if reducer is not None and bi < len(self.buckets) - 1:
-                ev = torch.cuda.Event()
-                ev.record()
-                ready.append((b, ev))
-        if reducer is not None:
-            # Bucketed gradient.  Every bucket's kernels are enqueued first; then each earlier
-            # bucket's all-reduce is issued from a side stream that waits on that bucket's
-            # gather event, so RCCL reduces it while the later buckets' wgrad runs on the compute
-            # stream — and the host-side cost of the collective call overlaps GPU work instead of
-            # leaving the GPU idle between launches.
-            for b, ev in ready:
-                self._reduce_stream.wait_event(ev)
-                with torch.cuda.stream(self._reduce_stream):
-                    self._pending_reduce.append(reducer(self.grad_flat[b["lo"]:b["hi"]]))
-            b = self.buckets[-1]
-            lo = 0 if b["partials"] else b["lo"]        # the partials bucket also owns log_std
-            self._pending_reduce.append(reducer(self.grad_flat[lo:b["hi"]]))
+        b = self.buckets[0]
+        self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
+                       b["tasks_host"], b["slab"], self.wgrad_waves)
+        if fused_apply:
+            if p.loss == "dppo_ref":   # train.py:164: the pre-update log_std, before Adam moves it
+                self.log_std_old.copy_(self.model.flat.data[:self.A])
+            b1, b2 = p.adam_betas
+            self.ext.gather_adam(b["slab"], self.src_off, self.src_meta, self.part, self.ntrain_blk,
+                                 self.npart, self.A, 1.0 / M, self.loss_sums, self.grad_flat,
+                                 self.model.flat.data, self.adam_m, self.adam_v, float(p.lr), float(b1),
+                                 float(b2), float(p.adam_eps), self.adam_step + 1, self.adam_state,
+                                 self.norm_part[:self.norm_n_whole], self.wimg, self.w_map, self.wt_map, self.dt,
+                                 self.no_q, self.A, 0xff)
+            return
+        self.ext.grad_gather(b["slab"], self.src_off, self.src_meta, self.part, self.ntrain_blk, self.npart,
+                             self.A, 1.0 / M, self.grad_flat, self.loss_sums, b["lo"], b["hi"], True, self.A, 0xff)
         if p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])  # train.py:164
 
@@ -684,7 +798,7 @@ class HipEngine:
         images, minibatch index buffer), and every buffer it touches is allocated once in ``__init__`` and
         only ever updated in place, so one capture per (chain, static-flag) key replays correctly for the
         whole run. The first call of a key runs eagerly (warm-up: code objects loaded, LDS attributes
-        set), the second captures and replays.
+        set), the second captures and replays.  (The per-head chains run eagerly.)
         """
         if not self.use_graphs:
             fn()
@@ -703,7 +817,9 @@ class HipEngine:
 
     @torch.no_grad()
     def apply(self, extra_grad: float = 0.0) -> None:
+        """whole-vector Adam (+ clip) after grad() [+ the all-reduce]"""
         p = self.p
+        self._flush_value()
         if extra_grad:
             self.grad_flat.add_(extra_grad)
         mx = float(p.max_grad_norm) if (p.max_grad_norm is not None and p.max_grad_norm > 0) else 0.0
@@ -713,9 +829,10 @@ class HipEngine:
         host_step = 0 if self.use_graphs else self.adam_step + 1
         self._launch(("adam",), lambda: self.ext.adam(
             self.model.flat.data, self.grad_flat, self.adam_m, self.adam_v, float(p.lr), float(b1), float(b2),
-            float(p.adam_eps), mx, self.adam_state, self.norm_part, self.wimg, self.w_map, self.wt_map, self.dt,
-            self.no_q, host_step))
+            float(p.adam_eps), mx, self.adam_state, self.norm_part[:self.norm_n_whole], self.wimg, self.w_map,
+            self.wt_map, self.dt, self.no_q, host_step))
         self.adam_step += 1
+        self._norm_n = self.norm_n_whole
         return None
 
     def pack_metrics(self, ep2: torch.Tensor) -> Optional[torch.Tensor]:
@@ -725,9 +842,9 @@ class HipEngine:
         copy ahead of the next pack)."""
         if self._loss_dev is None:
             return None
-        # every Adam path (fused no-clip, sumsq + clip, graph replay) leaves the per-block sums of
-        # squares of the gradient it applied in norm_part
-        self.ext.metrics_pack(ep2, self._loss_dev, self.norm_part, self.metrics_buf)
+        # every Adam path (fused no-clip, sumsq + clip, graph replay, per head) leaves the per-block
+        # sums of squares of the gradient it applied in norm_part[:_norm_n]
+        self.ext.metrics_pack(ep2, self._loss_dev, self.norm_part[:self._norm_n], self.metrics_buf)
         return self.metrics_buf
 
     def loss_vector(self) -> Optional[torch.Tensor]:

@@ -63,12 +63,6 @@ class DPPOWorker:
                                     device=self.device, max_episode_length=params.max_episode_length)
         self.stats = RunningObsStats(self.spec.obs_dim, self.device)
         self.engine = build_engine(params, self.model, self.env, self.stats, self.device, action_rank)
-        # bucketed gradient all-reduce (GPU, multi-rank): the value-side 83 % of the gradient is
-        # all-reduced on RCCL's stream while the policy-side wgrad still computes
-        want = {"auto": ctx.world_size > 1, "on": True, "off": False}[params.grad_buckets]
-        self.bucketed = bool(want and ctx.collective and params.grad_reduce == "sum"
-                             and hasattr(self.engine, "enable_bucketed_grad")
-                             and self.engine.enable_bucketed_grad(True))
         self.iteration = 0
         self.env_steps = 0            # global (all ranks)
         self.updates = 0
@@ -131,10 +125,12 @@ class DPPOWorker:
         tm.start("rollout")
         side = self._stats_stream if p.obs_norm_update == "rollout" else None
         ro = eng.rollout(stats_stream=side) if side is not None else eng.rollout()
-        # --overlap-rollout (SURVEY §5.8 option b): the previous iteration's final gradient
-        # all-reduce ran on RCCL's stream concurrently with the rollout kernel just enqueued
-        # (which acts with the pre-update weights: a 1-update policy lag, safe for PPO because
-        # logp_old is recorded at rollout).  Wait for it and apply that Adam step now.
+        # --overlap-rollout: the previous iteration's final gradient all-reduce ran on
+        # RCCL's stream concurrently with the rollout just enqueued.  GPU engine (per-head
+        # chains): only the VALUE head's last step was left pending — the rollout reads only the
+        # policy, so this is exact; apply it now, before values() reads the value head.  CPU
+        # engine: the whole last step (a 1-update policy lag, safe for PPO because logp_old is
+        # recorded at rollout).
         self.flush_pending()
         tm.stop("rollout")
         tm.start("obs_stats")
@@ -182,19 +178,14 @@ class DPPOWorker:
                 if p.compat and self.updates == 0:
                     extra = 1.0  # Q1: Shared_grad_buffers start at ones (model.py:51)
                 last = epoch == p.num_epoch - 1 and b == nmb - 1
+                if hasattr(eng, "step"):
+                    # GPU engine: gradient -> (async RCCL all-reduce per head) -> Adam, the heads as
+                    # independent chains whose all-reduces overlap the other head's kernels
+                    ar = (lambda t: self.ctx.allreduce_grads(t, async_op=True)) if self.ctx.collective else None
+                    eng.step(idx, extra, allreduce=ar, mean=mean)
+                    self.updates += 1
+                    continue
                 deferred = p.overlap_rollout and last and not mean and self.ctx.collective
-                if self.bucketed and not deferred:
-                    # R1 bucketed: each gradient range is all-reduced as soon as it is gathered
-                    eng.grad(idx, reducer=lambda t: self.ctx.allreduce_grads(t, async_op=True))
-                    eng.wait_reduce()
-                    eng.apply(extra)
-                    self.updates += 1
-                    continue
-                if (not self.ctx.collective and hasattr(eng, "can_fuse_apply")
-                        and eng.can_fuse_apply(extra)):
-                    eng.grad(idx, apply=True)           # world size 1: gather + Adam, one launch
-                    self.updates += 1
-                    continue
                 eng.grad(idx)
                 if deferred:
                     work = self.ctx.allreduce_grads(eng.grad_flat, async_op=True)
@@ -203,6 +194,8 @@ class DPPOWorker:
                     self.ctx.allreduce_grads(eng.grad_flat, mean=mean)
                     eng.apply(extra)
                 self.updates += 1
+        if hasattr(eng, "finish_steps") and not (p.overlap_rollout and self.ctx.collective):
+            eng.finish_steps()        # the last value-head step's all-reduce + Adam
         if stats_done is not None:
             # order the compute stream after the merge: the metrics read the episode stats, and
             # everything after this iteration (next rollout, snapshots, checkpoints) the stats
@@ -308,6 +301,8 @@ class DPPOWorker:
 
     def flush_pending(self) -> None:
         """complete a deferred (overlapped) all-reduce + Adam step, if any."""
+        if hasattr(self.engine, "finish_steps"):
+            self.engine.finish_steps()
         pend = getattr(self, "_pending", None)
         if pend is None:
             return

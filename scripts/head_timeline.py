@@ -1,0 +1,80 @@
+"""Per-phase cycle timeline of the per-head update kernels (csrc/mlp_head.hip HD_STAMP).
+
+Lane 0 of every wave of every EVERY-th workgroup stamps s_memtime (shader clock) at the phase
+boundaries; this prints the median cycles per phase (max over the 4 waves) for the policy and
+the value kernel at the bench geometry (Humanoid dims, 65,536-row full batch, split-bf16).
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from pytorch_dppo_amd.config import dppo_preset  # noqa: E402
+from pytorch_dppo_amd.envs import get_spec, make_vec_env  # noqa: E402
+from pytorch_dppo_amd.models.actor_critic import ActorCritic  # noqa: E402
+from pytorch_dppo_amd.runtime.engine_hip import HipEngine  # noqa: E402
+from pytorch_dppo_amd.utils.obs_stats import RunningObsStats  # noqa: E402
+
+# stamp i -> i+1 phases (HD_STAMP 0..7), plus fc1 sub-spans from stamps 8 / 9
+PHASES = ["fc1", "fc2", "fc3 wait", "fc3 + loss", "dgrad fc3", "dgrad fc2", "partials"]
+EVERY = 8
+
+
+def main():
+    os.environ.setdefault("DPPO_HEADS", "1")
+    dev = torch.device("cuda", 0)
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536, batch_size=65536,
+                    dtype="bf16x3")
+    spec = get_spec(p.env_name)
+    torch.manual_seed(0)
+    model = ActorCritic(spec.obs_dim, spec.act_dim).to(dev)
+    env = make_vec_env(spec, p.num_envs, device=dev)
+    stats = RunningObsStats(spec.obs_dim, dev)
+    eng = HipEngine(p, model, env, stats, dev, 0)
+    assert eng.heads
+    stats.observes(env.observe())
+    eng.rollout()
+    eng.values()
+    eng.gae()
+    eng.begin_update()
+    ext = eng.ext
+    nblk = eng.nhead_blk
+    out = {}
+    idx_t, first, xt_ready = eng._minibatch(None)
+    ablations = [int(x) for x in os.environ.get("HEAD_ABLATE", "0").split(",")]
+    for h, abl in [(h, a) for a in ablations for h in (0, 1)]:
+        buf = torch.zeros(((nblk + EVERY - 1) // EVERY) * 4 * 16, dtype=torch.int64, device=dev)
+        for _ in range(3):
+            eng._head_chain(h, idx_t, first, xt_ready)
+        torch.cuda.synchronize()
+        ext.set_train_tstamp(buf, EVERY)
+        ext.set_train_ablation(abl)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        eng._head_chain(h, idx_t, first, xt_ready)
+        ev[1].record()
+        torch.cuda.synchronize()
+        ext.set_train_ablation(0)
+        ext.set_train_tstamp(torch.empty(0, dtype=torch.int64, device=dev), 1)
+        t = buf.view(-1, 4, 16).cpu().double()
+        d = t[:, :, 1:8] - t[:, :, 0:7]
+        tot = t[:, :, 7] - t[:, :, 0]
+        res = {"sampled_blocks": t.shape[0], "total_cycles_median": float(tot.max(dim=1).values.median()),
+               "chain_ms": ev[0].elapsed_time(ev[1]),
+               "phases_median_cycles(max over waves)": {ph: float(d[:, :, i].max(dim=1).values.median())
+                                                        for i, ph in enumerate(PHASES)},
+               "fc1_first_span": float((t[:, :, 8] - t[:, :, 0]).max(dim=1).values.median()),
+               "fc1_mid_span(4 k-steps value / 3 stages policy)": float((t[:, :, 9] - t[:, :, 8]).max(dim=1).values.median())}
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        blk = torch.arange(t.shape[0]) * EVERY
+        rnd = blk // ncu
+        res["total_by_round"] = {int(r): float(tot[rnd == r].max(dim=1).values.median()) for r in sorted(set(rnd.tolist()))}
+        out[("policy" if h == 0 else "value") + (f"_ablate{abl}" if abl else "")] = res
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -45,9 +45,9 @@ def test_humanoid_value_fc1_streams_fewer_rows_than_square_tiles():
 
 @pytest.mark.parametrize("waves", [8, 16])
 @pytest.mark.parametrize("aligned", [False, True])
-@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("heads", [False, True])
 @pytest.mark.parametrize("env", ["Humanoid-v2", "HalfCheetah-v2"])
-def test_plan_tasks_cover_tiles_and_batch_once(env, split, aligned, waves):
+def test_plan_tasks_cover_tiles_and_batch_once(env, heads, aligned, waves):
     """The full task list (HipEngine._build_wgrad_plan run on a CPU stand-in): each output tile's
     tasks cover the batch rows [0, ldT) exactly once with 64-row-aligned chunks, every task owns
     a disjoint slab region, the task count is ~one per CU, and every parameter's gather entry
@@ -60,8 +60,8 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, split, aligned, waves):
     spec = get_spec(env)
     model = ActorCritic(spec.obs_dim, spec.act_dim)
     stub = SimpleNamespace(L=model.packed_layout(), ldT=65536, A=spec.act_dim, device=torch.device("cpu"),
-                           split_grad=split, _slab_index=HipEngine._slab_index, wgrad_aligned=aligned,
-                           wgrad_waves=waves)
+                           heads=heads, head_range=[model.head_ranges["policy"], model.head_ranges["value"]],
+                           _slab_index=HipEngine._slab_index, wgrad_aligned=aligned, wgrad_waves=waves)
     HipEngine._build_wgrad_plan(stub, model, target_wgs=256)
     total = 0
     for b in stub.buckets:
@@ -81,4 +81,8 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, split, aligned, waves):
     lo = min(b["lo"] for b in stub.buckets)
     meta = stub.src_meta[lo:]
     assert bool(((meta >> 4) >= 1).all()) and bool(((meta & 15) >= 1).all())
+    if heads:   # per-head buckets: policy [A, v_fc1.weight) (mu included), value [v_fc1.weight, n)
+        (b0, b1) = stub.buckets
+        assert (b0["lo"], b0["hi"]) == (spec.act_dim, model.head_ranges["policy"][1]) and b0["partials"]
+        assert (b1["lo"], b1["hi"]) == model.head_ranges["value"] and not b1["partials"]
     assert total >= 200
