@@ -265,9 +265,12 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   check(actions, "actions", at::kFloat, A);
   const int64_t nrows = actions.numel() / A;
   MlpArgs a = base_mlp((int)dt, L, scales, x_buf, idx, row0, M, wimg, flat, A, check_idx, nrows);
-  TORCH_CHECK(opts.size() == 5 || opts.size() == 6, "opts: loss_kind, value_loss, std_var, first_step, npart[, head]");
-  // head >= 0: one head's per-head streaming kernel (csrc/mlp_head.hip; 0 policy, 1 value)
-  const int head = opts.size() == 6 ? (int)opts[5] : -1;
+  TORCH_CHECK(opts.size() == 5 || opts.size() == 7,
+              "opts: loss_kind, value_loss, std_var, first_step, npart[, head, part_dw]");
+  // head >= 0: one head's per-head streaming kernel (csrc/mlp_head.hip; 0 policy, 1 value) with
+  // its fused narrow-layer weight gradient at partial column part_dw (policy [32][128], value [128])
+  const int head = opts.size() == 7 ? (int)opts[5] : -1;
+  const int part_dw = opts.size() == 7 ? (int)opts[6] : 0;
   TORCH_CHECK(head >= -1 && head <= 1, "head: -1 (both heads, one kernel), 0 policy, 1 value");
   TORCH_CHECK(fopts.size() == 2, "fopts: clip, ent_coeff");
   TORCH_CHECK(tbufs.size() == 11, "11 transposed buffers");
@@ -289,7 +292,10 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
                             L.n_out[0], L.n_out[1], L.n_out[2], L.n_out[3], L.n_out[4], L.n_out[5]};
   for (int i = 0; i < 11; ++i) check(tbufs[i], "transposed buffer", storage_type((int)dt), need[i] * ldT);
   const int npart = (int)opts[4];
-  TORCH_CHECK(npart >= (head == 1 ? 8 : 8 + A), "npart too small");
+  TORCH_CHECK(npart >= 8 + A || (head == 1 && npart >= 8), "npart too small");
+  if (head == 0) TORCH_CHECK(part_dw >= 8 + A && part_dw + 32 * 128 <= npart, "part_dw: policy dW_mu block");
+  if (head == 1) TORCH_CHECK(part_dw >= 8 && part_dw + 128 <= npart, "part_dw: value dW_v block");
+  a.part_dw = part_dw;
   const int nblk = (int)(Mpad / ROWS);
   check(part, "part", at::kFloat, (int64_t)nblk * npart);
   a.log_std_old = log_std_old.data_ptr<float>();
@@ -412,33 +418,32 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
   after_launch(__func__);
 }
 
-// i_lo/i_hi: flat parameter range gathered from the slabs (-1, -1: [A, n)); with_partials: also
-// the first nlog gradients (log_std) and the loss sums of the columns in loss_mask from the
-// per-workgroup partials (the slab range must then start at or after nlog).  grad / src_off /
-// src_meta may be one head's slice of the flat vectors.
+// The gradient of one flat range: slab elements [i_lo, i_hi) (src_meta != 0) as split-K slab
+// sums, and the reduce items (red_col / red_dst: the partial-row column of each, and its flat
+// index in `grad` or -1 - q for loss_out[q]) as column sums of the per-workgroup partial rows.
+// grad / src_off / src_meta may be one head's slice of the flat vectors; red_dst then indexes
+// the slice.  The item tables are validated on the host when the engine builds them
+// (HipEngine._reduce_items): no per-epoch device sync here.
 void grad_gather(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_meta, torch::Tensor part,
-                 int64_t nblk, int64_t npart, int64_t A, double scale, torch::Tensor grad, torch::Tensor loss_out,
-                 int64_t i_lo, int64_t i_hi, bool with_partials, int64_t nlog, int64_t loss_mask) {
+                 int64_t nblk, int64_t npart, torch::Tensor red_col, torch::Tensor red_dst, double scale,
+                 torch::Tensor grad, torch::Tensor loss_out, int64_t i_lo, int64_t i_hi) {
   const int64_t n = grad.numel();
-  if (nlog < 0) nlog = A;
-  if (i_lo < 0) i_lo = nlog;
   if (i_hi < 0) i_hi = n;
-  TORCH_CHECK(0 <= nlog && nlog <= A && (!with_partials || nlog <= i_lo) && i_lo <= i_hi && i_hi <= n,
-              "gather range must lie in [nlog, n)");
-  TORCH_CHECK(loss_mask >= 0 && loss_mask <= 255, "loss_mask");
+  TORCH_CHECK(0 <= i_lo && i_lo <= i_hi && i_hi <= n, "gather range must lie in [0, n)");
   check(grad, "grad", at::kFloat, n);
   check(src_off, "src_off", at::kInt, n);
   check(src_meta, "src_meta", at::kInt, n);
   check(slab, "slab", at::kFloat, 1);
   check(part, "part", at::kFloat, nblk * npart);
   check(loss_out, "loss_out", at::kFloat, 8);
-  TORCH_CHECK(npart >= 8 + (with_partials ? nlog : 0), "npart");
-  // the (offset, chunks x stride) of every element lies inside its bucket's slab by
-  // construction (HipEngine._build_wgrad_plan asserts it once; no per-epoch device sync here)
+  const int64_t nitems = red_col.numel();
+  check(red_col, "red_col", at::kInt, nitems);
+  check(red_dst, "red_dst", at::kInt, nitems);
+  TORCH_CHECK(red_dst.numel() == nitems, "red_col / red_dst sizes");
   launch_grad_gather(slab.data_ptr<float>(), src_off.data_ptr<int>(), src_meta.data_ptr<int>(),
-                     part.data_ptr<float>(), (int)nblk, (int)npart, (int)nlog, (int)loss_mask, (float)scale,
-                     grad.data_ptr<float>(), (int)i_lo, (int)i_hi, with_partials ? 1 : 0, loss_out.data_ptr<float>(),
-                     cur_stream());
+                     part.data_ptr<float>(), (int)nblk, (int)npart, red_col.data_ptr<int>(), red_dst.data_ptr<int>(),
+                     (int)nitems, (float)scale, grad.data_ptr<float>(), (int)i_lo, (int)i_hi,
+                     loss_out.data_ptr<float>(), cur_stream());
   after_launch(__func__);
 }
 
@@ -521,17 +526,15 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, do
   after_launch(__func__);
 }
 
-// grad_gather (partials pass + [nlog, n)) and the no-clip Adam step in one launch (world size 1:
-// nothing runs between them).  Bit-identical parameters to grad_gather -> adam(host_step).  The
-// flat tensors may be one head's slice (nlog = A for the policy slice that starts with log_std,
-// 0 for the value slice; loss_mask = the loss columns that head owns).
+// grad_gather (reduce items + slab elements of [i_lo, n)) and the no-clip Adam step in one
+// launch (world size 1: nothing runs between them).  Bit-identical parameters to grad_gather ->
+// adam(host_step).  The flat tensors may be one head's slice (red_dst indexes the slice).
 void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_meta, torch::Tensor part,
-                 int64_t npblk, int64_t npart, int64_t A, double scale, torch::Tensor loss_out, torch::Tensor g,
-                 torch::Tensor p, torch::Tensor m, torch::Tensor v, double lr, double b1, double b2, double eps,
-                 int64_t step, torch::Tensor state, torch::Tensor norm_part, torch::Tensor wimg, torch::Tensor w_map,
-                 torch::Tensor wt_map, int64_t dt, torch::Tensor qmul, int64_t nlog, int64_t loss_mask) {
-  if (nlog < 0) nlog = A;
-  TORCH_CHECK(0 <= nlog && nlog <= A && loss_mask >= 0 && loss_mask <= 255, "nlog / loss_mask");
+                 int64_t npblk, int64_t npart, torch::Tensor red_col, torch::Tensor red_dst, int64_t i_lo,
+                 double scale, torch::Tensor loss_out, torch::Tensor g, torch::Tensor p, torch::Tensor m,
+                 torch::Tensor v, double lr, double b1, double b2, double eps, int64_t step, torch::Tensor state,
+                 torch::Tensor norm_part, torch::Tensor wimg, torch::Tensor w_map, torch::Tensor wt_map, int64_t dt,
+                 torch::Tensor qmul) {
   const int64_t n = p.numel();
   check(p, "p", at::kFloat, n);
   check(g, "g", at::kFloat, n);
@@ -546,20 +549,22 @@ void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
   check(w_map, "w_map", at::kInt, n);
   check(wt_map, "wt_map", at::kInt, n);
   check(wimg, "wimg", storage_type((int)dt), 1);
-  TORCH_CHECK(npart >= 8 + nlog && nlog < n, "npart / nlog");
+  const int64_t nitems = red_col.numel();
+  check(red_col, "red_col", at::kInt, nitems);
+  check(red_dst, "red_dst", at::kInt, nitems);
+  TORCH_CHECK(red_dst.numel() == nitems && 0 <= i_lo && i_lo <= n, "red_col / red_dst / i_lo");
   TORCH_CHECK(step >= 1, "gather_adam needs the host step number (eager launches only)");
   const int nblk = (int)norm_part.numel();
   check(norm_part, "norm_part", at::kFloat, nblk);
-  TORCH_CHECK(nblk > nlog + 8 && nblk <= 4096, "norm_part must hold more than nlog + 8 blocks");
+  TORCH_CHECK(nblk > (nitems + 63) / 64 && nblk <= 4096, "norm_part must hold more blocks than the reduce blocks");
   const float* q = nullptr;
   if (qmul.defined() && qmul.numel() > 0) { check(qmul, "qmul", at::kFloat, n); q = qmul.data_ptr<float>(); }
   launch_gather_adam(slab.data_ptr<float>(), src_off.data_ptr<int>(), src_meta.data_ptr<int>(),
-                     part.data_ptr<float>(), (int)npblk, (int)npart, (int)nlog, (int)loss_mask, (float)scale,
-                     loss_out.data_ptr<float>(),
-                     g.data_ptr<float>(), p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (int)n,
-                     (float)lr, (float)b1, (float)b2, (float)eps, (int)step, state.data_ptr<float>(),
-                     norm_part.data_ptr<float>(), nblk, wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(),
-                     (int)dt, q, cur_stream());
+                     part.data_ptr<float>(), (int)npblk, (int)npart, red_col.data_ptr<int>(), red_dst.data_ptr<int>(),
+                     (int)nitems, (int)i_lo, (float)scale, loss_out.data_ptr<float>(), g.data_ptr<float>(),
+                     p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (int)n, (float)lr, (float)b1,
+                     (float)b2, (float)eps, (int)step, state.data_ptr<float>(), norm_part.data_ptr<float>(), nblk,
+                     wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q, cur_stream());
   after_launch(__func__);
 }
 

@@ -89,6 +89,8 @@ struct MlpArgs {
   int64_t x_bytes;        // bytes of x_buf (kernels with 32-bit buffer offsets refuse >= 2 GiB)
   float* part;            // [nblk][NPART] per-workgroup partial sums (loss terms, dlog_std)
   int npart;
+  int part_dw;            // per-head kernels: column of the fused narrow-layer weight gradient in a
+                          // partial row (policy: dW_mu [32][128], value: dW_v [128]; bias = column 100)
   // DIAGNOSTIC ONLY (scripts/phase_timeline.py; null in every real run): per-wave s_memtime
   // stamps at the phase boundaries of every tstamp_every-th workgroup, [blk][NW][16]
   unsigned long long* tstamp;
@@ -149,8 +151,8 @@ void set_wgrad_stages(int st);                 // bf16 wgrad DMA ring depth 3 / 
 // grad[i] for i in [i_lo, i_hi) from the slabs (src_off / src_meta: see grad_gather_kernel);
 // with_partials: also log_std grads [0, A) and the 8 loss sums from the per-workgroup partials
 void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part, int nblk,
-                        int npart, int nlog, int loss_mask, float scale, float* grad, int i_lo, int i_hi,
-                        int with_partials, float* loss_out, hipStream_t s);
+                        int npart, const int* red_col, const int* red_dst, int nitems, float scale, float* grad,
+                        int i_lo, int i_hi, float* loss_out, hipStream_t s);
 void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
                 int T, int E, float gamma, float lam, int mode, int seg, hipStream_t s);
 void set_adam_fused(int on);
@@ -161,8 +163,8 @@ void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, 
 // grad_gather (with the partials pass, range [A, n)) + no-clip Adam fused: world size 1 only
 // (no all-reduce between them); nblk = norm_part size, must exceed A + 8
 void launch_gather_adam(const float* slab, const int* src_off, const int* src_meta, const float* part, int npblk,
-                        int npart, int nlog, int loss_mask, float scale, float* loss_out, float* g, float* p,
-                        float* m, float* v,
+                        int npart, const int* red_col, const int* red_dst, int nitems, int i_lo, float scale,
+                        float* loss_out, float* g, float* p, float* m, float* v,
                         int n, float lr, float b1, float b2, float eps, int step, float* state, float* norm_part,
                         int nblk, void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale,
                         hipStream_t s);

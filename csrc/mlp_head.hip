@@ -83,6 +83,10 @@ static_assert(head_lds_bytes<0>() <= 160 * 1024 && head_lds_bytes<1>() <= 160 * 
 // loss scratch (after fc1, in the X ring): dL/dmu | dL/dv [32][SST], then the wave's partials
 static_assert(WROWS * SST + NPF + 32 <= xr_floats<1>(), "loss scratch fits the X ring");
 static_assert(WROWS * 32 <= RB * TILE_F, "mu tile fits the transpose tiles");
+// value: + its 128 dW_v partials; policy: + the [64][36] h2^T half image of the fused dW_mu
+static_assert(WROWS * SST + NPF + 32 + 128 <= xr_floats<1>(), "value partials fit the X ring");
+static_assert(((WROWS * SST + NPF + 32 + 3) & ~3) + 64 * 36 <= xr_floats<0>(), "h2^T image fits the X ring");
+static_assert(4 * 32 * 128 * 4 <= HeadCfg<0>::S * SB, "dW_mu wave tiles fit the ring");
 
 template <int HEAD>
 DEV int fc1_stages(int ks1) { return HEAD == 0 ? (ks1 + 1) >> 1 : 2 * ks1; }
@@ -419,7 +423,6 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
     return P::hi_ptr(reinterpret_cast<T*>(buf), fm_index(lr, mw + 16 * rb + 4 * lg, a.ldT));
   };
   void* const h1T = HEAD == 0 ? a.h1pT : a.h1vT;
-  void* const h2T = HEAD == 0 ? a.h2pT : a.h2vT;
   void* const g2T = HEAD == 0 ? a.g2pT : a.g2vT;
   void* const g1T = HEAD == 0 ? a.g1pT : a.g1vT;
 
@@ -503,13 +506,11 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
   // ---------------- fc2: h1 = tanh(fc1), one k-step's A operand prepared at a time ----------------
   const int n1 = a.n_out[C::L1], n2 = a.n_out[C::L2];
   __bf16* bh1[RB];
-  __bf16* bh2[RB];
   __bf16* bg2[RB];
   __bf16* bg1[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     bh1[rb] = lane_base(h1T, rb);
-    bh2[rb] = lane_base(h2T, rb);
     bg2[rb] = lane_base(g2T, rb);
     bg1[rb] = lane_base(g1T, rb);
   }
@@ -559,15 +560,11 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
     if constexpr (2 * j + 2 < C::K2) {
       nst += prep(std::integral_constant<int, 2 * j + 2>{}, a0);
     } else {
-      // h2 = tanh(fc2) (kept for dgrad fc3); its stores belong to this step
+      // h2 = tanh(fc2), kept in registers for fc3, dgrad fc3 and the fused narrow-layer wgrad
 #pragma unroll
       for (int t = 0; t < 8; ++t)
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-          acc2[rb][t] = act_tanh4<DT_S3>(acc2[rb][t]);
-          store_Tt(bh2[rb], t, tsb, bias_col(acc2[rb][t], 16 * t + lr, n2));   // (bias row 1, padding 0)
-        }
-      nst += 16 * RB;
+        for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = act_tanh4<DT_S3>(acc2[rb][t]);
     }
   });
 
@@ -707,9 +704,6 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
         wpart[6] = wpart[7] = 0.f;
       }
     }
-    // dY^T of mu: item = (feature, 8-row group) of the wave's 32 rows
-    for (int it = lane; it < 4 * A; it += 64)
-      store_T8(a.g3pT, dml, SST, it >> 2, it & 3, it >> 2, mw + 8 * (it & 3), a.ldT);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) ad[rb] = tp_getA(dml + 16 * rb * SST, lane);
   } else {
@@ -755,7 +749,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
       for (int k = 0; k < 6; ++k) wpart[k] = lt[k];
       wpart[6] = wpart[7] = 0.f;
     }
-    // dY^T of v (feature 0) in 8-row groups, and the A operand of dgrad fc3 (K = 32, only k = 0)
+    // the A operand of dgrad fc3 (K = 32, only k = 0 nonzero)
     float dvr[RB];
     {
       const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)dml;
@@ -767,9 +761,33 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
       dvr[0] = d0;
       dvr[1] = d1;
     }
-    if (lane < 4) store_T8(a.g3vT, dml, 1, 0, lane, 0, mw + 8 * lane, a.ldT);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) ad[rb] = split8(f32x8{lg == 0 ? dvr[rb] : 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
+    // the fused v-layer weight gradient over the wave's 32 rows: dW_v[k] = sum_r dL/dv[r] h2[r][k]
+    // (h2 with the bias column 1: k = 100 is the bias gradient) -> the wave's 128 partials
+    {
+      const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)dml;
+      float4 q0, q1;
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:64\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(q0), "=&v"(q1)
+                   : "v"(base + 16u * lg)
+                   : "memory");
+      const f32x4 dq[RB] = {f32x4{q0.x, q0.y, q0.z, q0.w}, f32x4{q1.x, q1.y, q1.z, q1.w}};
+      float* wdw = wpart + NPF + 32;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          const f32x4 h = bias_col(acc2[rb][t], 16 * t + lr, n2);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sacc = fmaf(dq[rb][i], h[i], sacc);
+        }
+        sacc += __shfl_xor(sacc, 16, 64);
+        sacc += __shfl_xor(sacc, 32, 64);
+        if (lg == 0) wdw[16 * t + lr] = sacc;
+      }
+    }
   }
 
   HD_STAMP(4);
@@ -848,12 +866,82 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
   epi(std::integral_constant<int, C::NS4 - 1>{});
   HD_STAMP(6);
 
+  // ---------------- policy: the fused mu-layer weight gradient over the wave's 32 rows ----------------
+  // dW_mu[j][k] = sum_r dL/dmu[r][j] h2[r][k] (h2 with the bias column 1: k = 100 is the bias
+  // gradient) as MFMAs with the rows as K: A = dL/dmu^T (lane j, 8 rows) from the loss tile,
+  // B = h2^T (lane k, 8 rows) through a [k][rows] LDS image, in two 64-feature halves
+  f32x4 dwm[2][8];
+  if constexpr (HEAD == 0) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) dwm[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    Frag am2[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      f32x8 x;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = dml[(8 * lg + e) * SST + 16 * m + lr];
+      am2[m] = split8(x);
+    }
+    constexpr int HLD = 36;                                    // [64 features][HLD] (32 rows + pad)
+    float* h2t = dml + ((WROWS * SST + NPF + 32 + 3) & ~3);    // after the loss tile + partials
+    static_for<0, 2>([&](auto hc) __attribute__((always_inline)) {
+      constexpr int hh = decltype(hc)::value;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int t = 4 * hh + tt;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          // lane (feature 16 t + lr, rows 16 rb + 4 lg .. +3): one 16-byte store
+          const f32x4 h = bias_col(acc2[rb][t], 16 * t + lr, n2);
+          *reinterpret_cast<float4*>(h2t + (16 * tt + lr) * HLD + 16 * rb + 4 * lg) = float4{h[0], h[1], h[2], h[3]};
+        }
+      }
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const float* r = h2t + (16 * tt + lr) * HLD + 8 * lg;
+        const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
+        const Frag bh = split8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
+#pragma unroll
+        for (int m = 0; m < 2; ++m) dwm[m][4 * hh + tt] = P::mma(dwm[m][4 * hh + tt], am2[m], bh);
+      }
+    });
+  }
+
   // ---------------- per-workgroup partials (deterministic fixed order) ----------------
   WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
   __syncthreads();
+  if constexpr (HEAD == 0) {
+    // every wave's dW_mu tile [32][128] into the (now idle) ring, then summed in wave order
+    float* red = reinterpret_cast<float*>(smem) + wave * 32 * 128;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[(16 * m + 4 * lg + i) * 128 + 16 * t + lr] = dwm[m][t][i];
+    __syncthreads();
+    const float* r0 = reinterpret_cast<const float*>(smem);
+    float* dst = a.part + (size_t)blockIdx.x * a.npart + a.part_dw;
+    for (int e = tid; e < 32 * 128; e += NW * 64)
+      dst[e] = ((r0[e] + r0[4096 + e]) + r0[2 * 4096 + e]) + r0[3 * 4096 + e];
+  } else {
+    const float* sc1 = reinterpret_cast<const float*>(smem + (size_t)S * SB);
+    float* dst = a.part + (size_t)blockIdx.x * a.npart + a.part_dw;
+    if (tid < 128) {
+      float sv = 0.f;
+      for (int w = 0; w < NW; ++w) sv += sc1[w * WS_F + WROWS * SST + NPF + 32 + tid];
+      dst[tid] = sv;
+    }
+  }
+  // (each head writes only its own columns — policy: loss terms 0, 2-7 and the A dlog_std;
+  // value: the value-loss column 1 — so both kernels can share one partial buffer)
   const float* sc0 = reinterpret_cast<const float*>(smem + (size_t)S * SB);
-  const int np = HEAD == 0 ? NPF + A : NPF;
-  for (int q = tid; q < np; q += NW * 64) {
+  const int np = HEAD == 0 ? NPF + A : 1;
+  for (int i = tid; i < np; i += NW * 64) {
+    const int q = HEAD == 0 ? (i == 1 ? NPF + A : i) : 1;   // (policy: column 1 is the value's)
+    if (q >= NPF + A) continue;
     float s = 0.f;
     for (int w = 0; w < NW; ++w) s += sc0[w * WS_F + WROWS * SST + q];
     a.part[(size_t)blockIdx.x * a.npart + q] = s;

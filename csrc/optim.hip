@@ -270,16 +270,16 @@ __global__ __launch_bounds__(256) void adam_noclip_kernel(float* __restrict__ p,
 // two, SURVEY K11+K12).  Element i's gradient is formed exactly as grad_gather_kernel forms it
 // (same fixed chunk order, same scale) and handed straight to adam_elem, so the parameters are
 // bit-identical to the grad_gather -> adam_noclip pair; the gradient is still written to g (the
-// metrics fallback reads it).  Grid = norm_part size: blocks [0, nlog) reduce the log_std
-// partials and update parameter j; blocks [nlog, nlog+8) reduce the loss sums (those in
-// loss_mask: a per-head launch owns its head's terms); the rest grid-stride over [nlog, n) — the
-// range may be one head's slice of the flat vectors (runtime/engine_hip.py).  Every block leaves
-// its sum of squares in norm_part (0 for the loss blocks).
+// metrics fallback reads it).  Grid = norm_part size: blocks [0, ceil(nitems / 64)) reduce the
+// partial-row columns of the reduce items (log_std, the loss terms, the per-head kernels' fused
+// narrow-layer weight gradients; item_reduce) and update their parameters; the rest grid-stride
+// over the slab elements of [i_lo, n) — the range may be one head's slice of the flat vectors
+// (runtime/engine_hip.py).  Every block leaves its sum of squares in norm_part.
 template <int DT>
 __global__ __launch_bounds__(256) void gather_adam_kernel(
     const float* __restrict__ slab, const int* __restrict__ src_off, const int* __restrict__ src_meta,
-    const float* __restrict__ part, int npblk, int npart, int nlog, int loss_mask, float scale,
-    float* __restrict__ loss_out,
+    const float* __restrict__ part, int npblk, int npart, const int* __restrict__ red_col,
+    const int* __restrict__ red_dst, int nitems, int i_lo, float scale, float* __restrict__ loss_out,
     float* __restrict__ g, float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, int n, float lr,
     float b1, float b2, float eps, float step, float* __restrict__ state, float* __restrict__ norm_part,
     typename Prec<DT>::T* __restrict__ wimg, const int* __restrict__ w_map, const int* __restrict__ wt_map,
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
   const float bc2 = 1.f - powf(b2, step);
   const float step_size = lr / bc1;
   const float rbc2 = 1.f / sqrtf(bc2);
-  const int nred = nlog + 8;
+  const int nrb = (nitems + 63) / 64;   // reduce blocks
   float ss = 0.f;
   // the optimizer-state loads are issued before the gradient is formed (they do not depend on
   // it), so their latency overlaps the slab loads'
@@ -306,41 +306,38 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
       P::put(wimg, wt_map[i], q);
     }
   };
-  if ((int)blockIdx.x < nred) {
-    const int j = blockIdx.x;
-    const int col = j < nlog ? 8 + j : j - nlog;
-    if (j == 0 && threadIdx.x == 0) {
+  if ((int)blockIdx.x < nrb) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
       state[0] = step;
       state[1] = step;
     }
-    if (j >= nlog && !((loss_mask >> (j - nlog)) & 1)) {   // a loss column this launch does not own
-      if (threadIdx.x == 0) norm_part[j] = 0.f;
-      return;
+    float tot = 0.f;
+    int j;
+    if (item_reduce(part, npblk, npart, red_col, nitems, blockIdx.x, red, tot, j)) {
+      const int d = red_dst[j];
+      if (d >= 0) {
+        const float gi = tot * scale;
+        update(d, gi, m[d], v[d], p[d], w_map[d]);
+        ss = gi * gi;
+      } else {
+        loss_out[-1 - d] = tot;
+      }
     }
-    float s = 0.f;
-    for (int b = threadIdx.x; b < npblk; b += 256) s += part[(size_t)b * npart + col];
-    red[threadIdx.x] = s;
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
+    red[threadIdx.x] = threadIdx.x < 64 ? ss : 0.f;
+    __syncthreads();
+    for (int w = 32; w > 0; w >>= 1) {
       if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
       __syncthreads();
     }
-    if (threadIdx.x == 0) {
-      if (j < nlog) {
-        const float gi = red[0] * scale;
-        update(j, gi, m[j], v[j], p[j], w_map[j]);
-        norm_part[j] = gi * gi;
-      } else {
-        loss_out[j - nlog] = red[0];
-        norm_part[j] = 0.f;
-      }
-    }
+    if (threadIdx.x == 0) norm_part[blockIdx.x] = red[0];
     return;
   }
-  const int nb = gridDim.x - nred;
-  for (int i = nlog + (blockIdx.x - nred) * 256 + threadIdx.x; i < n; i += nb * 256) {
-    const int o = src_off[i];
+  const int nb = gridDim.x - nrb;
+  for (int i = i_lo + (blockIdx.x - nrb) * 256 + threadIdx.x; i < n; i += nb * 256) {
     const int mt = src_meta[i];
+    if (mt == 0) continue;   // a reduce item's element (log_std, the fused narrow layers)
+    const int o = src_off[i];
     const float mi = m[i], vi = v[i], pv = p[i];
     const int wi = w_map[i];
     const int nch = mt >> 4;
@@ -556,13 +553,13 @@ extern "C" void launch_adam(float* p, const float* g, float* m, float* v, int n,
 }
 
 extern "C" void launch_gather_adam(const float* slab, const int* src_off, const int* src_meta, const float* part,
-                                   int npblk, int npart, int nlog, int loss_mask, float scale, float* loss_out,
-                                   float* g, float* p,
+                                   int npblk, int npart, const int* red_col, const int* red_dst, int nitems,
+                                   int i_lo, float scale, float* loss_out, float* g, float* p,
                                    float* m, float* v, int n, float lr, float b1, float b2, float eps, int step,
                                    float* state, float* norm_part, int nblk, void* wimg, const int* w_map,
                                    const int* wt_map, int dt, const float* img_scale, hipStream_t s) {
-#define GA_ARGS slab, src_off, src_meta, part, npblk, npart, nlog, loss_mask, scale, loss_out, g, p, m, v, n, lr, b1, \
-                b2, eps, \
+#define GA_ARGS slab, src_off, src_meta, part, npblk, npart, red_col, red_dst, nitems, i_lo, scale, loss_out, g, p, m, \
+                v, n, lr, b1, b2, eps, \
                 (float)step, state, norm_part
   if (dt == DT_F32)
     hipLaunchKernelGGL(gather_adam_kernel<DT_F32>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (float*)wimg, w_map, wt_map,

@@ -233,47 +233,37 @@ void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
   launch_wgrad_lds_t<DT, S, W, false>(a, s);
 }
 
-// With the partials pass (nred = nlog + 8 > 0):
-//   Workgroups [0, nlog): grad[j] = scale * sum_b part[b*npart + 8 + j]  (log_std, one WG per
-//                      dim, strided partial sums + LDS tree: fixed order, deterministic)
-//   Workgroups [nlog, nlog+8): loss_out[q] = sum_b part[b*npart + q] (loss-term sums for
-//                      logging; only the columns in loss_mask: a per-head gather owns its terms).
-// Workgroups [nred, grid): grad[i] = scale * sum_{c < nch} slab[src_off[i] + c * stride],
-//                    i in [i_lo, i_hi), with (nch, stride) of i's output tile packed in
-//                    src_meta[i] = nch * 16 + stride / 4096 (each tile has its own batch-chunk
-//                    count).  Fixed chunk order: deterministic; no float atomics anywhere.  A
-//                    bucketed gradient (all-reduce of one flat range overlapping the next
-//                    range's wgrad) gathers each range with its own launch.
+// Blocks [0, ceil(nitems / 64)): the reduce items (log_std, loss-term sums, the per-head
+// kernels' fused narrow-layer weight gradients): column sums of the per-workgroup partial rows in
+// a fixed order (item_reduce), grad[d] = scale * sum or loss_out[q] (red_dst).
+// Blocks past them: grad[i] = scale * sum_{c < nch} slab[src_off[i] + c * stride], i in
+// [i_lo, i_hi) with src_meta[i] != 0 (= nch * 16 + stride / 4096, each tile has its own
+// batch-chunk count).  Fixed chunk order: deterministic; no float atomics anywhere.
 __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restrict__ slab,
                                                           const int* __restrict__ src_off,
                                                           const int* __restrict__ src_meta,
                                                           const float* __restrict__ part,
-                                                          int nblk, int npart, int nlog, int loss_mask,
+                                                          int nblk, int npart, const int* __restrict__ red_col,
+                                                          const int* __restrict__ red_dst, int nitems,
                                                           float scale, float* __restrict__ grad, int i_lo,
-                                                          int i_hi, int nred, float* __restrict__ loss_out) {
-  if ((int)blockIdx.x < nred) {
+                                                          int i_hi, float* __restrict__ loss_out) {
+  const int nrb = (nitems + 63) / 64;
+  if ((int)blockIdx.x < nrb) {
     __shared__ float red[256];
-    const int j = blockIdx.x;
-    const int col = j < nlog ? 8 + j : j - nlog;
-    if (j >= nlog && !((loss_mask >> (j - nlog)) & 1)) return;
-    float s = 0.f;
-    for (int b = threadIdx.x; b < nblk; b += 256) s += part[(size_t)b * npart + col];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-      if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      if (j < nlog) grad[j] = red[0] * scale;
-      else loss_out[j - nlog] = red[0];
+    float tot = 0.f;
+    int j;
+    if (item_reduce(part, nblk, npart, red_col, nitems, blockIdx.x, red, tot, j)) {
+      const int d = red_dst[j];
+      if (d >= 0) grad[d] = tot * scale;
+      else loss_out[-1 - d] = tot;
     }
     return;
   }
-  const int nb = gridDim.x - nred;
-  for (int i = i_lo + (blockIdx.x - nred) * 256 + threadIdx.x; i < i_hi; i += nb * 256) {
-    const int o = src_off[i];
+  const int nb = gridDim.x - nrb;
+  for (int i = i_lo + (blockIdx.x - nrb) * 256 + threadIdx.x; i < i_hi; i += nb * 256) {
     const int mt = src_meta[i];
+    if (mt == 0) continue;   // a reduce item's element
+    const int o = src_off[i];
     const int nch = mt >> 4;
     const size_t st = (size_t)(mt & 15) << 12;
     const float s = slab_sum(slab + o, nch, st);
@@ -309,14 +299,13 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
 }
 
 extern "C" void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part,
-                                   int nblk, int npart, int nlog, int loss_mask, float scale, float* grad, int i_lo,
-                                   int i_hi, int with_partials, float* loss_out, hipStream_t s) {
+                                   int nblk, int npart, const int* red_col, const int* red_dst, int nitems,
+                                   float scale, float* grad, int i_lo, int i_hi, float* loss_out, hipStream_t s) {
   int grid = (i_hi - i_lo + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
-  const int nred = with_partials ? nlog + 8 : 0;
-  grid += nred;
+  grid += (nitems + 63) / 64;
   hipLaunchKernelGGL(grad_gather_kernel, dim3(grid), dim3(256), 0, s, slab, src_off, src_meta, part, nblk, npart,
-                     nlog, loss_mask, scale, grad, i_lo, i_hi, nred, loss_out);
+                     red_col, red_dst, nitems, scale, grad, i_lo, i_hi, loss_out);
   HIP_CHECK_LAUNCH();
 }

@@ -139,8 +139,8 @@ class HipEngine:
         # ---- update geometry ----
         self.mb = params.minibatch_rows()
         # per-head streaming kernels (csrc/mlp_head.hip, 128 rows per workgroup): split-bf16 and
-        # the reference network; DPPO_HEADS=1 selects them (A/B while they are tuned)
-        self.heads = (os.environ.get("DPPO_HEADS", "0") != "0"
+        # the reference network; DPPO_HEADS=0 forces the one-kernel update (A/B)
+        self.heads = (os.environ.get("DPPO_HEADS", "1") != "0"
                       and bool(self.ext.head_applies(self.dt, self.layout, A)))
         # operand rows: a multiple of the update kernel's row tile (every row it writes has a
         # column) and of 64 (wgrad consumes k-steps in pairs, csrc/wgrad.hip)
@@ -151,9 +151,19 @@ class HipEngine:
         self.part = torch.zeros(self.ldT // 16, self.npart, **f32)
         # per-head partial rows (one per 128-row workgroup): policy [8 loss terms | A dlog_std],
         # value [8 loss terms]; the loss columns each head's gather owns
+        # policy [loss terms (its columns) | A dlog_std | pad | dW_mu [32][128]], value [loss
+        # column 1 | .. | dW_v [128]] — the narrow output layers' weight gradients are summed in
+        # the head kernels (csrc/mlp_head.hip) instead of streaming two more operand pairs through
+        # the wgrad
         self.nhead_blk = self.ldT // 128
-        self.part_h = [torch.zeros(self.nhead_blk, 8 + A, **f32), torch.zeros(self.nhead_blk, 8, **f32)]
-        self.loss_mask = [0b111101, 0b000010]
+        self.part_dw = [_r(8 + A, 4), 8]
+        np_pol = self.part_dw[0] + 32 * 128
+        self.part_h = [torch.zeros(self.nhead_blk, np_pol, **f32), torch.zeros(self.nhead_blk, 8 + 128, **f32)]
+        # world size 1: both head kernels write ONE partial buffer (policy its columns, value
+        # column 1 and its dW_v after the policy's block) and one wgrad + gather/Adam launch
+        # covers both heads (the observation^T operand is streamed once for p_fc1 and v_fc1)
+        self.part_joint = torch.zeros(self.nhead_blk, np_pol + 128, **f32)
+        self.part_dw_joint = [self.part_dw[0], np_pol]
         self.head_range = [model.head_ranges["policy"], model.head_ranges["value"]]
         if os.environ.get("DPPO_MLP_ROWS"):     # diagnostics: force the fused-kernel row tile
             self.ext.set_mlp_rows(int(os.environ["DPPO_MLP_ROWS"]))
@@ -188,6 +198,13 @@ class HipEngine:
         if self.dt not in (1, 3):
             self.wgrad_waves = 8
         self._build_wgrad_plan(model)
+        if self.heads:
+            # the joint (one-bucket) plan of world size 1 beside the per-head buckets
+            heads_buckets, heads_src = self.buckets, (self.src_off, self.src_meta)
+            self._build_wgrad_plan(model, joint=True)
+            self.joint_bucket, self.joint_src = self.buckets[0], (self.src_off, self.src_meta)
+            self.buckets, (self.src_off, self.src_meta) = heads_buckets, heads_src
+        self.items = self._reduce_items(model)
         # ---- optimizer state ----
         n = model.num_params
         self.grad_flat = torch.zeros(n, **f32)
@@ -243,17 +260,19 @@ class HipEngine:
 
     # ------------------------------------------------------------------------------------------
     def _build_wgrad_plan(self, model: ActorCritic, target_wgs: Optional[int] = None,
-                          chunks_override: Optional[int] = None) -> None:
+                          chunks_override: Optional[int] = None, joint: bool = False) -> None:
         """Task lists of the grouped split-K wgrad launches: (layer, output tile, batch chunk),
         output tiles from wgrad_tiles().
 
         One *bucket* = one wgrad launch + one gather launch over a contiguous flat range of the
-        gradient.  Per-head kernels: bucket 0 = the policy layers (p_fc1, p_fc2, mu; flat
-        [A, v_fc1.weight) — log_std and the policy loss terms come from the policy kernel's
-        partials), bucket 1 = the value layers (v_fc1, v_fc2, v; flat [v_fc1.weight, n)), so
-        each head's chain gathers (and all-reduces) its own range.  One-kernel path: every layer
-        in one bucket.  Each bucket is chunked for ~target_wgs workgroups (default
-        WGRAD_TARGET_WGS, env DPPO_WGRAD_WGS) with its own fp32 partial slab."""
+        gradient.  Per-head kernels: bucket 0 = the policy layers p_fc1, p_fc2 (flat
+        [A, v_fc1.weight)), bucket 1 = the value layers v_fc1, v_fc2 (flat [v_fc1.weight, n)),
+        so each head's chain gathers (and all-reduces) its own range; ``joint`` (world size 1):
+        those four layers in ONE bucket over [A, n).  The narrow output layers mu and v, log_std
+        and the loss terms are the head kernels' reduce items (partial-row columns, _reduce_items),
+        so their elements carry src_meta 0.  One-kernel path: every layer in one bucket.  Each
+        bucket is chunked for ~target_wgs workgroups (default WGRAD_TARGET_WGS, env
+        DPPO_WGRAD_WGS) with its own fp32 partial slab."""
         if target_wgs is None:
             target_wgs = int(os.environ.get("DPPO_WGRAD_WGS", WGRAD_TARGET_WGS))
         if target_wgs <= 0:
@@ -261,9 +280,12 @@ class HipEngine:
                           if self.device.type == "cuda" else 256)
         ls = self.L.layers
         names = [l.name for l in ls]
-        if self.heads:
-            groups = [[names.index(n) for n in ("p_fc1", "p_fc2", "mu")],
-                      [names.index(n) for n in ("v_fc1", "v_fc2", "v")]]
+        if self.heads and joint:
+            groups = [[names.index(n) for n in ("p_fc1", "p_fc2", "v_fc1", "v_fc2")]]
+            ranges = [(self.A, model.num_params)]
+            partials = [True]
+        elif self.heads:
+            groups = [[names.index(n) for n in ("p_fc1", "p_fc2")], [names.index(n) for n in ("v_fc1", "v_fc2")]]
             (_, phi), (vlo, vhi) = self.head_range
             ranges = [(self.A, phi), (vlo, vhi)]
             partials = [True, False]
@@ -346,17 +368,70 @@ class HipEngine:
                 nb = torch.arange(l.fan_out)
                 src[boff:boff + bn], meta[boff:boff + bn] = self._slab_index(tile_off, li, nb,
                                                                              torch.full_like(nb, l.fan_in))
-            # every element this bucket gathers stays inside its slab (grad_gather relies on it)
+            # every element this bucket gathers from its slab stays inside it (grad_gather relies
+            # on it); the elements without a tile (src_meta 0) are reduce items
             so, sm = src[lo:hi], meta[lo:hi]
+            has = sm > 0
             reach = so + ((sm >> 4) - 1).clamp(min=0) * ((sm & 15) << 12)
-            assert bool((so >= 0).all()) and int(reach.max()) < base, "wgrad gather plan exceeds its slab"
+            assert bool((so[has] >= 0).all()) and int(reach[has].max()) < base, "wgrad gather plan exceeds its slab"
             self.buckets.append({
                 "tasks_host": tasks_host, "tasks": tasks_host.to(self.device),
                 "slab": torch.zeros(base, device=self.device, dtype=torch.float32),
                 "lo": lo, "hi": hi, "partials": partials[bi]})
-        src[src < 0] = 0  # log_std entries (handled from the partials)
+        src[src < 0] = 0  # reduce items (log_std, and with the per-head kernels mu / v)
         self.src_off = src.to(torch.int32).to(self.device)
         self.src_meta = meta.to(torch.int32).to(self.device)
+
+    def _reduce_items(self, model: ActorCritic) -> Dict[str, tuple]:
+        """Reduce items of the gather launches: (partial-row column, destination) pairs, the
+        destination a flat index of the gathered range or -1 - q for the loss term q.  "legacy":
+        the one-kernel update's [8 loss terms | A dlog_std] rows; "policy" / "value": one head's
+        partial buffer (its loss columns, log_std, and mu / v from the fused dW blocks), the value
+        destinations relative to its slice; "joint": both heads in the shared buffer."""
+        A = self.A
+        cols: Dict[str, list] = {k: [] for k in ("legacy", "policy", "value", "joint")}
+        dsts: Dict[str, list] = {k: [] for k in cols}
+
+        def add(kind, c, d):
+            cols[kind].append(int(c))
+            dsts[kind].append(int(d))
+        for q in range(8):
+            add("legacy", q, -1 - q)
+        for j in range(A):
+            add("legacy", 8 + j, j)
+        vlo = self.head_range[1][0]
+
+        def narrow(kind, layer, dw, base):
+            """the weight gradient of the narrow layer (rows j, k <= fan_in: k == fan_in is the bias)"""
+            l = model.layer(layer)
+            wo, bo = model.offsets[f"{layer}.weight"][0], model.offsets[f"{layer}.bias"][0]
+            for j in range(l.fan_out):
+                for k in range(l.fan_in):
+                    add(kind, dw + j * 128 + k, wo - base + j * l.fan_in + k)
+                add(kind, dw + j * 128 + l.fan_in, bo - base + j)
+        for kind, dwp, dwv, vbase in (("policy", self.part_dw[0], None, None),
+                                      ("value", None, self.part_dw[1], vlo),
+                                      ("joint", self.part_dw_joint[0], self.part_dw_joint[1], 0)):
+            if dwp is not None:
+                for q in (0, 2, 3, 4, 5, 6, 7):
+                    add(kind, q, -1 - q)
+                for j in range(A):
+                    add(kind, 8 + j, j)
+                narrow(kind, "mu", dwp, 0)
+            if dwv is not None:
+                add(kind, 1, -2)
+                narrow(kind, "v", dwv, vbase)
+        out = {}
+        for kind in cols:
+            c = torch.tensor(cols[kind], dtype=torch.int32)
+            d = torch.tensor(dsts[kind], dtype=torch.int32)
+            # the gather kernels index part rows and flat slices by these without a device check
+            lim = {"legacy": self.npart, "policy": self.part_h[0].shape[1], "value": self.part_h[1].shape[1],
+                   "joint": self.part_joint.shape[1]}[kind]
+            assert int(c.min()) >= 0 and int(c.max()) < lim, kind
+            assert len(set(d[d >= 0].tolist())) == int((d >= 0).sum()), kind   # one item per element
+            out[kind] = (c.to(self.device), d.to(self.device))
+        return out
 
     @staticmethod
     def _slab_index(tile_off, li, n, k):
@@ -639,7 +714,7 @@ class HipEngine:
         p = self.p
         clip = p.max_grad_norm is not None and p.max_grad_norm > 0
         if allreduce is None and self.can_fuse_apply(extra_grad):
-            self.grad(idx, apply=True)          # world size 1: gather + Adam in one launch (per head)
+            self.grad(idx, apply=True)          # world size 1: gather + Adam in one launch
             return
         if not self.heads:
             self.grad(idx)
@@ -692,37 +767,49 @@ class HipEngine:
         for h in (0, 1):
             self._head_chain(h, idx_t, first, xt_ready)
 
-    def _head_chain(self, h: int, idx_t, first: bool, xt_ready: bool, adam_step: int = 0) -> None:
-        """head h's kernel -> its wgrad -> its gather (+ the Adam step when adam_step > 0)."""
+    def _head_kernel(self, h: int, idx_t, first: bool, xt_ready: bool, part: torch.Tensor, part_dw: int) -> None:
         p, M = self.p, self.mb
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
-                1 if p.std_convention == "var" else 0, 1 if first else 0, self.part_h[h].shape[1], h]
+                1 if p.std_convention == "var" else 0, 1 if first else 0, part.shape[1], h, part_dw]
         self.ext.mlp_train(self.dt, self.x_buf, idx_t, 0, M, self.wimg, self.layout, self.scales,
                            self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
                            self.ret, self.values_buf, self.mu_prev, self.v_prev, opts,
-                           [float(p.clip), float(p.ent_coeff)], self.tbufs, self.ldT, self.part_h[h], False,
-                           xt_ready)
+                           [float(p.clip), float(p.ent_coeff)], self.tbufs, self.ldT, part, False, xt_ready)
         if h == 0 and p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])   # train.py:164, before Adam moves it
+
+    def _joint_step(self, idx_t, first: bool, xt_ready: bool) -> None:
+        """world size 1: policy kernel, value kernel (one shared partial buffer), ONE wgrad over
+        both heads' layers, ONE gather + Adam launch over the whole flat vector"""
+        p, M = self.p, self.mb
+        for h in (0, 1):
+            self._head_kernel(h, idx_t, first, xt_ready, self.part_joint, self.part_dw_joint[h])
+        b = self.joint_bucket
+        self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
+                       b["tasks_host"], b["slab"], self.wgrad_waves)
+        b1, b2 = p.adam_betas
+        src_off, src_meta = self.joint_src
+        rc, rd = self.items["joint"]
+        self.ext.gather_adam(b["slab"], src_off, src_meta, self.part_joint, self.nhead_blk, self.part_joint.shape[1],
+                             rc, rd, self.A, 1.0 / M, self.loss_sums, self.grad_flat, self.model.flat.data,
+                             self.adam_m, self.adam_v, float(p.lr), float(b1), float(b2), float(p.adam_eps),
+                             self.adam_step + 1, self.adam_state, self.norm_part[:self.norm_n_whole], self.wimg,
+                             self.w_map, self.wt_map, self.dt, self.no_q)
+        self.adam_step += 1
+        self._norm_n = self.norm_n_whole
+
+    def _head_chain(self, h: int, idx_t, first: bool, xt_ready: bool) -> None:
+        """head h's kernel -> its wgrad -> its gather into its flat range of grad_flat"""
+        M = self.mb
+        self._head_kernel(h, idx_t, first, xt_ready, self.part_h[h], self.part_dw[h])
         b = self.buckets[h]
         self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
                        b["tasks_host"], b["slab"], self.wgrad_waves)
         lo, hi = self.head_range[h]
-        nlog = self.A if h == 0 else 0
         part = self.part_h[h]
-        if adam_step > 0:
-            b1, b2 = p.adam_betas
-            r0, r1 = self.norm_regions[h]
-            self.ext.gather_adam(b["slab"], self.src_off[lo:hi], self.src_meta[lo:hi], part, self.nhead_blk,
-                                 part.shape[1], self.A, 1.0 / M, self.loss_sums, self.grad_flat[lo:hi],
-                                 self.model.flat.data[lo:hi], self.adam_m[lo:hi], self.adam_v[lo:hi], float(p.lr),
-                                 float(b1), float(b2), float(p.adam_eps), adam_step, self.adam_state,
-                                 self.norm_part[r0:r1], self.wimg, self.w_map[lo:hi], self.wt_map[lo:hi], self.dt,
-                                 self.no_q, nlog, self.loss_mask[h])
-        else:
-            self.ext.grad_gather(b["slab"], self.src_off[lo:hi], self.src_meta[lo:hi], part, self.nhead_blk,
-                                 part.shape[1], self.A, 1.0 / M, self.grad_flat[lo:hi], self.loss_sums, -1, -1,
-                                 True, nlog, self.loss_mask[h])
+        rc, rd = self.items["policy" if h == 0 else "value"]
+        self.ext.grad_gather(b["slab"], self.src_off[lo:hi], self.src_meta[lo:hi], part, self.nhead_blk,
+                             part.shape[1], rc, rd, 1.0 / M, self.grad_flat[lo:hi], self.loss_sums, 0, -1)
 
     def _head_adam(self, h: int, step_no: int) -> None:
         """no-clip Adam over head h's flat range (after its all-reduce); its norm region"""
@@ -744,11 +831,7 @@ class HipEngine:
             idx_t, first, xt_ready = self._minibatch(idx)
             if apply:
                 assert self.can_fuse_apply(), "fused gather + Adam is not available here"
-                step_no = self.adam_step + 1
-                for h in (0, 1):
-                    self._head_chain(h, idx_t, first, xt_ready, adam_step=step_no)
-                self.adam_step += 1
-                self._norm_n = self.norm_regions[1][1]
+                self._joint_step(idx_t, first, xt_ready)
             else:
                 self._heads_grad(idx_t, first, xt_ready)
             return None
@@ -779,15 +862,17 @@ class HipEngine:
             if p.loss == "dppo_ref":   # train.py:164: the pre-update log_std, before Adam moves it
                 self.log_std_old.copy_(self.model.flat.data[:self.A])
             b1, b2 = p.adam_betas
+            rc, rd = self.items["legacy"]
             self.ext.gather_adam(b["slab"], self.src_off, self.src_meta, self.part, self.ntrain_blk,
-                                 self.npart, self.A, 1.0 / M, self.loss_sums, self.grad_flat,
+                                 self.npart, rc, rd, self.A, 1.0 / M, self.loss_sums, self.grad_flat,
                                  self.model.flat.data, self.adam_m, self.adam_v, float(p.lr), float(b1),
                                  float(b2), float(p.adam_eps), self.adam_step + 1, self.adam_state,
                                  self.norm_part[:self.norm_n_whole], self.wimg, self.w_map, self.wt_map, self.dt,
-                                 self.no_q, self.A, 0xff)
+                                 self.no_q)
             return
+        rc, rd = self.items["legacy"]
         self.ext.grad_gather(b["slab"], self.src_off, self.src_meta, self.part, self.ntrain_blk, self.npart,
-                             self.A, 1.0 / M, self.grad_flat, self.loss_sums, b["lo"], b["hi"], True, self.A, 0xff)
+                             rc, rd, 1.0 / M, self.grad_flat, self.loss_sums, b["lo"], b["hi"])
         if p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])  # train.py:164
 

@@ -552,8 +552,10 @@ def test_rccl_world1_allreduce_and_training_step():
 def test_head_chains_through_rccl_bit_identical_to_fused(overlap, monkeypatch):
     """Per-head chains with the collective path (policy all-reduce issued before the value kernel,
     value all-reduce + Adam left pending into the next step — and with --overlap-rollout past
-    the next rollout) through the real RCCL call at world size 1 == the fused per-head
-    gather + Adam launches without collectives: bit-identical parameters after 2 iterations."""
+    the next rollout) through the real RCCL call at world size 1 == the same chains without
+    collectives (DPPO_FUSED_APPLY=0): bit-identical parameters after 2 iterations; and == the
+    joint world-size-1 path (both heads' layers in one wgrad + one gather/Adam) to fp32
+    summation-order tolerance."""
     import torch.distributed as dist
     from pytorch_dppo_amd.parallel.dist import DistContext, init_single_rank_collective
     from pytorch_dppo_amd.runtime.launcher import free_port
@@ -561,10 +563,18 @@ def test_head_chains_through_rccl_bit_identical_to_fused(overlap, monkeypatch):
     monkeypatch.setenv("DPPO_HEADS", "1")
     kw = dict(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 8, batch_size=64 * 8,
               num_epoch=3, dtype="bf16x3", seed=3, overlap_rollout=overlap)
+    wj = DPPOWorker(dppo_preset(**kw), DistContext(device=DEV))     # joint world-1 path
+    for _ in range(2):
+        wj.iteration_step()
+    monkeypatch.setenv("DPPO_FUSED_APPLY", "0")
     w1 = DPPOWorker(dppo_preset(**kw), DistContext(device=DEV))
-    assert w1.engine.heads and len(w1.engine.buckets) == 2
+    assert w1.engine.heads and len(w1.engine.buckets) == 2 and not w1.engine.can_fuse_apply()
     for _ in range(2):
         w1.iteration_step()
+    w1.flush_pending()
+    torch.cuda.synchronize()
+    rel = (w1.model.flat.data - wj.model.flat.data).norm() / wj.model.flat.data.norm()
+    assert rel.item() < 1e-5, rel.item()
     ctx = init_single_rank_collective(DEV, port=free_port())
     ctx.force_collectives = True
     try:

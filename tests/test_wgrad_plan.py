@@ -79,9 +79,16 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads, aligned, waves):
             rs.sort()
             assert rs[0][0] == 0 and rs[-1][1] == stub.ldT and all(a[1] == b_[0] for a, b_ in zip(rs, rs[1:]))
     lo = min(b["lo"] for b in stub.buckets)
-    meta = stub.src_meta[lo:]
-    assert bool(((meta >> 4) >= 1).all()) and bool(((meta & 15) >= 1).all())
-    if heads:   # per-head buckets: policy [A, v_fc1.weight) (mu included), value [v_fc1.weight, n)
+    slab_fed = torch.ones(model.num_params, dtype=torch.bool)
+    slab_fed[:lo] = False
+    if heads:   # mu and v are the head kernels' reduce items (fused dW partials): no tile, meta 0
+        for name in ("mu.weight", "mu.bias", "v.weight", "v.bias"):
+            o, n = model.offsets[name]
+            slab_fed[o:o + n] = False
+    meta = stub.src_meta
+    assert bool(((meta[slab_fed] >> 4) >= 1).all()) and bool(((meta[slab_fed] & 15) >= 1).all())
+    assert bool((meta[~slab_fed] == 0).all())
+    if heads:   # per-head buckets: policy [A, v_fc1.weight), value [v_fc1.weight, n)
         (b0, b1) = stub.buckets
         assert (b0["lo"], b0["hi"]) == (spec.act_dim, model.head_ranges["policy"][1]) and b0["partials"]
         assert (b1["lo"], b1["hi"]) == model.head_ranges["value"] and not b1["partials"]
