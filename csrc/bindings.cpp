@@ -321,7 +321,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   a.xT_ready = xT_ready ? 1 : 0;
   a.ablate = g_train_ablate;
   if (g_tstamp != nullptr) {
-    const int64_t nw = head >= 0 ? 4 : mlp_train_waves((int)dt, a);
+    const int64_t nw = head >= 0 ? mlp_head_waves(head) : mlp_train_waves((int)dt, a);
     TORCH_CHECK(g_tstamp_numel >= ((nblk + g_tstamp_every - 1) / g_tstamp_every) * nw * 16, "tstamp buffer too small");
     a.tstamp = g_tstamp;
     a.tstamp_every = g_tstamp_every;
@@ -612,6 +612,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_train", &mlp_train);
   m.def("head_applies", &head_applies);
   m.def("head_rows", []() { return (int64_t)mlp_head_rows(); });
+  m.def("head_waves", [](int64_t h) { return (int64_t)mlp_head_waves((int)h); });
   m.def("set_head_kernels", [](bool on) { set_head_kernels(on ? 1 : 0); });
   m.def("head_kernels_enabled", []() { return head_kernels_enabled() != 0; });
   m.def("train_lds_bytes", &train_lds_bytes);

@@ -103,6 +103,7 @@ extern "C" int mlp_rs_applies(const MlpArgs& a);
 // per-head streaming update (csrc/mlp_head.hip): head 0 = policy, 1 = value; 128 rows per workgroup
 extern "C" int mlp_head_applies(const MlpArgs& a);
 extern "C" int mlp_head_rows();
+extern "C" int mlp_head_waves(int head);
 extern "C" void launch_mlp_head(int head, const MlpArgs& a, hipStream_t s);
 extern "C" void set_head_kernels(int enable);
 extern "C" int head_kernels_enabled();

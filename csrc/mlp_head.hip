@@ -43,16 +43,21 @@ using Frag = P::Frag;
 
 constexpr float HD_LOG_2PI = 1.8378770664093453f;
 constexpr int NPF = 8;                      // fixed loss-term columns of a partial row
-constexpr int NW = 4, RB = 2;               // waves; 16-row blocks per wave
-constexpr int WROWS = 16 * RB, ROWS = NW * WROWS;   // 32 rows per wave, 128 per workgroup
+constexpr int ROWS = 128;                   // rows per workgroup (both heads)
 constexpr int FB = 2048;                    // bytes of one split-bf16 fragment (512 slots x 4 B)
-constexpr int NSLOT = 16, SPW = NSLOT / NW, SB = NSLOT * FB, GL = 2 * SPW;
+constexpr int NSLOT = 16, SB = NSLOT * FB;  // fragments (bytes) per ring stage
 constexpr int SST = 36, TILE_F = 16 * SST;  // [16][SST] fp32 transpose tile (conflict-free)
 constexpr int MAX_STEPS = 64;
-constexpr int XDMA = 2 * RB;                // DMA instructions of one wave's X fragments of a k-step
 
 template <int HEAD> struct HeadCfg;
+// NW waves of RB 16-row blocks each (NW * 16 * RB = 128 rows).  Policy: 4 waves (one per SIMD,
+// up to 512 registers) of 32 rows — its chain is light, so each weight fragment read from LDS
+// feeds 6 MFMAs.  Value: 8 waves (two per SIMD, 256 registers each) of 16 rows — its 32 fc1
+// tiles fill a wave's registers at one row block, and the SIMD's two waves interleave one's VALU
+// epilogues and LDS transposes with the other's MFMAs (an in-order wave alone runs them back to
+// back).
 template <> struct HeadCfg<0> {   // policy: p_fc1 -> p_fc2 -> mu
+  static constexpr int NW = 4, RB = 2;
   static constexpr int L1 = 0, L2 = 1, L3 = 2;
   static constexpr int N1 = 8, N1R = 7;     // fc1 tiles held / real (100 features + the bias column)
   static constexpr int K2 = 4;              // fc2 k-steps (fc1 output padded to 128)
@@ -62,6 +67,7 @@ template <> struct HeadCfg<0> {   // policy: p_fc1 -> p_fc2 -> mu
   static constexpr int NS4 = 2;             // dgrad fc2 stages (4 output tiles each)
 };
 template <> struct HeadCfg<1> {   // value: v_fc1 -> v_fc2 -> v
+  static constexpr int NW = 8, RB = 1;
   static constexpr int L1 = 3, L2 = 4, L3 = 5;
   static constexpr int N1 = 32, N1R = 32;   // 500 features + the bias column: 32 tiles
   static constexpr int K2 = 16;
@@ -72,21 +78,24 @@ template <> struct HeadCfg<1> {   // value: v_fc1 -> v_fc2 -> v
 };
 
 template <int HEAD>
-constexpr int xr_floats() { return HeadCfg<HEAD>::XS * RB * FB / 4; }
+constexpr int xr_floats() { return HeadCfg<HEAD>::XS * HeadCfg<HEAD>::RB * FB / 4; }
 template <int HEAD>
-constexpr int ws_floats() { return xr_floats<HEAD>() + RB * TILE_F; }
+constexpr int ws_floats() { return xr_floats<HEAD>() + HeadCfg<HEAD>::RB * TILE_F; }
 template <int HEAD>
 constexpr size_t head_lds_bytes() {
-  return (size_t)HeadCfg<HEAD>::S * SB + (size_t)NW * ws_floats<HEAD>() * sizeof(float);
+  return (size_t)HeadCfg<HEAD>::S * SB + (size_t)HeadCfg<HEAD>::NW * ws_floats<HEAD>() * sizeof(float);
 }
+template <int HEAD>
+constexpr int wrows() { return 16 * HeadCfg<HEAD>::RB; }
 static_assert(head_lds_bytes<0>() <= 160 * 1024 && head_lds_bytes<1>() <= 160 * 1024, "LDS");
-// loss scratch (after fc1, in the X ring): dL/dmu | dL/dv [32][SST], then the wave's partials
-static_assert(WROWS * SST + NPF + 32 <= xr_floats<1>(), "loss scratch fits the X ring");
-static_assert(WROWS * 32 <= RB * TILE_F, "mu tile fits the transpose tiles");
+static_assert(HeadCfg<0>::NW * wrows<0>() == ROWS && HeadCfg<1>::NW * wrows<1>() == ROWS, "128 rows per workgroup");
+// loss scratch (after fc1, in the X ring): dL/dmu | dL/dv [rows][SST], then the wave's partials
+static_assert(wrows<0>() * 32 <= HeadCfg<0>::RB * TILE_F, "mu tile fits the transpose tiles");
 // value: + its 128 dW_v partials; policy: + the [64][36] h2^T half image of the fused dW_mu
-static_assert(WROWS * SST + NPF + 32 + 128 <= xr_floats<1>(), "value partials fit the X ring");
-static_assert(((WROWS * SST + NPF + 32 + 3) & ~3) + 64 * 36 <= xr_floats<0>(), "h2^T image fits the X ring");
-static_assert(4 * 32 * 128 * 4 <= HeadCfg<0>::S * SB, "dW_mu wave tiles fit the ring");
+static_assert(wrows<1>() * SST + NPF + 32 + 128 <= xr_floats<1>(), "value partials fit the X ring");
+static_assert(((wrows<0>() * SST + NPF + 32 + 3) & ~3) + 64 * 36 <= xr_floats<0>(), "h2^T image fits the X ring");
+static_assert(HeadCfg<0>::NW * 32 * 128 * 4 <= HeadCfg<0>::S * SB, "dW_mu wave tiles fit the ring");
+static_assert(HeadCfg<0>::RB == 2, "the policy's fused dW_mu takes K = 32 rows from its two row blocks");
 
 template <int HEAD>
 DEV int fc1_stages(int ks1) { return HEAD == 0 ? (ks1 + 1) >> 1 : 2 * ks1; }
@@ -247,6 +256,37 @@ DEV void for_slots(const char* stg, int lane, F&& f) {
   });
 }
 
+// One scheduling region of a stage's fragments q in [Q0, Q1) with bit q of MASK set: all their
+// LDS reads first, then the MFMAs f(q, fragment) INTERLEAVED with other independent work v()
+// (VALU epilogues / operand preparation of the next k-step, their stores and LDS writes): the
+// sched_group_barrier pipeline asks the scheduler for 1 MFMA then up to VPM VALU instructions,
+// NM times, so the VALU issues in the MFMAs' shadow instead of after them (at one wave per SIMD
+// an in-order wave otherwise runs the MFMA block and the VALU block back to back).  v() must not
+// contain inline asm (a scheduling boundary).
+template <unsigned MASK, int Q0, int Q1, int NM, int VPM, typename F, typename V>
+DEV void mma_mix(const char* stg, int lane, F&& f, V&& v) {
+  constexpr int N = Q1 - Q0;
+  Frag b[N];
+  const char* base = stg + lane_off(lane);
+  static_for<0, N>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int q = Q0 + decltype(ic)::value;
+    if constexpr ((MASK >> q) & 1u)
+      b[decltype(ic)::value] = Frag{*reinterpret_cast<const bf16x8*>(base + q * FB),
+                                    *reinterpret_cast<const bf16x8*>(base + q * FB + 512)};
+  });
+  __builtin_amdgcn_sched_barrier(0);
+  static_for<0, N>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int q = Q0 + decltype(ic)::value;
+    if constexpr ((MASK >> q) & 1u) f(std::integral_constant<int, q>{}, b[decltype(ic)::value]);
+  });
+  v();
+  static_for<0, NM>([&](auto) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // 1 MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);   // then VALU
+  });
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int G>
 DEV float xsum(float x) {   // sum over the lanes that differ only in the bits of G (xor tree)
 #pragma unroll
@@ -266,9 +306,13 @@ DEV float xsum(float x) {   // sum over the lanes that differ only in the bits o
   } while (0)
 
 template <int HEAD>
-__global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
+__global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
   using C = HeadCfg<HEAD>;
   constexpr int S = C::S, XS = C::XS;
+  constexpr int NW = C::NW, RB = C::RB, WROWS = 16 * RB;
+  constexpr int SPW = NSLOT / NW, GL = 2 * SPW;   // ring slots / DMA instructions per wave per stage
+  constexpr int XDMA = 2 * RB;                    // DMA instructions of one wave's X fragments of a k-step
+  constexpr int TPR = 64 / WROWS;                 // loss lanes per row
   constexpr int WS_F = ws_floats<HEAD>();
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const int tid = threadIdx.x, lane = tid & 63;
@@ -291,9 +335,9 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
     return a.idx ? a.idx[rr] : a.row0 + rr;
   };
   const int mw = m0 + WROWS * wave;
-  // the loss's row and sub-lane: policy 2 lanes per row (32 rows), value lanes 0-31 one row each
-  const int lrow = HEAD == 0 ? lane >> 1 : lane & 31;
-  const int lsub = HEAD == 0 ? lane & 1 : lane >> 5;
+  // the loss's row and sub-lane: policy 2 lanes per row (32 rows), value lanes 0-15 one row each
+  const int lrow = HEAD == 0 ? lane / TPR : lane % WROWS;
+  const int lsub = HEAD == 0 ? lane % TPR : lane / WROWS;
   const bool lvalid = mw + lrow < a.M;
   const int lsrc = src_of(WROWS * wave + lrow);
 
@@ -339,7 +383,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
     return (uint32_t)(c >> 9);
   };
   const uint32_t cw0 = code16(lane, SPW * wave) | (code16(lane, SPW * wave + 1) << 16);
-  const uint32_t cw1 = code16(lane, SPW * wave + 2) | (code16(lane, SPW * wave + 3) << 16);
+  const uint32_t cw1 = SPW > 2 ? code16(lane, SPW * wave + 2) | (code16(lane, SPW * wave + 3) << 16) : 0u;
 
   // diagnostics only (scripts/head_timeline.py ablations; 0 in every real run): bit 1 no weight
   // DMA, bit 3 no observation DMA, bit 5 no fc1 MFMAs
@@ -348,7 +392,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
     if (abl & 2) return;
     const int l = min(st, MAX_STEPS - 1);
     const uint32_t w01 = __builtin_amdgcn_readlane(cw0, l);
-    const uint32_t w23 = __builtin_amdgcn_readlane(cw1, l);
+    const uint32_t w23 = SPW > 2 ? __builtin_amdgcn_readlane(cw1, l) : 0u;
     __attribute__((address_space(3))) char* stg =
         (__attribute__((address_space(3))) char*)(ring + stage * SB) + SPW * wave * FB;
 #pragma unroll
@@ -516,7 +560,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
   }
   // A operand of fc2 k-step I (h1 features 32 I .. 32 I + 31) for both row blocks: tanh in place,
   // the h1^T stores, the transposes; returns the number of stores
-  auto prep = [&](auto Ic, Frag (&fa)[RB]) __attribute__((always_inline)) -> int {
+  auto prep_a = [&](auto Ic) __attribute__((always_inline)) {
     constexpr int I = decltype(Ic)::value;
     constexpr bool last = I == C::K2 - 1;
     const int c0 = 32 * I + lr;
@@ -531,8 +575,14 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
       store_Tt(bh1[rb], 2 * I + 1, tsb, s1);
       tp_put(tpb + rb * TILE_F, s0, s1, lane);
     }
+  };
+  auto prep_b = [&](Frag (&fa)[RB]) __attribute__((always_inline)) {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) fa[rb] = tp_getA(tpb + rb * TILE_F, lane);
+  };
+  auto prep = [&](auto Ic, Frag (&fa)[RB]) __attribute__((always_inline)) -> int {
+    prep_a(Ic);
+    prep_b(fa);
     return 4 * RB;
   };
   f32x4 acc2[RB][8];
@@ -546,20 +596,29 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
   static_for<0, C::K2 / 2>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     stg = wait_step(nst);
-    for_slots<0x7fu, 0, 8, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    // k-step 2j's MFMAs with k-step 2j+1's operand preparation in their shadow, then k-step
+    // 2j+1's with 2j+2's
+    mma_mix<0x7fu, 0, 8, 7 * RB * 3, 3>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int t = decltype(qc)::value;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a0[rb], b);
-    });
-    nst = prep(std::integral_constant<int, 2 * j + 1>{}, a1);
-    for_slots<0x7f00u, 8, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
-      constexpr int t = decltype(qc)::value - 8;
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a1[rb], b);
-    });
+    }, [&]() __attribute__((always_inline)) { prep_a(std::integral_constant<int, 2 * j + 1>{}); });
+    prep_b(a1);
+    nst = 4 * RB;
     if constexpr (2 * j + 2 < C::K2) {
-      nst += prep(std::integral_constant<int, 2 * j + 2>{}, a0);
+      mma_mix<0x7f00u, 8, 16, 7 * RB * 3, 3>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+        constexpr int t = decltype(qc)::value - 8;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a1[rb], b);
+      }, [&]() __attribute__((always_inline)) { prep_a(std::integral_constant<int, 2 * j + 2>{}); });
+      prep_b(a0);
+      nst += 4 * RB;
     } else {
+      for_slots<0x7f00u, 8, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+        constexpr int t = decltype(qc)::value - 8;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a1[rb], b);
+      });
       // h2 = tanh(fc2), kept in registers for fc3, dgrad fc3 and the fused narrow-layer wgrad
 #pragma unroll
       for (int t = 0; t < 8; ++t)
@@ -743,7 +802,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
       dml[lrow] = dv;   // dL/dv of the wave's 32 rows
     }
 #pragma unroll
-    for (int k = 0; k < 6; ++k) lt[k] = xsum<31>(lt[k]);
+    for (int k = 0; k < 6; ++k) lt[k] = xsum<WROWS - 1>(lt[k]);
     if (lane == 0) {
 #pragma unroll
       for (int k = 0; k < 6; ++k) wpart[k] = lt[k];
@@ -753,13 +812,12 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
     float dvr[RB];
     {
       const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)dml;
-      float d0, d1;
-      asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:64\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&v"(d0), "=&v"(d1)
-                   : "v"(base + 4u * lr)
-                   : "memory");
-      dvr[0] = d0;
-      dvr[1] = d1;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        float d0;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(d0) : "v"(base + 4u * (16 * rb + lr)) : "memory");
+        dvr[rb] = d0;
+      }
     }
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) ad[rb] = split8(f32x8{lg == 0 ? dvr[rb] : 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
@@ -767,12 +825,13 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
     // (h2 with the bias column 1: k = 100 is the bias gradient) -> the wave's 128 partials
     {
       const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)dml;
-      float4 q0, q1;
-      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:64\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&v"(q0), "=&v"(q1)
-                   : "v"(base + 16u * lg)
-                   : "memory");
-      const f32x4 dq[RB] = {f32x4{q0.x, q0.y, q0.z, q0.w}, f32x4{q1.x, q1.y, q1.z, q1.w}};
+      f32x4 dq[RB];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        float4 q0;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(q0) : "v"(base + 16u * (4 * rb + lg)) : "memory");
+        dq[rb] = f32x4{q0.x, q0.y, q0.z, q0.w};
+      }
       float* wdw = wpart + NPF + 32;
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
@@ -954,7 +1013,7 @@ void head_launch(const MlpArgs& a, hipStream_t s) {
   const size_t lds = head_lds_bytes<HEAD>();
   set_max_lds_once<mlp_head_kernel<HEAD>>(lds);
   const int nblk = (a.M + ROWS - 1) / ROWS;
-  hipLaunchKernelGGL((mlp_head_kernel<HEAD>), dim3(nblk), dim3(NW * 64), lds, s, a);
+  hipLaunchKernelGGL((mlp_head_kernel<HEAD>), dim3(nblk), dim3(HeadCfg<HEAD>::NW * 64), lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
@@ -973,6 +1032,7 @@ extern "C" int mlp_head_applies(const MlpArgs& a) {
 }
 
 extern "C" int mlp_head_rows() { return ROWS; }
+extern "C" int mlp_head_waves(int head) { return head == 0 ? HeadCfg<0>::NW : HeadCfg<1>::NW; }
 
 extern "C" void launch_mlp_head(int head, const MlpArgs& a, hipStream_t s) {
   if (head == 0) head_launch<0>(a, s);

@@ -46,7 +46,8 @@ def main():
     idx_t, first, xt_ready = eng._minibatch(None)
     ablations = [int(x) for x in os.environ.get("HEAD_ABLATE", "0").split(",")]
     for h, abl in [(h, a) for a in ablations for h in (0, 1)]:
-        buf = torch.zeros(((nblk + EVERY - 1) // EVERY) * 4 * 16, dtype=torch.int64, device=dev)
+        nw = int(ext.head_waves(h))
+        buf = torch.zeros(((nblk + EVERY - 1) // EVERY) * nw * 16, dtype=torch.int64, device=dev)
         for _ in range(3):
             eng._head_chain(h, idx_t, first, xt_ready)
         torch.cuda.synchronize()
@@ -59,7 +60,7 @@ def main():
         torch.cuda.synchronize()
         ext.set_train_ablation(0)
         ext.set_train_tstamp(torch.empty(0, dtype=torch.int64, device=dev), 1)
-        t = buf.view(-1, 4, 16).cpu().double()
+        t = buf.view(-1, nw, 16).cpu().double()
         d = t[:, :, 1:8] - t[:, :, 0:7]
         tot = t[:, :, 7] - t[:, :, 0]
         res = {"sampled_blocks": t.shape[0], "total_cycles_median": float(tot.max(dim=1).values.median()),
