@@ -50,14 +50,12 @@ constexpr int SST = 36, TILE_F = 16 * SST;  // [16][SST] fp32 transpose tile (co
 constexpr int MAX_STEPS = 64;
 
 template <int HEAD> struct HeadCfg;
-// NW waves of RB 16-row blocks each (NW * 16 * RB = 128 rows).  Policy: 4 waves (one per SIMD,
-// up to 512 registers) of 32 rows — its chain is light, so each weight fragment read from LDS
-// feeds 6 MFMAs.  Value: 8 waves (two per SIMD, 256 registers each) of 16 rows — its 32 fc1
-// tiles fill a wave's registers at one row block, and the SIMD's two waves interleave one's VALU
-// epilogues and LDS transposes with the other's MFMAs (an in-order wave alone runs them back to
-// back).
+// NW waves of RB 16-row blocks each (NW * 16 * RB = 128 rows): 8 waves (two per SIMD, 256
+// registers each) of 16 rows — the SIMD's two waves interleave one's VALU epilogues, loss and LDS
+// transposes with the other's MFMAs (an in-order wave alone runs them back to back; measured on
+// the value kernel: 181k -> 143k cycles per workgroup against 4 waves of 32 rows).
 template <> struct HeadCfg<0> {   // policy: p_fc1 -> p_fc2 -> mu
-  static constexpr int NW = 4, RB = 2;
+  static constexpr int NW = 8, RB = 1;
   static constexpr int L1 = 0, L2 = 1, L3 = 2;
   static constexpr int N1 = 8, N1R = 7;     // fc1 tiles held / real (100 features + the bias column)
   static constexpr int K2 = 4;              // fc2 k-steps (fc1 output padded to 128)
@@ -93,9 +91,9 @@ static_assert(HeadCfg<0>::NW * wrows<0>() == ROWS && HeadCfg<1>::NW * wrows<1>()
 static_assert(wrows<0>() * 32 <= HeadCfg<0>::RB * TILE_F, "mu tile fits the transpose tiles");
 // value: + its 128 dW_v partials; policy: + the [64][36] h2^T half image of the fused dW_mu
 static_assert(wrows<1>() * SST + NPF + 32 + 128 <= xr_floats<1>(), "value partials fit the X ring");
-static_assert(((wrows<0>() * SST + NPF + 32 + 3) & ~3) + 64 * 36 <= xr_floats<0>(), "h2^T image fits the X ring");
-static_assert(HeadCfg<0>::NW * 32 * 128 * 4 <= HeadCfg<0>::S * SB, "dW_mu wave tiles fit the ring");
-static_assert(HeadCfg<0>::RB == 2, "the policy's fused dW_mu takes K = 32 rows from its two row blocks");
+static_assert(((wrows<0>() * SST + NPF + 32 + 3) & ~3) + 64 * 20 <= xr_floats<0>(), "h2^T image fits the X ring");
+static_assert(4 * 32 * 128 * 4 <= HeadCfg<0>::S * SB, "dW_mu tiles of 4 waves fit the ring");
+static_assert(HeadCfg<0>::NW == 8 && HeadCfg<0>::RB == 1, "the fused dW_mu reduction assumes 8 waves of 16 rows");
 
 template <int HEAD>
 DEV int fc1_stages(int ks1) { return HEAD == 0 ? (ks1 + 1) >> 1 : 2 * ks1; }
@@ -344,13 +342,13 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   // loss inputs of this lane's row, loaded before any DMA: older than every ring batch, they never
   // hold up a counted wait (policy: 4 x 16 registers, held through fc1 / fc2)
   const bool ref_loss = a.loss_kind != 0;
-  constexpr int JM = HEAD == 0 ? 16 : 1;   // action dims per lane (policy: j = lsub + 2 q, A <= 32)
+  constexpr int JM = HEAD == 0 ? 32 / TPR : 1;   // action dims per lane (policy: j = lsub + TPR q, A <= 32)
   float actv[JM], lsv[JM], lsov[JM], mupv[JM];
   float l_adv = 0.f, l_ret = 0.f, l_lpo = 0.f, l_vold = 0.f, l_vprev = 0.f;
   if constexpr (HEAD == 0) {
 #pragma unroll
     for (int q = 0; q < JM; ++q) {
-      const int j = lsub + 2 * q;
+      const int j = lsub + TPR * q;
       actv[q] = j < A ? a.actions[(size_t)lsrc * A + j] : 0.f;
       lsv[q] = j < A ? a.log_std[j] : 0.f;
       lsov[q] = (ref_loss && j < A) ? a.log_std_old[j] : 0.f;
@@ -671,9 +669,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         if (16 + lr < A) mus[r * 32 + 16 + lr] = a3[rb][1][i];
       }
     {
-      // zero the wave's dL/dmu tile (columns >= A are the padded K of dgrad fc3)
-      float4* z = reinterpret_cast<float4*>(dml + (lane >> 1) * SST + 16 * (lane & 1));
-      z[0] = z[1] = z[2] = z[3] = float4{0.f, 0.f, 0.f, 0.f};
+      // zero the wave's dL/dmu tile [16][32] (columns >= A are the padded K of dgrad fc3)
+      float4* z = reinterpret_cast<float4*>(dml + (lane >> 2) * SST + 8 * (lane & 3));
+      z[0] = z[1] = float4{0.f, 0.f, 0.f, 0.f};
     }
     const int r = lrow, sub = lsub;
     const bool valid = lvalid;
@@ -684,13 +682,13 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       float logp = 0.f;
 #pragma unroll
       for (int q = 0; q < JM; ++q) {
-        const int j = sub + 2 * q;
+        const int j = sub + TPR * q;
         if (j >= A) break;
         const float lsig = cvar * lsv[q];
         const float z = (actv[q] - mus[r * 32 + j]) * __expf(-lsig);
         logp += -0.5f * z * z - 0.5f * HD_LOG_2PI - lsig;
       }
-      logp += __shfl_xor(logp, 1, 64);
+      logp = xsum<TPR - 1>(logp);
       const float lrat = logp - l_lpo;
       const float ratio = __expf(lrat);
       const float s1 = ratio * l_adv;
@@ -701,7 +699,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       cf = (fabsf(ratio - 1.f) > a.clip) ? 1.f : 0.f;
 #pragma unroll
       for (int q = 0; q < JM; ++q) {
-        const int j = sub + 2 * q;
+        const int j = sub + TPR * q;
         if (j >= A) break;
         const float lsig = cvar * lsv[q];
         const float isig = __expf(-lsig);
@@ -710,14 +708,14 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         dls[q] = valid ? (dlogp * (z * z - 1.f) - a.ent_coeff) * cvar : 0.f;
         lent += -a.ent_coeff * (0.5f + 0.5f * HD_LOG_2PI + lsig);
       }
-      lent += __shfl_xor(lent, 1, 64);
+      lent = xsum<TPR - 1>(lent);
     } else {
       // ---- reference DPPO loss (train.py:142-161): per-dim pdf ratio, variance convention ----
       const float invA = 1.f / (float)A;
       const bool first = a.first_step != 0;
 #pragma unroll
       for (int q = 0; q < JM; ++q) {
-        const int j = sub + 2 * q;
+        const int j = sub + TPR * q;
         if (j >= A) break;
         const float mu = mus[r * 32 + j];
         const float var = __expf(lsv[q]);
@@ -740,9 +738,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         cf += (fabsf(ratio - 1.f) > a.clip) ? invA : 0.f;
         if (valid) a.mu_prev[(size_t)lsrc * A + j] = mu;   // train.py:164 model_old <- model
       }
-      lclip += __shfl_xor(lclip, 1, 64);
-      lent += __shfl_xor(lent, 1, 64);
-      cf += __shfl_xor(cf, 1, 64);
+      lclip = xsum<TPR - 1>(lclip);
+      lent = xsum<TPR - 1>(lent);
+      cf = xsum<TPR - 1>(cf);
     }
     if (sub == 0) {
       const float vm = valid ? 1.f : 0.f;
@@ -750,13 +748,13 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     }
     // the wave's partial sums over its 32 rows (lanes of one sub-lane: xor over lane bits 1-5)
 #pragma unroll
-    for (int q = 0; q < JM; ++q) dls[q] = xsum<62>(dls[q]);
+    for (int q = 0; q < JM; ++q) dls[q] = xsum<63 & ~(TPR - 1)>(dls[q]);
 #pragma unroll
-    for (int k = 0; k < 6; ++k) lt[k] = xsum<62>(lt[k]);
-    if (lane < 2) {
+    for (int k = 0; k < 6; ++k) lt[k] = xsum<63 & ~(TPR - 1)>(lt[k]);
+    if (lane < TPR) {
 #pragma unroll
       for (int q = 0; q < JM; ++q)
-        if (lane + 2 * q < A) wpart[NPF + lane + 2 * q] = dls[q];
+        if (lane + TPR * q < A) wpart[NPF + lane + TPR * q] = dls[q];
       if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) wpart[k] = lt[k];
@@ -925,7 +923,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   epi(std::integral_constant<int, C::NS4 - 1>{});
   HD_STAMP(6);
 
-  // ---------------- policy: the fused mu-layer weight gradient over the wave's 32 rows ----------------
+  // ---------------- policy: the fused mu-layer weight gradient over the wave's rows ----------------
   // dW_mu[j][k] = sum_r dL/dmu[r][j] h2[r][k] (h2 with the bias column 1: k = 100 is the bias
   // gradient) as MFMAs with the rows as K: A = dL/dmu^T (lane j, 8 rows) from the loss tile,
   // B = h2^T (lane k, 8 rows) through a [k][rows] LDS image, in two 64-feature halves
@@ -935,15 +933,16 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int t = 0; t < 8; ++t) dwm[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // (the wave's 16 rows are k = 0-15 of the MFMA's 32: lane groups 2, 3 hold zeros)
     Frag am2[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       f32x8 x;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = dml[(8 * lg + e) * SST + 16 * m + lr];
+      for (int e = 0; e < 8; ++e) x[e] = lg < 2 ? dml[(8 * lg + e) * SST + 16 * m + lr] : 0.f;
       am2[m] = split8(x);
     }
-    constexpr int HLD = 36;                                    // [64 features][HLD] (32 rows + pad)
+    constexpr int HLD = 20;                                    // [64 features][HLD] (16 rows + pad)
     float* h2t = dml + ((WROWS * SST + NPF + 32 + 3) & ~3);    // after the loss tile + partials
     static_for<0, 2>([&](auto hc) __attribute__((always_inline)) {
       constexpr int hh = decltype(hc)::value;
@@ -959,8 +958,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       }
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
-        const float* r = h2t + (16 * tt + lr) * HLD + 8 * lg;
-        const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
+        const float* r = h2t + (16 * tt + lr) * HLD + 8 * (lg & 1);
+        float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
+        if (lg >= 2) x0 = x1 = float4{0.f, 0.f, 0.f, 0.f};
         const Frag bh = split8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
 #pragma unroll
         for (int m = 0; m < 2; ++m) dwm[m][4 * hh + tt] = P::mma(dwm[m][4 * hh + tt], am2[m], bh);
@@ -972,14 +972,26 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
   __syncthreads();
   if constexpr (HEAD == 0) {
-    // every wave's dW_mu tile [32][128] into the (now idle) ring, then summed in wave order
-    float* red = reinterpret_cast<float*>(smem) + wave * 32 * 128;
+    // the 8 waves' dW_mu tiles [32][128] through the (now idle) 64 KiB ring in two rounds:
+    // slot w = wave w + 4's tile, then + wave w's; the 4 slots summed in order (fixed order)
+    float* red = reinterpret_cast<float*>(smem) + (wave & 3) * 32 * 128;
+    if (wave >= 4) {
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int t = 0; t < 8; ++t)
+        for (int t = 0; t < 8; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) red[(16 * m + 4 * lg + i) * 128 + 16 * t + lr] = dwm[m][t][i];
+          for (int i = 0; i < 4; ++i) red[(16 * m + 4 * lg + i) * 128 + 16 * t + lr] = dwm[m][t][i];
+    }
+    __syncthreads();
+    if (wave < 4) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) red[(16 * m + 4 * lg + i) * 128 + 16 * t + lr] += dwm[m][t][i];
+    }
     __syncthreads();
     const float* r0 = reinterpret_cast<const float*>(smem);
     float* dst = a.part + (size_t)blockIdx.x * a.npart + a.part_dw;
