@@ -29,10 +29,6 @@ void after_launch(const char* what) {
   TORCH_CHECK(e == hipSuccess, "debug-sync: ", what, " failed: ", hipGetErrorString(e));
 }
 
-// diagnostics only: phase-ablation mask for mlp_train (scripts/ablate_train.py); always 0 in
-// training runs (the results of an ablated call are not a gradient)
-int g_train_ablate = 0;
-void set_train_ablation(int64_t mask) { g_train_ablate = (int)mask; }
 // diagnostics only: per-phase cycle sums of the rollout kernel (scripts/phase_timeline.py)
 unsigned long long* g_roll_tstamp = nullptr;
 int64_t g_roll_tstamp_numel = 0;
@@ -56,12 +52,6 @@ void set_train_tstamp(torch::Tensor buf, int64_t every) {
 }
 int g_x_stream = 0;     // A/B: non-temporal observation-row loads in the value / update kernels
 void set_x_stream(int64_t on) { g_x_stream = on ? 1 : 0; }
-int g_wgrad_dense = 1;   // split-bf16 wgrad: dense-DMA fragment layout
-int g_wgrad_impl = 0;   // 0: LDS-DMA staged, 1: register-streamed (A/B diagnostics)
-void set_wgrad_impl(int64_t impl) {
-  TORCH_CHECK(impl == 0 || impl == 1, "wgrad impl: 0 LDS-DMA, 1 register");
-  g_wgrad_impl = (int)impl;
-}
 
 // dt 3 (split-bf16): one 4-byte slot per logical element (hi | lo bf16 pairs in 32-byte groups,
 // csrc/common.h Prec<DT_S3>), held in int32 tensors so numel counts logical elements
@@ -282,7 +272,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   check(v_prev, "v_prev", at::kFloat, nrows);
   check(log_std_old, "log_std_old", at::kFloat, A);
   if (head >= 0)
-    TORCH_CHECK(dt == 3 && mlp_head_applies(a), "the per-head kernels cover split-bf16 and the reference network only");
+    TORCH_CHECK((dt == 3 || dt == 1) && mlp_head_applies(a), "the per-head kernels cover split-bf16 / bf16 and the reference network only");
   const int ROWS = head >= 0 ? mlp_head_rows() : mlp_train_rows((int)dt, a);
   TORCH_CHECK(head >= 0 || train_lds_bytes_impl((int)dt, L, A) <= 160 * 1024, "mlp_train tile does not fit LDS");
   const int64_t Mpad = ((M + ROWS - 1) / ROWS) * ROWS;
@@ -319,7 +309,6 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   // a precomputed xT is only valid for the identity row order covering the whole buffer
   TORCH_CHECK(!xT_ready || (a.idx == nullptr && row0 == 0 && ldT == M), "xT_ready needs a full-batch call");
   a.xT_ready = xT_ready ? 1 : 0;
-  a.ablate = g_train_ablate;
   if (g_tstamp != nullptr) {
     const int64_t nw = head >= 0 ? mlp_head_waves(head) : mlp_train_waves((int)dt, a);
     TORCH_CHECK(g_tstamp_numel >= ((nblk + g_tstamp_every - 1) / g_tstamp_every) * nw * 16, "tstamp buffer too small");
@@ -328,7 +317,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   }
   a.part = part.data_ptr<float>();
   if (head >= 0) {
-    launch_mlp_head(head, a, cur_stream());
+    launch_mlp_head((int)dt, (int)head, a, cur_stream());
   } else {
     launch_mlp_train((int)dt, a, cur_stream());
   }
@@ -341,7 +330,7 @@ bool head_applies(int64_t dt, std::vector<int64_t> layout, int64_t A) {
   MlpArgs a{};
   for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
   a.A = (int)A;
-  return dt == 3 && mlp_head_applies(a) != 0;
+  return (dt == 3 || dt == 1) && mlp_head_applies(a) != 0;
 }
 
 int64_t train_lds_bytes(int64_t dt, std::vector<int64_t> layout, int64_t A) {
@@ -353,7 +342,7 @@ int64_t train_rows(int64_t dt, std::vector<int64_t> layout, int64_t A, int64_t x
   MlpArgs a{};
   for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
   a.A = (int)A;
-  a.x_bytes = x_bytes;   // the row tile depends on which kernel the buffer admits
+  a.x_bytes = x_bytes;
   return mlp_train_rows((int)dt, a);
 }
 
@@ -371,12 +360,8 @@ void set_mlp_rows(int64_t rows) {
 }
 
 void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor> xT, std::vector<int64_t> g_rows,
-           std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab,
-           int64_t waves) {
-  TORCH_CHECK(waves == 8 || (waves == 16 && (dt == 1 || dt == 3) && g_wgrad_impl == 0),
-              "wgrad workgroup waves: 8, or 16 for the bf16 / bf16x3 LDS-DMA kernel");
-  TORCH_CHECK(dt != 3 || g_wgrad_impl == 0, "split-bf16 wgrad runs on the LDS-DMA kernel only");
-  const int wmax = (int)waves, smax = waves == 16 ? 8 : 6;
+           std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab) {
+  const int wmax = 8, smax = 6;   // quadrants per task: one per wave of the 8-wave workgroup
   TORCH_CHECK(gT.size() == 6 && xT.size() == 6 && g_rows.size() == 6 && x_rows.size() == 6, "6 layers");
   check(tasks, "tasks", at::kInt, WGRAD_TASK_INTS);
   TORCH_CHECK(tasks.numel() % WGRAD_TASK_INTS == 0, "tasks are 8-int records");
@@ -410,9 +395,6 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
   a.tasks = reinterpret_cast<const WgradTask*>(tasks.data_ptr<int>());
   a.ntasks = ntasks;
   a.slab = slab.data_ptr<float>();
-  a.impl = g_wgrad_impl;
-  a.waves = (int)waves;
-  a.dense = g_wgrad_dense;
   TORCH_CHECK(dt == 0 || dt == 1 || dt == 3, "wgrad runs in fp32, bf16 or bf16x3 (the fp8 mode's update is bf16)");
   launch_wgrad((int)dt, a, cur_stream());
   after_launch(__func__);
@@ -627,14 +609,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     TORCH_CHECK(nw == 4 || nw == 8, "split-bf16 train waves: 4 or 8");
     set_s3_train_waves((int)nw);
   });
-  m.def("s3_stream_state", []() { return (int64_t)s3_stream_state(); });
-  m.def(
-      "set_s3_stream",
-      [](bool enable, int64_t stages, int64_t dense) {
-        TORCH_CHECK(stages == 2 || stages == 3, "split-bf16 streaming update: 2 or 3 ring stages (32 KiB each)");
-        set_s3_stream(enable ? 1 : 0, (int)stages, (int)dense);
-      },
-      py::arg("enable"), py::arg("stages"), py::arg("dense") = -1);
   m.def("set_debug_sync", &set_debug_sync);
   m.def("set_rollout_waves", [](int64_t nw) {
     TORCH_CHECK(nw == 4 || nw == 8, "rollout waves: 4 or 8");
@@ -645,11 +619,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad", &wgrad);
   m.def("grad_gather", &grad_gather);
   m.def("gae", &gae);
-  m.def("set_train_ablation", &set_train_ablation);
-  m.def("set_wgrad_impl", &set_wgrad_impl);
-  m.def("set_wgrad_dense", [](bool on) { g_wgrad_dense = on ? 1 : 0; });
-  m.def("wgrad_dense", []() { return (bool)g_wgrad_dense; });
-  m.def("set_wgrad_stages", [](int64_t st) { set_wgrad_stages((int)st); });
   m.def("set_adam_fused", [](int64_t on) { set_adam_fused((int)on); });
   m.def("obs_reduce", &obs_reduce);
   m.def("obs_merge", &obs_merge);

@@ -82,9 +82,6 @@ struct MlpArgs {
   void* g1pT; void* g2pT; void* g3pT; void* g1vT; void* g2vT; void* g3vT;
   int ldT;                // = M (row length of every transposed buffer)
   int xT_ready;           // 1: xT already holds this call's rows (full-batch: the rollout wrote it)
-  int ablate;             // DIAGNOSTIC ONLY (scripts/ablate_train.py; 0 in every real run): bit0 no
-                          // transposed stores, bit1 skip v_fc1, bit2 skip dgrad chain, bit3 skip loss,
-                          // bit4 skip the observation loads (zero X tile)
   int x_stream;           // 1: non-temporal observation-row loads (A/B knob; 0 default: cached)
   int64_t x_bytes;        // bytes of x_buf (kernels with 32-bit buffer offsets refuse >= 2 GiB)
   float* part;            // [nblk][NPART] per-workgroup partial sums (loss terms, dlog_std)
@@ -97,27 +94,21 @@ struct MlpArgs {
   int tstamp_every;
 };
 
-// row-stationary weight-streaming split-bf16 update (mlp_stream.hip): the default mlp_train
-// kernel for DT_S3 whenever the shapes fit its register tiles
-extern "C" int mlp_rs_applies(const MlpArgs& a);
 // per-head streaming update (csrc/mlp_head.hip): head 0 = policy, 1 = value; 128 rows per workgroup
 extern "C" int mlp_head_applies(const MlpArgs& a);
 extern "C" int mlp_head_rows();
 extern "C" int mlp_head_waves(int head);
-extern "C" void launch_mlp_head(int head, const MlpArgs& a, hipStream_t s);
+extern "C" void launch_mlp_head(int dt, int head, const MlpArgs& a, hipStream_t s);   // dt: bf16x3 or bf16
+extern "C" void launch_mlp_head_value(int dt, const MlpArgs& a, hipStream_t s);   // V(x) on the value head kernel
 extern "C" void set_head_kernels(int enable);
 extern "C" int head_kernels_enabled();
-extern "C" size_t mlp_rs_lds_bytes();
-extern "C" void launch_mlp_train_rs(const MlpArgs& a, hipStream_t s);
-extern "C" void set_s3_stream(int enable, int stages, int dense);   // dense < 0: unchanged
-extern "C" int s3_stream_state();   // 0 off, else ring depth + 10 * dense-DMA layout
 
 struct WgradTask {
   int layer;      // 0..5
   int n0, k0;     // output tile origin
   int m0, m1;     // reduction (batch) range
   int slab;       // slab offset (floats) of this task's [nq*64][kq*64] tile
-  int nq, kq;     // tile extent in 64x64 quadrants (one per wave): nq*kq <= W, nq + kq <= 6 (W 8) / 8 (W 16)
+  int nq, kq;     // tile extent in 64x64 quadrants (one per wave): nq*kq <= 8, nq + kq <= 6
 };
 
 struct WgradArgs {
@@ -127,9 +118,6 @@ struct WgradArgs {
   const WgradTask* tasks;
   int ntasks;
   float* slab;
-  int impl;            // 0: LDS-DMA staged (default), 1: register-streamed (A/B diagnostics)
-  int waves;           // workgroup size of the LDS-DMA kernel: 8, or 16 (bf16; tiles up to 16 quadrants)
-  int dense;           // split-bf16: dense-DMA fragment layout (csrc/mlp_stream.hip frag_lane_off)
 };
 
 extern "C" {
@@ -148,7 +136,6 @@ void set_s3_train_waves(int nw);                // split-bf16 32-row tile: 4 or 
 void set_s3_value_waves(int nw);                // split-bf16 value forward: 4 or 8 waves (A/B)
 int mlp_train_waves(int dt, const MlpArgs& a);  // workgroup waves the launcher will use
 void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
-void set_wgrad_stages(int st);                 // bf16 wgrad DMA ring depth 3 / 4 / 6 (A/B)
 // grad[i] for i in [i_lo, i_hi) from the slabs (src_off / src_meta: see grad_gather_kernel);
 // with_partials: also log_std grads [0, A) and the 8 loss sums from the per-workgroup partials
 void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part, int nblk,

@@ -43,8 +43,7 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 // batch is in flight, so the HBM latency is paid once per tile instead of once per item.
 template <int DT, int NT, typename F>
 DEV void load_rows(const typename Prec<DT>::T* xb, const int* idx, int row0, int m0, int nvalid,
-                   int d, typename Prec<DT>::T* X, int ldx, int ROWS, int tid, F&& between,
-                   bool skip = false, bool stream = false) {
+                   int d, typename Prec<DT>::T* X, int ldx, int ROWS, int tid, F&& between, bool stream = false) {
   constexpr int E16 = 16 / Prec<DT>::BYTES;
   constexpr int B = 8;
   const int chunks = d / E16;
@@ -61,7 +60,7 @@ DEV void load_rows(const typename Prec<DT>::T* xb, const int* idx, int row0, int
       v[j] = make_uint4(0, 0, 0, 0);
       if (r < ROWS) {
         off[j] = r * ldx + c * E16;
-        if (r < nvalid && !skip) {
+        if (r < nvalid) {
           const int src = idx ? idx[m0 + r] : row0 + m0 + r;
           // plain (cached) load: the observation buffer (100 MB at split-bf16) is re-read by every
           // epoch and stays in the 256 MB Infinity Cache between them; measured at the bench
@@ -186,7 +185,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mlp_value_kernel(MlpArgs a) {
                               ldx, ROWS, tid);
   } else {
     load_rows<DT, NT>(reinterpret_cast<const T*>(a.x_buf), a.idx, a.row0, m0, nvalid, a.d_in[3], X, ldx, ROWS, tid,
-                      [] {}, false, a.x_stream != 0);
+                      [] {}, a.x_stream != 0);
   }
   preset_pad<DT>(H1, ld1, ROWS, a.n_out[3], tid, NT);
   preset_pad<DT>(H2, ld2, ROWS, a.n_out[4], tid, NT);
@@ -284,23 +283,21 @@ __global__ __launch_bounds__(NW * 64, (TrainOcc<DT, NW>::V)) void mlp_train_kern
                       preset_pad<DT>(H1p, ld1p, ROWS, a.n_out[0], tid, NT);
                       preset_pad<DT>(H1v, ld1v, ROWS, a.n_out[3], tid, NT);
                     },
-                    (a.ablate & 16) != 0, a.x_stream != 0);
+                    a.x_stream != 0);
   __syncthreads();
   STAMP(1);
   // ---------------- forward ----------------
   // Activations go to the feature-major wgrad operands straight from the MFMA accumulators
   // (rows < n_real; the constant-1 bias row of each buffer is preset once by the host).
-  const bool no_T = (a.ablate & 1) != 0;   // diagnostics only (see MlpArgs::ablate)
-  T* h1pT = no_T ? nullptr : reinterpret_cast<T*>(a.h1pT);
-  T* h2pT = no_T ? nullptr : reinterpret_cast<T*>(a.h2pT);
-  T* h1vT = no_T ? nullptr : reinterpret_cast<T*>(a.h1vT);
-  T* h2vT = no_T ? nullptr : reinterpret_cast<T*>(a.h2vT);
-  if (!a.xT_ready && !no_T) write_transposed<DT, ROWS, NT>(X, ldx, a.d_in[0], a.xT, a.ldT, m0, tid);  // else: rollout wrote it
+  T* h1pT = reinterpret_cast<T*>(a.h1pT);
+  T* h2pT = reinterpret_cast<T*>(a.h2pT);
+  T* h1vT = reinterpret_cast<T*>(a.h1vT);
+  T* h2vT = reinterpret_cast<T*>(a.h2vT);
+  if (!a.xT_ready) write_transposed<DT, ROWS, NT>(X, ldx, a.d_in[0], a.xT, a.ldT, m0, tid);  // else: rollout wrote it
   layer_gemm<DT, HR, SNW, EPI_TANH, true>(X + sh * ldx, ldx, a.d_in[0], W + a.off_w[0], a.n_out[0], H1p + sh * ld1p,
                                           ld1p, a.scale[0], sw, lane, h1pT, a.ldT, m0 + sh, 0, &pf_p);
-  if (!(a.ablate & 2))
-    layer_gemm<DT, ROWS, NW, EPI_TANH, true>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1v, ld1v, a.scale[3],
-                                             wave, lane, h1vT, a.ldT, m0, VR, &pf_v);
+  layer_gemm<DT, ROWS, NW, EPI_TANH, true>(X, ldx, a.d_in[3], W + a.off_w[3], a.n_out[3], H1v, ld1v, a.scale[3],
+                                           wave, lane, h1vT, a.ldT, m0, VR, &pf_v);
   STAMP(2);
   layer_prefetch<DT, HR2, SNW2>(pf_p, W + a.off_w[1], a.d_in[1], a.n_out[1], sw2, lane);
   layer_prefetch<DT, HR2, SNW2>(pf_v, W + a.off_w[4], a.d_in[4], a.n_out[4], sw2, lane, SPLIT2 ? 0 : VR);
@@ -352,7 +349,7 @@ __global__ __launch_bounds__(NW * 64, (TrainOcc<DT, NW>::V)) void mlp_train_kern
   // Every thread works: the TPR consecutive lanes of a row split its A action dims and
   // combine their partial sums (log-prob, clip/entropy terms) with xor-shuffles inside the
   // group, so the per-row serial chain is ceil(A / TPR) dims long instead of A.
-  if (!(a.ablate & 8)) {
+  {
     const int r = lrow_r, sub = lsub, src = lsrc;
     const bool valid = lvalid;
     const float* act = a.actions + (size_t)src * A;
@@ -477,9 +474,8 @@ __global__ __launch_bounds__(NW * 64, (TrainOcc<DT, NW>::V)) void mlp_train_kern
   write_transposed<DT, ROWS, NT>(DV, ldv, 1, a.g3vT, a.ldT, m0, tid);
   STAMP(9);
   // ---------------- dgrad chain (dY^T of every layer stored from the accumulators) --------
-  if (a.ablate & 4) return;   // diagnostics only
-  T* g2pT = no_T ? nullptr : reinterpret_cast<T*>(a.g2pT);
-  T* g2vT = no_T ? nullptr : reinterpret_cast<T*>(a.g2vT);
+  T* g2pT = reinterpret_cast<T*>(a.g2pT);
+  T* g2vT = reinterpret_cast<T*>(a.g2vT);
   layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE, true>(DMU, ldmu, a.d_out[2], W + a.off_wt[2], a.n_out[1], H2p, ld2p,
                                                     a.scale[2], wave, lane, g2pT, a.ldT, m0, 0, &pf_p);
   layer_gemm<DT, ROWS, NW, EPI_DTANH_INPLACE, true>(DV, ldv, a.d_out[5], W + a.off_wt[5], a.n_out[4], H2v, ld2v,
@@ -535,10 +531,9 @@ int train_rows_t(const MlpArgs& a) {
   if constexpr (DT == DT_F32) {
     return 16;
   } else if constexpr (DT == DT_S3) {
-    // the row-stationary streaming kernel (mlp_stream.hip) owns 64 rows per workgroup; otherwise
     // split-bf16 fragments are fp32-sized: the 64-row / 8-wave form spills (2 x 256 VGPRs per
-    // SIMD is not enough), and at Humanoid dims only the 32-row tile fits LDS anyway
-    if (g_rows_override == 0 && mlp_rs_applies(a)) return 64;
+    // SIMD is not enough), and at Humanoid dims only the 32-row tile fits LDS anyway (the
+    // reference network's update runs on the per-head kernels, csrc/mlp_head.hip)
     return g_rows_override == 16 ? 16 : 32;
   } else {
     const int want = g_rows_override;
@@ -587,7 +582,6 @@ int g_s3_train_waves = 8;
 template <int DT>
 int train_waves_t(const MlpArgs& a) {
   const int rows = train_rows_t<DT>(a);
-  if (DT == DT_S3 && rows == 64) return 4;   // streaming kernel
   if (rows == 64) return 8;
   if (DT == DT_S3 && rows == 32 && g_s3_train_waves == 8) return 8;
   return 4;
@@ -600,10 +594,6 @@ void train_t(const MlpArgs& a, hipStream_t s) {
   } else {
     const int rows = train_rows_t<DT>(a);
     if constexpr (DT == DT_S3) {
-      if (rows == 64) {
-        launch_mlp_train_rs(a, s);
-        return;
-      }
       if (rows == 32 && train_waves_t<DT>(a) == 8) {
         train_launch<DT, 32, 8>(a, s);
         return;
@@ -622,11 +612,23 @@ void value_t(const MlpArgs& a, hipStream_t s) {
   if constexpr (DT == DT_F32) {
     value_launch<DT, 32, 4>(a, s);
   } else if constexpr (DT == DT_S3) {
+    // the reference network: the value head's 128-row streaming kernel in forward mode
+    // (csrc/mlp_head.hip; DPPO_HEADS=0 / set_head_kernels(0) keep this kernel)
+    if (mlp_head_applies(a)) {
+      launch_mlp_head_value(DT_S3, a, s);
+      return;
+    }
     // like the update: the 32-row tile takes most of LDS (one workgroup per CU), so a second
     // wave per SIMD is the latency hiding (scripts/ab_train.py: 162 vs 217 us per call)
     if (g_s3_value_waves == 8) value_launch<DT, 32, 8>(a, s);
     else value_launch<DT, 32, 4>(a, s);
   } else {
+    if constexpr (DT == DT_BF16) {
+      if (mlp_head_applies(a)) {   // the value head's 128-row streaming kernel, forward mode
+        launch_mlp_head_value(DT_BF16, a, s);
+        return;
+      }
+    }
     if (value_rows_t<DT>(a) == 64) value_launch<DT, 64, 8>(a, s);
     else value_launch<DT, 32, 4>(a, s);
   }
@@ -635,7 +637,6 @@ void value_t(const MlpArgs& a, hipStream_t s) {
 template <int DT>
 size_t train_lds_any(const MlpArgs& a) {
   const int rows = train_rows_t<DT>(a);
-  if (DT == DT_S3 && rows == 64) return mlp_rs_lds_bytes();
   return rows == 64 ? train_lds<DT, 64>(a) : rows == 32 ? train_lds<DT, 32>(a) : train_lds<DT, 16>(a);
 }
 

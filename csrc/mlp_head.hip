@@ -1,10 +1,11 @@
-// Per-head, row-stationary, weight-streaming fused PPO update (split-bf16, the fp32-accurate
-// headline precision).  SURVEY K4, K5, K8, K10, K11; loss = corrected ppo.py:148-167 or the
-// reference DPPO loss train.py:142-161; the backward of model.py:35-45 through one head.
+// Per-head, row-stationary, weight-streaming fused PPO update, in split-bf16 (bf16x3, the
+// fp32-accurate headline precision) and bf16 (BASELINE configs 2 and 5: the fp8 mode's update
+// runs in bf16).  SURVEY K4, K5, K8, K10, K11; loss = corrected ppo.py:148-167 or the reference
+// DPPO loss train.py:142-161; the backward of model.py:35-45 through one head.
 //
 // The actor-critic's two heads share only their input rows: the policy loss (clip + entropy,
 // log_std) reads p_fc1 -> p_fc2 -> mu, the value loss v_fc1 -> v_fc2 -> v.  So the update runs
-// as TWO kernels, one per head, instead of mlp_stream.hip's one:
+// as TWO kernels, one per head, instead of one over the whole network:
 //  * each head's whole gradient chain (kernel -> wgrad -> gather -> [all-reduce] -> Adam) is
 //    independent of the other head's, so at world size > 1 one head's RCCL all-reduce overlaps
 //    the other head's kernels (runtime/engine_hip.py), the reference's chief sum
@@ -26,10 +27,10 @@
 //            is prepared between the two k-steps' MFMAs
 //   fc3 + loss + dgrad fc3   one stage (fc3 slots 0-7, dgrad fc3 slots 8-14)
 //   dgrad fc2  4 output tiles x 4 k-steps per stage; a stage's dtanh epilogue runs in the next
-// Weights stream through an S-stage LDS ring (16 split-bf16 fragments = 32 KiB per stage, wave w
-// DMAs slots 4w..4w+3 by buffer_load ... lds with the fragment codes of every step held in two
-// VGPRs' lanes); counted vmcnt waits + a raw s_barrier per step (the bookkeeping of
-// mlp_stream.hip: vector-memory operations retire in issue order).
+// Weights stream through an S-stage LDS ring (16 fragments per stage: 32 KiB split-bf16, 16 KiB
+// bf16; wave w DMAs slots 2w, 2w+1 by buffer_load ... lds with the fragment codes of every step
+// held in two VGPRs' lanes); counted vmcnt waits + a raw s_barrier per step (vector-memory
+// operations retire in issue order).
 #include <type_traits>
 
 #include "kernels.h"
@@ -37,17 +38,77 @@
 
 namespace {
 
-using P = Prec<DT_S3>;
-using T = P::T;
-using Frag = P::Frag;
-
 constexpr float HD_LOG_2PI = 1.8378770664093453f;
 constexpr int NPF = 8;                      // fixed loss-term columns of a partial row
 constexpr int ROWS = 128;                   // rows per workgroup (both heads)
-constexpr int FB = 2048;                    // bytes of one split-bf16 fragment (512 slots x 4 B)
-constexpr int NSLOT = 16, SB = NSLOT * FB;  // fragments (bytes) per ring stage
+constexpr int NSLOT = 16;                   // fragments per ring stage
 constexpr int SST = 36, TILE_F = 16 * SST;  // [16][SST] fp32 transpose tile (conflict-free)
 constexpr int MAX_STEPS = 64;
+
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4h;
+
+// Operand precision of the head kernels: how a 512-element fragment sits in global memory and in
+// LDS, and how fp32 register values become MFMA operands / stored wgrad operands.
+template <int DT> struct HT;
+// split-bf16: 2 KiB fragments (lane l: 8 hi then 8 lo bf16), moved as two DMA instructions — the
+// dense layout: instruction h moves lanes 32h .. 32h+31 and lands as [their hi][their lo], so lane
+// l reads hi at (l / 32) KiB + 16 (l % 32), lo 512 bytes on (both conflict-free)
+template <> struct HT<DT_S3> {
+  using P = Prec<DT_S3>;
+  using Frag = P::Frag;
+  static constexpr int FB = 2048, NI = 2;   // fragment bytes, DMA instructions per fragment
+  static constexpr int SPS = 2;             // opnd_store instructions per store4 / store8
+  DEV static int lane_off(int lane) { return (lane >> 5) * 1024 + (lane & 31) * 16; }
+  DEV static unsigned wsrc(int lane) { return (unsigned)((lane & 31) * 32 + (lane >> 5) * 16); }
+  // observation row bytes of lane l's slot in DMA instruction 0 (k-groups 2h, 2h+1 per instruction)
+  DEV static int xlane(int lane) { return 32 * ((lane >> 4) & 1) + 16 * (lane >> 5); }
+  DEV static Frag lds(const char* p) {
+    return Frag{*reinterpret_cast<const bf16x8*>(p), *reinterpret_cast<const bf16x8*>(p + 512)};
+  }
+  DEV static Frag from8(const f32x8& x) {
+    const bf16x8 h = __builtin_convertvector(x, bf16x8);
+    const bf16x8 l = __builtin_convertvector(x - __builtin_convertvector(h, f32x8), bf16x8);
+    return Frag{h, l};
+  }
+  DEV static f32x8 to8(const Frag& f) {
+    return __builtin_convertvector(f.h, f32x8) + __builtin_convertvector(f.l, f32x8);
+  }
+  DEV static char* eptr(void* buf, size_t i) { return reinterpret_cast<char*>(P::hi_ptr(reinterpret_cast<P::T*>(buf), i)); }
+  // 4 consecutive elements of an 8-group (hi at p, lo 16 bytes on)
+  DEV static void store4(char* p, const f32x4& v) {
+    const bf16x4v hv = __builtin_convertvector(v, bf16x4v);
+    const bf16x4v lv = __builtin_convertvector(v - __builtin_convertvector(hv, f32x4), bf16x4v);
+    opnd_store(*reinterpret_cast<const u32x2*>(&hv), reinterpret_cast<u32x2*>(p));
+    opnd_store(*reinterpret_cast<const u32x2*>(&lv), reinterpret_cast<u32x2*>(p + 16));
+  }
+  DEV static void store8(char* p, const f32x8& v) {
+    const Frag f = from8(v);
+    opnd_store(*reinterpret_cast<const u32x4h*>(&f.h), reinterpret_cast<u32x4h*>(p));
+    opnd_store(*reinterpret_cast<const u32x4h*>(&f.l), reinterpret_cast<u32x4h*>(p + 16));
+  }
+};
+// bf16: 1 KiB fragments, lane order, one DMA instruction
+template <> struct HT<DT_BF16> {
+  using P = Prec<DT_BF16>;
+  using Frag = P::Frag;
+  static constexpr int FB = 1024, NI = 1, SPS = 1;
+  DEV static int lane_off(int lane) { return lane * 16; }
+  DEV static unsigned wsrc(int lane) { return (unsigned)lane * 16u; }
+  DEV static int xlane(int lane) { return 16 * (lane >> 4); }
+  DEV static Frag lds(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+  DEV static Frag from8(const f32x8& x) { return __builtin_convertvector(x, bf16x8); }
+  DEV static f32x8 to8(const Frag& f) { return __builtin_convertvector(f, f32x8); }
+  DEV static char* eptr(void* buf, size_t i) { return reinterpret_cast<char*>(reinterpret_cast<__bf16*>(buf) + i); }
+  DEV static void store4(char* p, const f32x4& v) {
+    const bf16x4v hv = __builtin_convertvector(v, bf16x4v);
+    opnd_store(*reinterpret_cast<const u32x2*>(&hv), reinterpret_cast<u32x2*>(p));
+  }
+  DEV static void store8(char* p, const f32x8& v) {
+    const bf16x8 h = __builtin_convertvector(v, bf16x8);
+    opnd_store(*reinterpret_cast<const u32x4h*>(&h), reinterpret_cast<u32x4h*>(p));
+  }
+};
 
 template <int HEAD> struct HeadCfg;
 // NW waves of RB 16-row blocks each (NW * 16 * RB = 128 rows): 8 waves (two per SIMD, 256
@@ -61,8 +122,9 @@ template <> struct HeadCfg<0> {   // policy: p_fc1 -> p_fc2 -> mu
   static constexpr int K2 = 4;              // fc2 k-steps (fc1 output padded to 128)
   static constexpr int N3 = 2;              // fc3 output tiles (A <= 32)
   static constexpr int XS = 4;              // X ring slots (k-steps): 2 per stage, 2 ahead
-  static constexpr int S = 2;               // weight ring stages
+  static constexpr int S3 = 2, SBF = 4;     // weight ring stages (split-bf16 / bf16: 64 KiB)
   static constexpr int NS4 = 2;             // dgrad fc2 stages (4 output tiles each)
+  static constexpr int NEED = 1900;         // per-wave scratch floats: loss tile, partials, h2^T image
 };
 template <> struct HeadCfg<1> {   // value: v_fc1 -> v_fc2 -> v
   static constexpr int NW = 8, RB = 1;
@@ -71,28 +133,43 @@ template <> struct HeadCfg<1> {   // value: v_fc1 -> v_fc2 -> v
   static constexpr int K2 = 16;
   static constexpr int N3 = 1;
   static constexpr int XS = 2;              // 1 k-step per 2 stages, 1 k-step ahead
-  static constexpr int S = 3;
+  static constexpr int S3 = 3, SBF = 6;     // (96 KiB)
   static constexpr int NS4 = 8;
+  static constexpr int NEED = 744;          // loss tile, partials, dW_v partials
 };
 
-template <int HEAD>
-constexpr int xr_floats() { return HeadCfg<HEAD>::XS * HeadCfg<HEAD>::RB * FB / 4; }
-template <int HEAD>
-constexpr int ws_floats() { return xr_floats<HEAD>() + HeadCfg<HEAD>::RB * TILE_F; }
-template <int HEAD>
+template <int DT, int HEAD>
+constexpr int head_stages() { return DT == DT_S3 ? HeadCfg<HEAD>::S3 : HeadCfg<HEAD>::SBF; }
+template <int DT>
+constexpr int stage_bytes() { return NSLOT * HT<DT>::FB; }
+// per-wave scratch: the X ring (fc1), reused after fc1 for the loss tile and the partials
+template <int DT, int HEAD>
+constexpr int xr_floats() {
+  constexpr int x = HeadCfg<HEAD>::XS * HeadCfg<HEAD>::RB * HT<DT>::FB / 4;
+  return x > HeadCfg<HEAD>::NEED ? x : HeadCfg<HEAD>::NEED;
+}
+template <int DT, int HEAD>
+constexpr int ws_floats() { return xr_floats<DT, HEAD>() + HeadCfg<HEAD>::RB * TILE_F; }
+template <int DT, int HEAD>
 constexpr size_t head_lds_bytes() {
-  return (size_t)HeadCfg<HEAD>::S * SB + (size_t)HeadCfg<HEAD>::NW * ws_floats<HEAD>() * sizeof(float);
+  return (size_t)head_stages<DT, HEAD>() * stage_bytes<DT>() +
+         (size_t)HeadCfg<HEAD>::NW * ws_floats<DT, HEAD>() * sizeof(float);
 }
 template <int HEAD>
 constexpr int wrows() { return 16 * HeadCfg<HEAD>::RB; }
-static_assert(head_lds_bytes<0>() <= 160 * 1024 && head_lds_bytes<1>() <= 160 * 1024, "LDS");
+template <int DT>
+constexpr bool head_lds_ok() {
+  return head_lds_bytes<DT, 0>() <= 160 * 1024 && head_lds_bytes<DT, 1>() <= 160 * 1024 &&
+         // value: loss tile + partials + its 128 dW_v partials; policy: + the [64][20] h2^T image
+         wrows<1>() * SST + NPF + 32 + 128 <= xr_floats<DT, 1>() &&
+         ((wrows<0>() * SST + NPF + 32 + 3) & ~3) + 64 * 20 <= xr_floats<DT, 0>() &&
+         // the dW_mu tiles of 4 waves go through the policy ring
+         4 * 32 * 128 * 4 <= head_stages<DT, 0>() * stage_bytes<DT>();
+}
+static_assert(head_lds_ok<DT_S3>() && head_lds_ok<DT_BF16>(), "head kernel LDS carving");
 static_assert(HeadCfg<0>::NW * wrows<0>() == ROWS && HeadCfg<1>::NW * wrows<1>() == ROWS, "128 rows per workgroup");
 // loss scratch (after fc1, in the X ring): dL/dmu | dL/dv [rows][SST], then the wave's partials
 static_assert(wrows<0>() * 32 <= HeadCfg<0>::RB * TILE_F, "mu tile fits the transpose tiles");
-// value: + its 128 dW_v partials; policy: + the [64][36] h2^T half image of the fused dW_mu
-static_assert(wrows<1>() * SST + NPF + 32 + 128 <= xr_floats<1>(), "value partials fit the X ring");
-static_assert(((wrows<0>() * SST + NPF + 32 + 3) & ~3) + 64 * 20 <= xr_floats<0>(), "h2^T image fits the X ring");
-static_assert(4 * 32 * 128 * 4 <= HeadCfg<0>::S * SB, "dW_mu tiles of 4 waves fit the ring");
 static_assert(HeadCfg<0>::NW == 8 && HeadCfg<0>::RB == 1, "the fused dW_mu reduction assumes 8 waves of 16 rows");
 
 template <int HEAD>
@@ -104,12 +181,13 @@ DEV int rot_ks(int ks, int rot, int ks1) {
 }
 
 // Ring slot q of stream step st: element offset of a weight fragment, or -1 (a slot no MFMA
-// reads; its DMA re-loads slot 0's fragment so every wave issues GL DMAs per step)
-template <int HEAD>
+// reads; its DMA re-loads slot 0's fragment so every wave issues GL DMAs per step).  FWD (the
+// value forward): the stream ends with the fc3 stage.
+template <int HEAD, bool FWD>
 DEV int step_src(const MlpArgs& a, int st, int q, int rot, int ks1) {
   using C = HeadCfg<HEAD>;
   const int ns1 = fc1_stages<HEAD>(ks1), ns2 = C::K2 / 2;
-  const int s_fc3 = ns1 + ns2, s_dg2 = s_fc3 + 1, s_end = s_dg2 + C::NS4;
+  const int s_fc3 = ns1 + ns2, s_dg2 = s_fc3 + 1, s_end = FWD ? s_dg2 : s_dg2 + C::NS4;
   if (st >= s_end) st = s_end - 1;
   if (st < ns1) {
     int ks, t;
@@ -141,22 +219,6 @@ DEV int step_src(const MlpArgs& a, int st, int q, int rot, int ks1) {
   return a.off_wt[C::L2] + (int)fm_frag(t, ks, a.d_out[C::L2], 0);
 }
 
-// dense LDS image of a DMA'd fragment (mlp_stream.hip frag_lane_off<true>): lane l reads hi at
-// (l / 32) KiB + 16 (l % 32), lo 512 bytes on
-DEV int lane_off(int lane) { return (lane >> 5) * 1024 + (lane & 31) * 16; }
-
-typedef __attribute__((ext_vector_type(8))) float f32x8;
-
-DEV Frag split8(const f32x8& x) {
-  const bf16x8 h = __builtin_convertvector(x, bf16x8);
-  const bf16x8 l = __builtin_convertvector(x - __builtin_convertvector(h, f32x8), bf16x8);
-  return Frag{h, l};
-}
-
-DEV f32x8 join8(const Frag& f) {
-  return __builtin_convertvector(f.h, f32x8) + __builtin_convertvector(f.l, f32x8);
-}
-
 // C-layout tiles of features c0..c0+15 (v0) and c0+16..c0+31 (v1) -> [16][SST] fp32
 DEV void tp_put(float* tp, const f32x4& v0, const f32x4& v1, int lane) {
   const int lr = lane & 15, lg = lane >> 4;
@@ -167,9 +229,10 @@ DEV void tp_put(float* tp, const f32x4& v0, const f32x4& v1, int lane) {
   }
 }
 
-// A operand (row lane & 15, k = 8 (lane >> 4) .. +7) of a [16][SST] tile, split; reads + wait in
-// one asm statement (a plain LDS load would wait vmcnt(0) for the ring's LDS-DMA)
-DEV Frag tp_getA(const float* tp, int lane) {
+// A operand (row lane & 15, k = 8 (lane >> 4) .. +7) of a [16][SST] tile; reads + wait in one asm
+// statement (a plain LDS load would wait vmcnt(0) for the ring's LDS-DMA)
+template <int DT>
+DEV typename HT<DT>::Frag tp_getA(const float* tp, int lane) {
   const float* r = tp + (lane & 15) * SST + 8 * (lane >> 4);
   const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)r;
   float4 x0, x1;
@@ -177,7 +240,7 @@ DEV Frag tp_getA(const float* tp, int lane) {
                : "=&v"(x0), "=&v"(x1)
                : "v"(addr)
                : "memory");
-  return split8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
+  return HT<DT>::from8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
 }
 
 DEV f32x4 bias_col(const f32x4& v, int c, int nb) {
@@ -186,24 +249,18 @@ DEV f32x4 bias_col(const f32x4& v, int c, int nb) {
 }
 
 // 4 consecutive m of feature 16 t + (lane & 15) -> the FM wgrad operand from the lane's base
-DEV void store_Tt(__bf16* lane_base, int t, size_t tsb, const f32x4& v) {
-  const bf16x4v hv = __builtin_convertvector(v, bf16x4v);
-  const bf16x4v lv = __builtin_convertvector(v - __builtin_convertvector(hv, f32x4), bf16x4v);
-  char* p = reinterpret_cast<char*>(lane_base) + (size_t)t * tsb;
-  opnd_store(*reinterpret_cast<const u32x2*>(&hv), reinterpret_cast<u32x2*>(p));
-  opnd_store(*reinterpret_cast<const u32x2*>(&lv), reinterpret_cast<u32x2*>(p + 16));
+template <int DT>
+DEV void store_Tt(char* lane_base, int t, size_t tsb, const f32x4& v) {
+  HT<DT>::store4(lane_base + (size_t)t * tsb, v);
 }
 
 // 8 consecutive m (rows 8h..8h+7) of column col of a [rows][ld] fp32 tile -> one FM group
+template <int DT>
 DEV void store_T8(void* outT, const float* tile, int ld, int col, int h, int feat, int m, int ldT) {
   f32x8 x;
 #pragma unroll
   for (int j = 0; j < 8; ++j) x[j] = tile[(8 * h + j) * ld + col];
-  const Frag s = split8(x);
-  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-  u32x4* o = reinterpret_cast<u32x4*>(P::hi_ptr(reinterpret_cast<T*>(outT), fm_index(feat, m, ldT)));
-  opnd_store(*reinterpret_cast<const u32x4*>(&s.h), o);
-  opnd_store(*reinterpret_cast<const u32x4*>(&s.l), o + 1);
+  HT<DT>::store8(HT<DT>::eptr(outT, fm_index(feat, m, ldT)), x);
 }
 
 // s_waitcnt vmcnt(BASE + extra) with a compile-time immediate (mlp_stream.hip wait_vm):
@@ -228,18 +285,18 @@ DEV void static_for(F&& f) {
 
 // Fragments q in [Q0, Q1) of a stage with bit q of MASK set, read in groups of G: group g + 1's
 // LDS reads are in flight while group g's MFMAs run.  f(integral_constant<q>, fragment).
-template <unsigned MASK, int Q0, int Q1, int G, typename F>
+template <int DT, unsigned MASK, int Q0, int Q1, int G, typename F>
 DEV void for_slots(const char* stg, int lane, F&& f) {
+  using H = HT<DT>;
   constexpr int NG = (Q1 - Q0 + G - 1) / G;
-  Frag b[2][G];
-  const char* base = stg + lane_off(lane);
+  typename H::Frag b[2][G];
+  const char* base = stg + H::lane_off(lane);
   auto rd = [&](auto gc) __attribute__((always_inline)) {
     constexpr int g = decltype(gc)::value;
     static_for<0, G>([&](auto ic) __attribute__((always_inline)) {
       constexpr int q = Q0 + g * G + decltype(ic)::value;
       if constexpr (q < Q1 && ((MASK >> q) & 1u))
-        b[g & 1][decltype(ic)::value] = Frag{*reinterpret_cast<const bf16x8*>(base + q * FB),
-                                             *reinterpret_cast<const bf16x8*>(base + q * FB + 512)};
+        b[g & 1][decltype(ic)::value] = H::lds(base + q * H::FB);
     });
   };
   rd(std::integral_constant<int, 0>{});
@@ -261,16 +318,15 @@ DEV void for_slots(const char* stg, int lane, F&& f) {
 // NM times, so the VALU issues in the MFMAs' shadow instead of after them (at one wave per SIMD
 // an in-order wave otherwise runs the MFMA block and the VALU block back to back).  v() must not
 // contain inline asm (a scheduling boundary).
-template <unsigned MASK, int Q0, int Q1, int NM, int VPM, typename F, typename V>
+template <int DT, unsigned MASK, int Q0, int Q1, int NM, int VPM, typename F, typename V>
 DEV void mma_mix(const char* stg, int lane, F&& f, V&& v) {
+  using H = HT<DT>;
   constexpr int N = Q1 - Q0;
-  Frag b[N];
-  const char* base = stg + lane_off(lane);
+  typename H::Frag b[N];
+  const char* base = stg + H::lane_off(lane);
   static_for<0, N>([&](auto ic) __attribute__((always_inline)) {
     constexpr int q = Q0 + decltype(ic)::value;
-    if constexpr ((MASK >> q) & 1u)
-      b[decltype(ic)::value] = Frag{*reinterpret_cast<const bf16x8*>(base + q * FB),
-                                    *reinterpret_cast<const bf16x8*>(base + q * FB + 512)};
+    if constexpr ((MASK >> q) & 1u) b[decltype(ic)::value] = H::lds(base + q * H::FB);
   });
   __builtin_amdgcn_sched_barrier(0);
   static_for<0, N>([&](auto ic) __attribute__((always_inline)) {
@@ -303,15 +359,25 @@ DEV float xsum(float x) {   // sum over the lanes that differ only in the bits o
           __builtin_amdgcn_s_memtime();                                                           \
   } while (0)
 
-template <int HEAD>
+// FWD (value head only): the forward alone, V(x) of rows [row0, row0 + M) into v_out — the GAE
+// input pass (train.py:87,109-112) at the update kernel's 128 rows per weight stream instead of
+// mlp.hip's 32-row value kernel
+template <int DT, int HEAD, bool FWD = false>
 __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
+  static_assert(!FWD || HEAD == 1, "forward mode is the value head's");
   using C = HeadCfg<HEAD>;
-  constexpr int S = C::S, XS = C::XS;
+  using H = HT<DT>;
+  using P = typename H::P;
+  using T = typename P::T;
+  using Frag = typename H::Frag;
+  constexpr int FB = H::FB, SB = stage_bytes<DT>();
+  constexpr int S = head_stages<DT, HEAD>(), XS = C::XS;
   constexpr int NW = C::NW, RB = C::RB, WROWS = 16 * RB;
-  constexpr int SPW = NSLOT / NW, GL = 2 * SPW;   // ring slots / DMA instructions per wave per stage
-  constexpr int XDMA = 2 * RB;                    // DMA instructions of one wave's X fragments of a k-step
-  constexpr int TPR = 64 / WROWS;                 // loss lanes per row
-  constexpr int WS_F = ws_floats<HEAD>();
+  constexpr int SPW = NSLOT / NW, GL = H::NI * SPW;   // ring slots / DMA instructions per wave per stage
+  constexpr int XDMA = H::NI * RB;                    // DMA instructions of one wave's X fragments of a k-step
+  constexpr int TPR = 64 / WROWS;                     // loss lanes per row
+  constexpr int WS_F = ws_floats<DT, HEAD>();
+  constexpr int MPP = DT == DT_S3 ? 3 : 1;            // MFMAs per fragment product
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -323,7 +389,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   char* ring = smem;
   float* scr = reinterpret_cast<float*>(smem + (size_t)S * SB) + wave * WS_F;
   char* xring = reinterpret_cast<char*>(scr);
-  float* tpb = scr + xr_floats<HEAD>();   // RB transpose tiles [16][SST]
+  float* tpb = scr + xr_floats<DT, HEAD>();   // RB transpose tiles [16][SST]
   float* dml = scr;                        // (after fc1) dL/dmu [32][SST] | dL/dv column 32
   float* wpart = scr + WROWS * SST;        // (after fc1) [8 loss terms | 32 dlog_std]
   float* mus = tpb;                        // (loss) mu [32][32] | v [32]
@@ -356,7 +422,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     }
     l_adv = a.adv[lsrc];
     l_lpo = !ref_loss ? a.logp_old[lsrc] : 0.f;
-  } else {
+  } else if constexpr (!FWD) {
     l_ret = a.ret[lsrc];
     l_vold = !ref_loss ? a.v_old[lsrc] : 0.f;
     l_vprev = ref_loss ? a.v_prev[lsrc] : 0.f;
@@ -364,30 +430,26 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 
   // ---- DMA sources ----
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), (short)0, 0x7fffffff, 0x00020000);
-  const unsigned vw = (unsigned)((lane & 31) * 32 + (lane >> 5) * 16);
+  const unsigned vw = H::wsrc(lane);
   // observation rows: 64-bit per-lane addresses (global_load_lds), so a buffer of any size works;
-  // instruction h of a row block moves k-groups 2h, 2h+1 (64 contiguous bytes of each row)
+  // instruction h of a row block moves 64 contiguous bytes of each row (split-bf16: k-groups 2h,
+  // 2h+1; bf16: the whole k-step)
   const char* xsrc[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
     xsrc[rb] = reinterpret_cast<const char*>(a.x_buf) +
-               (size_t)src_of(WROWS * wave + 16 * rb + lr) * (size_t)a.d_in[0] * sizeof(T) + 32 * ((lane >> 4) & 1) +
-               16 * (lane >> 5);
+               (size_t)src_of(WROWS * wave + 16 * rb + lr) * (size_t)a.d_in[0] * sizeof(T) + H::xlane(lane);
   const int rot = (int)(blockIdx.x % (unsigned)ks1);
   auto code16 = [&](int st, int q) __attribute__((always_inline)) {
-    int c = step_src<HEAD>(a, st, q, rot, ks1);
-    if (c < 0) c = step_src<HEAD>(a, st, 0, rot, ks1);
+    int c = step_src<HEAD, FWD>(a, st, q, rot, ks1);
+    if (c < 0) c = step_src<HEAD, FWD>(a, st, 0, rot, ks1);
     if (c < 0) c = a.off_w[C::L1];
     return (uint32_t)(c >> 9);
   };
   const uint32_t cw0 = code16(lane, SPW * wave) | (code16(lane, SPW * wave + 1) << 16);
   const uint32_t cw1 = SPW > 2 ? code16(lane, SPW * wave + 2) | (code16(lane, SPW * wave + 3) << 16) : 0u;
 
-  // diagnostics only (scripts/head_timeline.py ablations; 0 in every real run): bit 1 no weight
-  // DMA, bit 3 no observation DMA, bit 5 no fc1 MFMAs
-  const int abl = a.ablate;
   auto issue = [&](int st, int stage) __attribute__((always_inline)) {
-    if (abl & 2) return;
     const int l = min(st, MAX_STEPS - 1);
     const uint32_t w01 = __builtin_amdgcn_readlane(cw0, l);
     const uint32_t w23 = SPW > 2 ? __builtin_amdgcn_readlane(cw1, l) : 0u;
@@ -396,30 +458,35 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
     for (int u = 0; u < SPW; ++u) {
       const uint32_t code = ((u < 2 ? w01 : w23) >> (16 * (u & 1))) & 0xffffu;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB, 16, vw, code * 2048u, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB + 1024, 16, vw, code * 2048u + 1024u, 0, 0);
+#pragma unroll
+      for (int h = 0; h < H::NI; ++h)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB + 1024 * h, 16, vw, code * (unsigned)FB + 1024u * h, 0, 0);
     }
   };
   // this wave's RB observation fragments of fc1 k-step ks into X ring slot ks % XS
   auto issue_x = [&](int ks) __attribute__((always_inline)) {
-    if (abl & 8) return;
-    const size_t xo = (size_t)rot_ks(min(ks, ks1 - 1), rot, ks1) * 128u;
+    const size_t xo = (size_t)rot_ks(min(ks, ks1 - 1), rot, ks1) * (32u * sizeof(T));
     char* d = xring + (ks & (XS - 1)) * (RB * FB);
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      glds16(xsrc[rb] + xo, d + rb * FB);
-      glds16(xsrc[rb] + xo + 64, d + rb * FB + 1024);
-    }
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int h = 0; h < H::NI; ++h) glds16(xsrc[rb] + xo + 64 * h, d + rb * FB + 1024 * h);
   };
   auto read_x = [&](int ks, int rb) __attribute__((always_inline)) {
     const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(
-                              xring + (ks & (XS - 1)) * (RB * FB) + rb * FB) + lane_off(lane);
-    bf16x8 h, l;
-    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:512\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&v"(h), "=&v"(l)
-                 : "v"(addr)
-                 : "memory");
-    return Frag{h, l};
+                              xring + (ks & (XS - 1)) * (RB * FB) + rb * FB) + H::lane_off(lane);
+    if constexpr (DT == DT_S3) {
+      bf16x8 h, l;
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:512\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(h), "=&v"(l)
+                   : "v"(addr)
+                   : "memory");
+      return Frag{h, l};
+    } else {
+      bf16x8 h;
+      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(h) : "v"(addr) : "memory");
+      return h;
+    }
   };
 
   // Ring bookkeeping.  Every step: wait for its stage (this wave's DMAs by count, every wave's by
@@ -460,9 +527,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
   for (int st = 0; st < S - 1; ++st) issue(st, st);
 
-  const size_t tsb = (size_t)a.ldT * 64;   // bytes of one 16-feature row block of an FM operand
+  const size_t tsb = (size_t)a.ldT * 16 * sizeof(T);   // bytes of one 16-feature row block of an FM operand
   auto lane_base = [&](void* buf, int rb) __attribute__((always_inline)) {
-    return P::hi_ptr(reinterpret_cast<T*>(buf), fm_index(lr, mw + 16 * rb + 4 * lg, a.ldT));
+    return H::eptr(buf, fm_index(lr, mw + 16 * rb + 4 * lg, a.ldT));
   };
   void* const h1T = HEAD == 0 ? a.h1pT : a.h1vT;
   void* const g2T = HEAD == 0 ? a.g2pT : a.g2vT;
@@ -480,11 +547,11 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   // block of k-step ks of row block rb, transposed through its tile)
   auto put_xT = [&](const Frag& x, int ks, int rb) __attribute__((always_inline)) {
     float* tp = tpb + rb * TILE_F;
-    const f32x8 v = join8(x);
+    const f32x8 v = H::to8(x);
     float4* w = reinterpret_cast<float4*>(tp + lr * SST + 8 * lg);
     w[0] = float4{v[0], v[1], v[2], v[3]};
     w[1] = float4{v[4], v[5], v[6], v[7]};
-    store_T8(a.xT, tp, SST, lane >> 1, lane & 1, 32 * rot_ks(ks, rot, ks1) + (lane >> 1),
+    store_T8<DT>(a.xT, tp, SST, lane >> 1, lane & 1, 32 * rot_ks(ks, rot, ks1) + (lane >> 1),
              mw + 16 * rb + 8 * (lane & 1), a.ldT);
   };
   if constexpr (HEAD == 1) {
@@ -497,8 +564,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb) xa[rb] = read_x(ks, rb);
         }
-        if (!(abl & 32))
-          for_slots<0xffffu, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+        for_slots<DT, 0xffffu, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
             constexpr int t = 16 * sub + decltype(qc)::value;
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) acc1[rb][t] = P::mma(acc1[rb][t], xa[rb], b);
@@ -519,7 +585,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         xa[rb] = read_x(ka, rb);
         xb[rb] = read_x(kb, rb);
       }
-      for_slots<0x7f7fu, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      for_slots<DT, 0x7f7fu, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
         constexpr int q = decltype(qc)::value;
         if constexpr (q < 8) {
 #pragma unroll
@@ -547,9 +613,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   HD_STAMP(1);
   // ---------------- fc2: h1 = tanh(fc1), one k-step's A operand prepared at a time ----------------
   const int n1 = a.n_out[C::L1], n2 = a.n_out[C::L2];
-  __bf16* bh1[RB];
-  __bf16* bg2[RB];
-  __bf16* bg1[RB];
+  char* bh1[RB];
+  char* bg2[RB];
+  char* bg1[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     bh1[rb] = lane_base(h1T, rb);
@@ -558,6 +624,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   }
   // A operand of fc2 k-step I (h1 features 32 I .. 32 I + 31) for both row blocks: tanh in place,
   // the h1^T stores, the transposes; returns the number of stores
+  constexpr int NSTA = FWD ? 0 : 2 * H::SPS * RB;   // h1^T store instructions of one prep_a
   auto prep_a = [&](auto Ic) __attribute__((always_inline)) {
     constexpr int I = decltype(Ic)::value;
     constexpr bool last = I == C::K2 - 1;
@@ -569,19 +636,21 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       acc1[rb][2 * I + 1] = h1;
       // (the last k-step holds the bias column (1) and zero padding: stored as such)
       const f32x4 s0 = last ? bias_col(h0, c0, n1) : h0, s1 = last ? bias_col(h1, c0 + 16, n1) : h1;
-      store_Tt(bh1[rb], 2 * I, tsb, s0);
-      store_Tt(bh1[rb], 2 * I + 1, tsb, s1);
+      if constexpr (!FWD) {
+        store_Tt<DT>(bh1[rb], 2 * I, tsb, s0);
+        store_Tt<DT>(bh1[rb], 2 * I + 1, tsb, s1);
+      }
       tp_put(tpb + rb * TILE_F, s0, s1, lane);
     }
   };
   auto prep_b = [&](Frag (&fa)[RB]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) fa[rb] = tp_getA(tpb + rb * TILE_F, lane);
+    for (int rb = 0; rb < RB; ++rb) fa[rb] = tp_getA<DT>(tpb + rb * TILE_F, lane);
   };
   auto prep = [&](auto Ic, Frag (&fa)[RB]) __attribute__((always_inline)) -> int {
     prep_a(Ic);
     prep_b(fa);
-    return 4 * RB;
+    return NSTA;
   };
   f32x4 acc2[RB][8];
 #pragma unroll
@@ -596,23 +665,23 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     stg = wait_step(nst);
     // k-step 2j's MFMAs with k-step 2j+1's operand preparation in their shadow, then k-step
     // 2j+1's with 2j+2's
-    mma_mix<0x7fu, 0, 8, 7 * RB * 3, 3>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    mma_mix<DT, 0x7fu, 0, 8, 7 * RB * MPP, 3>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int t = decltype(qc)::value;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a0[rb], b);
     }, [&]() __attribute__((always_inline)) { prep_a(std::integral_constant<int, 2 * j + 1>{}); });
     prep_b(a1);
-    nst = 4 * RB;
+    nst = NSTA;
     if constexpr (2 * j + 2 < C::K2) {
-      mma_mix<0x7f00u, 8, 16, 7 * RB * 3, 3>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      mma_mix<DT, 0x7f00u, 8, 16, 7 * RB * MPP, 3>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
         constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a1[rb], b);
       }, [&]() __attribute__((always_inline)) { prep_a(std::integral_constant<int, 2 * j + 2>{}); });
       prep_b(a0);
-      nst += 4 * RB;
+      nst += NSTA;
     } else {
-      for_slots<0x7f00u, 8, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      for_slots<DT, 0x7f00u, 8, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
         constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a1[rb], b);
@@ -643,15 +712,29 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       tp_put(tpb + rb * TILE_F, bias_col(acc2[rb][2 * ks], c0, n2), bias_col(acc2[rb][2 * ks + 1], c0 + 16, n2), lane);
-      am[rb] = tp_getA(tpb + rb * TILE_F, lane);
+      am[rb] = tp_getA<DT>(tpb + rb * TILE_F, lane);
     }
     constexpr unsigned M3 = C::N3 == 2 ? ((1u << ks) | (1u << (4 + ks))) : (1u << ks);
-    for_slots<M3, 0, 8, 8>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    for_slots<DT, M3, 0, 8, 8>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int t = decltype(qc)::value >> 2;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) a3[rb][t] = P::mma(a3[rb][t], am[rb], b);
     });
   });
+  if constexpr (FWD) {
+    // V of the wave's rows: column 0 of the fc3 tile (lanes lr == 0 hold rows 4 lg .. 4 lg + 3)
+    if (lr == 0) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = mw + 16 * rb + 4 * lg + i;
+          if (m < a.M) a.v_out[m] = a3[rb][0][i];
+        }
+    }
+    WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
+    return;
+  } else {
   // (the transpose tiles hold mu / v from here: every wave's own)
   float dls[JM], lt[6];
 #pragma unroll
@@ -762,7 +845,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       }
     }
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) ad[rb] = tp_getA(dml + 16 * rb * SST, lane);
+    for (int rb = 0; rb < RB; ++rb) ad[rb] = tp_getA<DT>(dml + 16 * rb * SST, lane);
   } else {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -818,7 +901,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       }
     }
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) ad[rb] = split8(f32x8{lg == 0 ? dvr[rb] : 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
+    for (int rb = 0; rb < RB; ++rb) ad[rb] = H::from8(f32x8{lg == 0 ? dvr[rb] : 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
     // the fused v-layer weight gradient over the wave's 32 rows: dW_v[k] = sum_r dL/dv[r] h2[r][k]
     // (h2 with the bias column 1: k = 100 is the bias gradient) -> the wave's 128 partials
     {
@@ -854,7 +937,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int t = 0; t < 8; ++t) d2[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for_slots<0x7f00u, 8, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+  for_slots<DT, 0x7f00u, 8, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
     constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) d2[rb][t] = P::mma(d2[rb][t], ad[rb], b);
@@ -866,17 +949,17 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       d2[rb][t] = c < n2 ? d2[rb][t] * (1.0f - acc2[rb][t] * acc2[rb][t]) : f32x4{0.f, 0.f, 0.f, 0.f};
-      store_Tt(bg2[rb], t, tsb, d2[rb][t]);
+      store_Tt<DT>(bg2[rb], t, tsb, d2[rb][t]);
     }
   }
-  nst += 16 * RB;
+  nst += 8 * H::SPS * RB;
   Frag a2[4][RB];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       tp_put(tpb + rb * TILE_F, d2[rb][2 * ks], d2[rb][2 * ks + 1], lane);
-      a2[ks][rb] = tp_getA(tpb + rb * TILE_F, lane);
+      a2[ks][rb] = tp_getA<DT>(tpb + rb * TILE_F, lane);
     }
   // (the loss's dY^T stores are not counted: an undercount, the next waits cover them)
 
@@ -892,9 +975,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
           const f32x4 h = acc1[rb][tt];
-          store_Tt(bg1[rb], tt, tsb, gq[decltype(uc)::value][rb] * (1.0f - h * h));
+          store_Tt<DT>(bg1[rb], tt, tsb, gq[decltype(uc)::value][rb] * (1.0f - h * h));
         }
-        n += 2 * RB;
+        n += H::SPS * RB;
       }
     });
     return n;
@@ -908,7 +991,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) g[u][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
     constexpr unsigned M4 = (4 * s + 3 < C::N1R) ? 0xffffu : ((1u << (4 * ((C::N1R - 4 * s) & 3))) - 1u);
-    for_slots<M4, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    for_slots<DT, M4, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) g[q >> 2][rb] = P::mma(g[q >> 2][rb], a2[q & 3][rb], b);
@@ -940,7 +1023,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       f32x8 x;
 #pragma unroll
       for (int e = 0; e < 8; ++e) x[e] = lg < 2 ? dml[(8 * lg + e) * SST + 16 * m + lr] : 0.f;
-      am2[m] = split8(x);
+      am2[m] = H::from8(x);
     }
     constexpr int HLD = 20;                                    // [64 features][HLD] (16 rows + pad)
     float* h2t = dml + ((WROWS * SST + NPF + 32 + 3) & ~3);    // after the loss tile + partials
@@ -961,7 +1044,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         const float* r = h2t + (16 * tt + lr) * HLD + 8 * (lg & 1);
         float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
         if (lg >= 2) x0 = x1 = float4{0.f, 0.f, 0.f, 0.f};
-        const Frag bh = split8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
+        const Frag bh = H::from8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
 #pragma unroll
         for (int m = 0; m < 2; ++m) dwm[m][4 * hh + tt] = P::mma(dwm[m][4 * hh + tt], am2[m], bh);
       }
@@ -1018,14 +1101,15 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     a.part[(size_t)blockIdx.x * a.npart + q] = s;
   }
   HD_STAMP(7);
+  }   // !FWD
 }
 
-template <int HEAD>
+template <int DT, int HEAD, bool FWD = false>
 void head_launch(const MlpArgs& a, hipStream_t s) {
-  const size_t lds = head_lds_bytes<HEAD>();
-  set_max_lds_once<mlp_head_kernel<HEAD>>(lds);
+  const size_t lds = head_lds_bytes<DT, HEAD>();
+  set_max_lds_once<mlp_head_kernel<DT, HEAD, FWD>>(lds);
   const int nblk = (a.M + ROWS - 1) / ROWS;
-  hipLaunchKernelGGL((mlp_head_kernel<HEAD>), dim3(nblk), dim3(HeadCfg<HEAD>::NW * 64), lds, s, a);
+  hipLaunchKernelGGL((mlp_head_kernel<DT, HEAD, FWD>), dim3(nblk), dim3(HeadCfg<HEAD>::NW * 64), lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
@@ -1046,9 +1130,20 @@ extern "C" int mlp_head_applies(const MlpArgs& a) {
 extern "C" int mlp_head_rows() { return ROWS; }
 extern "C" int mlp_head_waves(int head) { return head == 0 ? HeadCfg<0>::NW : HeadCfg<1>::NW; }
 
-extern "C" void launch_mlp_head(int head, const MlpArgs& a, hipStream_t s) {
-  if (head == 0) head_launch<0>(a, s);
-  else head_launch<1>(a, s);
+extern "C" void launch_mlp_head(int dt, int head, const MlpArgs& a, hipStream_t s) {
+  if (dt == DT_S3) {
+    if (head == 0) head_launch<DT_S3, 0>(a, s);
+    else head_launch<DT_S3, 1>(a, s);
+  } else {
+    if (head == 0) head_launch<DT_BF16, 0>(a, s);
+    else head_launch<DT_BF16, 1>(a, s);
+  }
+}
+
+// the value forward (GAE input) on the value head's streaming kernel (split-bf16)
+extern "C" void launch_mlp_head_value(int dt, const MlpArgs& a, hipStream_t s) {
+  if (dt == DT_S3) head_launch<DT_S3, 1, true>(a, s);
+  else head_launch<DT_BF16, 1, true>(a, s);
 }
 
 extern "C" void set_head_kernels(int enable) { g_head_enable = enable ? 1 : 0; }

@@ -17,107 +17,32 @@
 namespace {
 
 constexpr int WG_WAVES = 8;
+constexpr int WG_SLOTS = 24;   // fragment slots per stage: (nq + kq) * 4 <= 24 (nq + kq <= 6)
 
-// register-streamed variant (A/B diagnostics; the LDS-DMA kernel below is the default): each
-// active wave loads its own 4 + 4 fragments per k-step straight into registers
-template <int DT>
-__global__ __launch_bounds__(WG_WAVES * 64) void wgrad_reg_kernel(WgradArgs a) {
-  using P = Prec<DT>;
-  using T = typename P::T;
-  using Frag = typename P::Frag;
-  const WgradTask tk = a.tasks[blockIdx.x];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (wave >= tk.nq * tk.kq) return;          // no barriers in this kernel
-  const int wn = wave / tk.kq, wk = wave - wn * tk.kq;
-  const T* g = reinterpret_cast<const T*>(a.gT[tk.layer]);
-  const T* x = reinterpret_cast<const T*>(a.xT[tk.layer]);
-  // operands are fragment-major (FM): the fragment of (row tile, k-step) is 512 contiguous
-  // elements, so each of the 8 loads per k-step is one contiguous 1 KiB wave read
-  const size_t blk_row = (size_t)(a.ld >> 5) * 512;  // elements per 16-row block-row
-  const T* gp = g + fm_frag((tk.n0 + wn * 64) >> 4, tk.m0 >> 5, a.ld, lane);
-  const T* xp = x + fm_frag((tk.k0 + wk * 64) >> 4, tk.m0 >> 5, a.ld, lane);
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // Two register slots in ping-pong, the loop unrolled by two so each slot keeps fixed
-  // registers (no copies).  Every prefetch is unconditional (clamped to the last step; its
-  // data unused) and every MFMA in the loop is unconditional, so the number of loads in flight
-  // is path-independent and the compiler's waits stay partial.
-  const int nk = (tk.m1 - tk.m0) >> 5;
-  struct Slot { Frag a[4], b[4]; };
-  auto fetch = [&](Slot& d, int k) {
-    const size_t ko = (size_t)min(k, nk - 1) * 512;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      d.a[i] = P::load(gp + i * blk_row + ko);
-      d.b[i] = P::load(xp + i * blk_row + ko);
-    }
-  };
-  auto mma = [&](const Slot& c) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(acc[i][j], c.a[i], c.b[j]);
-  };
-  // the host plan makes every chunk a multiple of 64 rows (two steps; checked in bindings.cpp)
-  Slot r0, r1;
-  fetch(r0, 0);
-  for (int k = 0; k < nk; k += 2) {
-    fetch(r1, k + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(r0);
-    __builtin_amdgcn_sched_barrier(0);
-    fetch(r0, k + 2);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(r1);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  const int KE = tk.kq * 64;
-  float* out = a.slab + tk.slab;
-  const int col = wk * 64 + (lane & 15);
-  const int rbase = wn * 64 + (lane >> 4) * 4;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * KE + col + 16 * j] = acc[i][j][q];
-}
-
-// ---- LDS-DMA staged variant (default) ----------------------------------------------------
-// The workgroup stages each k-step's distinct fragments (4*nq of dY^T, 4*kq of X^T; 1 KiB
-// each at bf16) ONCE into LDS with global_load_lds_dwordx4: an FM fragment is 64 lanes x 16 B
-// in lane order, exactly the lane-linear image the DMA writes, so each fragment is one DMA
-// instruction and the fragment reads are conflict-free ds_read_b128 at lane*16.  Each wave
-// DMAs C fixed slots per stage (C = 2 when the task has <= 16 fragments, else 3; slots past
-// the task's fragment count re-load one of its fragments, an L2 hit, so every wave's DMA count
-// — and with it the vmcnt arithmetic — is task-independent).  S-deep ring, counted vmcnt and a
-// raw s_barrier keep S-1 steps of DMA in flight across the barrier (cdna_hip_programming.md
+// The workgroup stages each k-step's distinct fragments (4*nq of dY^T, 4*kq of X^T) ONCE into
+// LDS with LDS-DMA (global_load_lds_dwordx4): an FM fragment is 64 lanes x 16 B per KiB in lane
+// order, exactly the lane-linear image the DMA writes, so the fragment reads are conflict-free
+// ds_read_b128 at lane*16.  A split-bf16 fragment (32 B per lane: hi | lo) is two DMA
+// instructions, instruction h moving the fragment's h-th KiB (lanes 32h .. 32h+31) so it lands
+// as [their hi][their lo] (the dense layout of mlp_stream.hip frag_lane_off).  Each wave DMAs C
+// fixed slots per stage (C = 2 when the task has <= 16 fragments, else 3; slots past the task's
+// fragment count re-load one of its fragments, an L2 hit, so every wave's DMA count — and with
+// it the vmcnt arithmetic — is task-independent).  S-deep ring, counted vmcnt and a raw
+// s_barrier keep S-1 steps of DMA in flight across the barrier (cdna_hip_programming.md
 // 'Pipelining across barriers'): no VGPRs hold in-flight data.
-// fragment slots per stage: (nq + kq) * 4 <= 24 at 8 waves (nq + kq <= 6), <= 32 at 16 waves
-// (nq + kq <= 8: e.g. 4x4 tiles, 256x256 outputs per workgroup)
-template <int W> struct WgSlots { static constexpr int N = W == 16 ? 32 : 24; };
-
 template <int DT>
 constexpr int wgrad_frag_bytes() { return 512 * Prec<DT>::BYTES; }
-template <int DT, int S, int W = 8>
-constexpr size_t wgrad_lds_bytes() { return (size_t)S * WgSlots<W>::N * wgrad_frag_bytes<DT>(); }
-// ring depth of the bf16 kernel (A/B knob set_wgrad_stages): 3 (72 KiB, two workgroups per
-// CU), 4 (96 KiB) or 6 (144 KiB; five steps = 120 KiB of DMA in flight per CU)
-int g_wgrad_stages = 4;
+template <int DT, int S>
+constexpr size_t wgrad_lds_bytes() { return (size_t)S * WG_SLOTS * wgrad_frag_bytes<DT>(); }
 
-
-template <int DT, int S, int C, int W, bool HS>
+template <int DT, int S, int C>
 DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   using P = Prec<DT>;
   using T = typename P::T;
   using Frag = typename P::Frag;
   constexpr int FB = wgrad_frag_bytes<DT>();     // bytes per fragment
   constexpr int NI = FB / 1024;                  // DMA instructions per fragment (64 lanes x 16 B)
-  constexpr int SB = WgSlots<W>::N * FB;         // bytes per stage
+  constexpr int SB = WG_SLOTS * FB;              // bytes per stage
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const char* g = reinterpret_cast<const char*>(a.gT[tk.layer]);
@@ -144,13 +69,8 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
     for (int q = 0; q < C; ++q)
 #pragma unroll
       for (int h = 0; h < NI; ++h) {
-        // split-bf16 fragments (32 B per lane: hi | lo) are de-interleaved by the DMA itself.
-        // HS (dense): instruction h moves the fragment's h-th KiB (lanes 32h .. 32h+31), landing
-        // as [their hi][their lo]; otherwise instruction h moves every lane's h-th 16 bytes (LDS:
-        // the hi block, then the lo block).  Both are read conflict-free.
-        const size_t go = IsSplit<DT>::value
-                              ? (HS ? (size_t)h * 1024 + (lane & 31) * 32 + (lane >> 5) * 16 : (size_t)lane * 32 + h * 16)
-                              : (size_t)h * 1024 + lane * 16;
+        const size_t go = IsSplit<DT>::value ? (size_t)h * 1024 + (lane & 31) * 32 + (lane >> 5) * 16
+                                             : (size_t)h * 1024 + lane * 16;
         glds16(src[q] + (size_t)kk * FB + go, st + dst[q] + h * 1024);
       }
   };
@@ -172,8 +92,8 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
       Frag af[4], bf[4];
       auto lds_frag = [&](int f) {
         if constexpr (IsSplit<DT>::value) {
-          const char* b = st + f * FB + (HS ? (lane >> 5) * 1024 + (lane & 31) * 16 : lane * 16);
-          return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + (HS ? 512 : 1024))};
+          const char* b = st + f * FB + (lane >> 5) * 1024 + (lane & 31) * 16;
+          return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + 512)};
         } else {
           return P::load(reinterpret_cast<const T*>(st + f * FB) + lane * 8);
         }
@@ -203,34 +123,20 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
       for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * KE + col + 16 * j] = acc[i][j][q];
 }
 
-template <int DT, int S, int W, bool HS>
-__global__ __launch_bounds__(W * 64) void wgrad_kernel(WgradArgs a) {
+template <int DT, int S>
+__global__ __launch_bounds__(WG_WAVES * 64) void wgrad_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const WgradTask tk = a.tasks[blockIdx.x];
-  if constexpr (W == 16) {
-    wgrad_lds_body<DT, S, 2, W, HS>(a, tk, smem);    // 32 slots = 2 per wave
-  } else {
-    if (4 * (tk.nq + tk.kq) <= 2 * W) wgrad_lds_body<DT, S, 2, W, HS>(a, tk, smem);
-    else wgrad_lds_body<DT, S, 3, W, HS>(a, tk, smem);
-  }
+  if (4 * (tk.nq + tk.kq) <= 2 * WG_WAVES) wgrad_lds_body<DT, S, 2>(a, tk, smem);
+  else wgrad_lds_body<DT, S, 3>(a, tk, smem);
 }
 
-template <int DT, int S, int W, bool HS>
-void launch_wgrad_lds_t(const WgradArgs& a, hipStream_t s) {
-  const size_t lds = wgrad_lds_bytes<DT, S, W>();
-  set_max_lds_once<wgrad_kernel<DT, S, W, HS>>(lds);
-  hipLaunchKernelGGL((wgrad_kernel<DT, S, W, HS>), dim3(a.ntasks), dim3(W * 64), lds, s, a);
-}
-
-template <int DT, int S, int W = 8>
+// ring depth: fp32 and split-bf16 3 stages (144 KiB), bf16 4 (96 KiB)
+template <int DT, int S>
 void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
-  if constexpr (IsSplit<DT>::value) {
-    if (a.dense) {
-      launch_wgrad_lds_t<DT, S, W, true>(a, s);
-      return;
-    }
-  }
-  launch_wgrad_lds_t<DT, S, W, false>(a, s);
+  const size_t lds = wgrad_lds_bytes<DT, S>();
+  set_max_lds_once<wgrad_kernel<DT, S>>(lds);
+  hipLaunchKernelGGL((wgrad_kernel<DT, S>), dim3(a.ntasks), dim3(WG_WAVES * 64), lds, s, a);
 }
 
 // Blocks [0, ceil(nitems / 64)): the reduce items (log_std, loss-term sums, the per-head
@@ -273,28 +179,11 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
 
 }  // namespace
 
-extern "C" void set_wgrad_stages(int st) { g_wgrad_stages = (st == 3 || st == 6) ? st : 4; }
-
 extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
   if (a.ntasks <= 0) return;
-  const dim3 block(WG_WAVES * 64);
-  if (a.impl == 1) {   // (bindings.cpp rejects the split-bf16 operands here)
-    if (dt == DT_F32) hipLaunchKernelGGL(wgrad_reg_kernel<DT_F32>, dim3(a.ntasks), block, 0, s, a);
-    else hipLaunchKernelGGL(wgrad_reg_kernel<DT_BF16>, dim3(a.ntasks), block, 0, s, a);
-  } else if (dt == DT_F32) {
-    launch_wgrad_lds<DT_F32, 3>(a, s);
-  } else if (dt == DT_S3) {
-    if (a.waves == 16) launch_wgrad_lds<DT_S3, 2, 16>(a, s);   // 2 x 32 slots x 2 KiB = 128 KiB
-    else launch_wgrad_lds<DT_S3, 3>(a, s);
-  } else if (a.waves == 16) {
-    launch_wgrad_lds<DT_BF16, 4, 16>(a, s);
-  } else if (g_wgrad_stages == 3) {
-    launch_wgrad_lds<DT_BF16, 3>(a, s);
-  } else if (g_wgrad_stages == 6) {
-    launch_wgrad_lds<DT_BF16, 6>(a, s);
-  } else {
-    launch_wgrad_lds<DT_BF16, 4>(a, s);
-  }
+  if (dt == DT_F32) launch_wgrad_lds<DT_F32, 3>(a, s);
+  else if (dt == DT_S3) launch_wgrad_lds<DT_S3, 3>(a, s);
+  else launch_wgrad_lds<DT_BF16, 4>(a, s);
   HIP_CHECK_LAUNCH();
 }
 

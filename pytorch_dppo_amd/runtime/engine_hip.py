@@ -37,19 +37,18 @@ NPART_FIXED = 8
 WT = 128            # operand-buffer row padding (csrc/kernels.h WGRAD_TILE)
 
 
-def wgrad_tiles(li: int, n: int, k: int, waves: int = 8):
+def wgrad_tiles(li: int, n: int, k: int):
     """Output tiles of one layer's weight gradient ([n][k], k including the bias column) for the
     wgrad kernel: (layer, n0, k0, nq, kq), a tile = nq x kq quadrants of 64x64, one per wave of
-    the workgroup (8 waves: nq*kq <= 8, nq + kq <= 6; 16 waves: nq*kq <= 16, nq + kq <= 8).  The kernel streams (nq + kq) * 64 operand
+    the 8-wave workgroup (nq*kq <= 8, nq + kq <= 6).  The kernel streams (nq + kq) * 64 operand
     rows per 32-row k-step, so the (nq, kq) minimising the layer's total rows read wins (ties:
     fewer tasks, then wider n).  Humanoid v_fc1 (512 x 377): 4x2 tiles, 2304 rows per step
     instead of 3072 with 128x128 tiles."""
     N, K = -(-n // 64), -(-k // 64)
     best = None
-    smax = 8 if waves == 16 else 6
-    for nq in range(1, 17):
-        for kq in range(1, 17):
-            if nq * kq > waves or nq + kq > smax or nq > N or kq > K:
+    for nq in range(1, 9):
+        for kq in range(1, 9):
+            if nq * kq > 8 or nq + kq > 6 or nq > N or kq > K:
                 continue
             tl = []
             for a in range(0, N, nq):
@@ -62,7 +61,6 @@ def wgrad_tiles(li: int, n: int, k: int, waves: int = 8):
     return best[1]
 ROLL_ROWS = 16
 WGRAD_TARGET_WGS = 0     # wgrad tasks per launch; 0: one per CU of the device (256 on MI355X)
-WGRAD_ALIGNED = False    # one batch-row grid for all tiles (A/B: HipEngine.wgrad_aligned)
 
 
 def _r(x: int, m: int) -> int:
@@ -191,12 +189,6 @@ class HipEngine:
         for buf, r in ((self.h1pT, lp1.fan_out), (self.h2pT, lp2.fan_out), (self.h1vT, lv1.fan_out),
                        (self.h2vT, lv2.fan_out)):
             storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), 1.0, self.dt)
-        # wgrad workgroup waves: 8 (A/B: 16-wave workgroups with up to 16-quadrant tiles stream
-        # fewer operand rows — 1,792 vs 2,304 per step for v_fc1 — but took 243 vs 226 us per
-        # grad call; bf16 only, env DPPO_WGRAD_WAVES=16)
-        self.wgrad_waves = int(os.environ.get("DPPO_WGRAD_WAVES", 8))
-        if self.dt not in (1, 3):
-            self.wgrad_waves = 8
         self._build_wgrad_plan(model)
         if self.heads:
             # the joint (one-bucket) plan of world size 1 beside the per-head buckets
@@ -259,8 +251,7 @@ class HipEngine:
         self.params_changed()
 
     # ------------------------------------------------------------------------------------------
-    def _build_wgrad_plan(self, model: ActorCritic, target_wgs: Optional[int] = None,
-                          chunks_override: Optional[int] = None, joint: bool = False) -> None:
+    def _build_wgrad_plan(self, model: ActorCritic, target_wgs: Optional[int] = None, joint: bool = False) -> None:
         """Task lists of the grouped split-K wgrad launches: (layer, output tile, batch chunk),
         output tiles from wgrad_tiles().
 
@@ -301,40 +292,22 @@ class HipEngine:
             tiles = []  # (layer, n0, k0, nq, kq)
             for li in layers:
                 l = ls[li]
-                tiles += wgrad_tiles(li, l.fan_out, l.fan_in + 1, self.wgrad_waves)
+                tiles += wgrad_tiles(li, l.fan_out, l.fan_in + 1)
             # Batch chunks PER TILE, in proportion to the tile's operand stream ((nq + kq) * 64
             # rows per k-step): every task then streams about the same bytes, and the task count
             # is ~target_wgs = one workgroup per CU (the kernel is bound by each CU's operand
             # stream, so every CU gets one equal share; largest-remainder rounding).
             costs = [t[3] + t[4] for t in tiles]
-            aligned = self.wgrad_aligned if hasattr(self, "wgrad_aligned") else WGRAD_ALIGNED
-            if chunks_override:                       # A/B diagnostics: uniform chunk count
-                nch = [chunks_override] * len(tiles)
-            elif aligned:
-                # one row grid for every tile (tiles sharing an operand read the same rows at the
-                # same time, on the same XCD); cheap tiles take runs of r grid chunks so every
-                # task streams about the same bytes; the finest grid within target_wgs tasks
-                cmax = max(costs)
-                run = [max(1, int(round(cmax / c))) for c in costs]
-                g = 1
-                for cand in range(1, max_chunks + 1):
-                    if sum(-(-cand // r) for r in run) <= target_wgs:
-                        g = cand
-                nch = [-(-g // r) for r in run]
-                grid = _r(-(-self.ldT // g), 64)
-            else:
-                raw = [target_wgs * c / sum(costs) for c in costs]
-                nch = [max(1, int(r)) for r in raw]
-                rest = sorted(range(len(tiles)), key=lambda t: raw[t] - int(raw[t]), reverse=True)
-                for t in rest[:max(0, target_wgs - sum(nch))]:
-                    nch[t] += 1
+            raw = [target_wgs * c / sum(costs) for c in costs]
+            nch = [max(1, int(r)) for r in raw]
+            rest = sorted(range(len(tiles)), key=lambda t: raw[t] - int(raw[t]), reverse=True)
+            for t in rest[:max(0, target_wgs - sum(nch))]:
+                nch[t] += 1
             nch = [min(max_chunks, n) for n in nch]
             tasks, tile_off, base = [], {}, 0
-            for ti, (t, n) in enumerate(zip(tiles, nch)):
+            for t, n in zip(tiles, nch):
                 size = t[3] * t[4] * 64 * 64
                 mc = _r(-(-self.ldT // n), 64)        # even number of 32-row k-steps per task
-                if aligned and not chunks_override:
-                    mc = grid * run[ti]
                 chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
                 tile_off[t] = (base, len(chunks), size)
                 for ci, (m0, m1) in enumerate(chunks):
@@ -786,7 +759,7 @@ class HipEngine:
             self._head_kernel(h, idx_t, first, xt_ready, self.part_joint, self.part_dw_joint[h])
         b = self.joint_bucket
         self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                       b["tasks_host"], b["slab"], self.wgrad_waves)
+                       b["tasks_host"], b["slab"])
         b1, b2 = p.adam_betas
         src_off, src_meta = self.joint_src
         rc, rd = self.items["joint"]
@@ -804,7 +777,7 @@ class HipEngine:
         self._head_kernel(h, idx_t, first, xt_ready, self.part_h[h], self.part_dw[h])
         b = self.buckets[h]
         self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                       b["tasks_host"], b["slab"], self.wgrad_waves)
+                       b["tasks_host"], b["slab"])
         lo, hi = self.head_range[h]
         part = self.part_h[h]
         rc, rd = self.items["policy" if h == 0 else "value"]
@@ -857,7 +830,7 @@ class HipEngine:
                            self.ldT, self.part, False, xt_ready)
         b = self.buckets[0]
         self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                       b["tasks_host"], b["slab"], self.wgrad_waves)
+                       b["tasks_host"], b["slab"])
         if fused_apply:
             if p.loss == "dppo_ref":   # train.py:164: the pre-update log_std, before Adam moves it
                 self.log_std_old.copy_(self.model.flat.data[:self.A])

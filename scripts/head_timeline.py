@@ -44,21 +44,18 @@ def main():
     nblk = eng.nhead_blk
     out = {}
     idx_t, first, xt_ready = eng._minibatch(None)
-    ablations = [int(x) for x in os.environ.get("HEAD_ABLATE", "0").split(",")]
-    for h, abl in [(h, a) for a in ablations for h in (0, 1)]:
+    for h in (0, 1):
         nw = int(ext.head_waves(h))
         buf = torch.zeros(((nblk + EVERY - 1) // EVERY) * nw * 16, dtype=torch.int64, device=dev)
         for _ in range(3):
             eng._head_chain(h, idx_t, first, xt_ready)
         torch.cuda.synchronize()
         ext.set_train_tstamp(buf, EVERY)
-        ext.set_train_ablation(abl)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
         eng._head_chain(h, idx_t, first, xt_ready)
         ev[1].record()
         torch.cuda.synchronize()
-        ext.set_train_ablation(0)
         ext.set_train_tstamp(torch.empty(0, dtype=torch.int64, device=dev), 1)
         t = buf.view(-1, nw, 16).cpu().double()
         d = t[:, :, 1:8] - t[:, :, 0:7]
@@ -73,7 +70,7 @@ def main():
         blk = torch.arange(t.shape[0]) * EVERY
         rnd = blk // ncu
         res["total_by_round"] = {int(r): float(tot[rnd == r].max(dim=1).values.median()) for r in sorted(set(rnd.tolist()))}
-        out[("policy" if h == 0 else "value") + (f"_ablate{abl}" if abl else "")] = res
+        out["policy" if h == 0 else "value"] = res
     print(json.dumps(out, indent=1))
 
 

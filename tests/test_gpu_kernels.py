@@ -86,6 +86,38 @@ def test_value_forward(env_name, dtype, tol):
     assert err / scale < tol, (err, scale)
 
 
+@pytest.mark.parametrize("dtype,tol", [("bf16x3", 2e-5), ("bf16", 3e-2)])
+def test_value_forward_on_head_kernel_matches_tile_kernel(dtype, tol):
+    """values() on the value head's streaming kernel in forward mode (csrc/mlp_head.hip FWD, 128
+    rows per workgroup) vs mlp.hip's value kernel and the fp32 torch model, at a row count that is
+    not a multiple of 128"""
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=1000, exploration_size=1000 * 9,
+                    batch_size=1000 * 9, dtype=dtype)
+    eng, model, _, _ = _engine(p)
+    O = model.num_inputs
+    M = (eng.T + 1) * eng.E
+    assert M % 128 != 0
+    xb = torch.zeros(M, eng.d0, device=DEV)
+    xb[:, :O] = torch.randn(M, O, device=DEV).clamp(-5, 5)
+    xb[:, O] = 1.0
+    eng.x_buf.copy_(eng.encode(xb))
+    out = {}
+    try:
+        for on in (True, False):
+            eng.ext.set_head_kernels(on)
+            eng.values_buf.fill_(float("nan"))
+            eng.values()
+            out[on] = eng.values_buf.clone()
+    finally:
+        eng.ext.set_head_kernels(True)
+    with torch.no_grad():
+        _, _, v = model(eng.decode(eng.x_buf)[:, :O])
+    scale = v.abs().max().item()
+    assert torch.isfinite(out[True]).all()
+    assert (out[True] - v.reshape(-1)).abs().max().item() < tol * scale
+    assert (out[True] - out[False]).abs().max().item() < tol * scale
+
+
 def _torch_rollout(params, model, seed_state_from):
     from pytorch_dppo_amd.runtime.engine_torch import TorchEngine
     spec = get_spec(params.env_name)
@@ -273,9 +305,11 @@ def test_fused_loss_backward_matches_autograd(env_name, dtype, value_loss, conv,
 
 @pytest.mark.parametrize("rows", [32, 64])
 @pytest.mark.parametrize("env_name,mb", [("Humanoid-v2", 200), ("HalfCheetah-v2", 320)])
-def test_fused_loss_backward_row_tiles(rows, env_name, mb):
-    """bf16 fused update at both row tiles (64 rows / 8 waves and 32 rows / 4 waves), with a
-    ragged last tile, vs autograd; and the value kernel at both tiles."""
+def test_fused_loss_backward_row_tiles(rows, env_name, mb, monkeypatch):
+    """bf16 one-kernel tile update (csrc/mlp.hip; DPPO_HEADS=0) at both row tiles (64 rows / 8
+    waves and 32 rows / 4 waves), with a ragged last tile, vs autograd; and the value kernel at
+    both tiles."""
+    monkeypatch.setenv("DPPO_HEADS", "0")
     ext = _ext()
     p = ppo_preset(device="gpu", env_name=env_name, num_envs=64, exploration_size=64 * 8,
                    batch_size=mb, dtype="bf16", ent_coeff=0.01)
@@ -299,80 +333,8 @@ def test_fused_loss_backward_row_tiles(rows, env_name, mb):
         ext.set_mlp_rows(0)
 
 
-def test_s3_wgrad_dense_dma_layout_is_bitwise_identical():
-    """split-bf16 wgrad (csrc/wgrad.hip): the dense-DMA fragment layout moves the same fragments
-    into a different LDS image and feeds the same MFMAs in the same order — the full gradient is
-    bitwise the sparse layout's."""
-    ext = _ext()
-    p = ppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 8,
-                   batch_size=512, dtype="bf16x3", ent_coeff=0.01)
-    eng, model, _, _ = _engine(p)
-    _fill_buffer(eng, model)
-    idx = torch.randperm(eng.N, generator=torch.Generator().manual_seed(5))[:512]
-    state = ext.wgrad_dense()
-    res = {}
-    try:
-        for on in (True, False):
-            ext.set_wgrad_dense(on)
-            eng.begin_update()
-            eng.grad(idx)
-            res[on] = eng.grad_flat.clone()
-    finally:
-        ext.set_wgrad_dense(state)
-    assert torch.equal(res[True], res[False])
-    assert res[True].abs().sum().item() > 0
-
-
-@pytest.mark.parametrize("env_name,mb,stages,dense", [
-    ("Humanoid-v2", 512, 3, 1), ("Humanoid-v2", 512, 3, 0), ("Humanoid-v2", 200, 2, 1),
-    ("Humanoid-v2", 200, 2, 0), ("HalfCheetah-v2", 256, 3, 1), ("Pendulum-v0", 64, 3, 0)])
-def test_s3_streaming_update_matches_tile_kernel(env_name, mb, stages, dense, monkeypatch):
-    """split-bf16: the row-stationary weight-streaming update (csrc/mlp_stream.hip, 64 rows per
-    workgroup, every ring depth, both DMA fragment layouts) vs the 32-row tile kernel (mlp.hip) on the same minibatch —
-    gradients, loss terms and the wgrad operands both write (idx gather, ragged last tile, the
-    in-kernel X^T path)."""
-    ext = _ext()
-    monkeypatch.setenv("DPPO_HEADS", "0")   # the one-kernel update (the per-head kernels have their own test)
-    p = ppo_preset(device="gpu", env_name=env_name, num_envs=64, exploration_size=64 * 8,
-                   batch_size=mb, dtype="bf16x3", ent_coeff=0.01)
-    eng, model, _, _ = _engine(p)
-    xq = _fill_buffer(eng, model)
-    idx = torch.randperm(eng.N, generator=torch.Generator().manual_seed(11))[:mb]
-    res = {}
-    state = ext.s3_stream_state()
-    try:
-        for on in (True, False):
-            ext.set_s3_stream(on, stages, dense)
-            eng.sync_tile()
-            assert eng.train_rows == (64 if on else 32)
-            eng.begin_update()
-            eng.grad(idx)
-            res[on] = (eng.grad_flat.clone(), eng.last_losses(), eng.g1vT.clone(), eng.h1pT.clone())
-    finally:
-        ext.set_s3_stream(state > 0, (state % 10) or 3, state // 10 if state else -1)
-        eng.sync_tile()
-    g_rs, l_rs, g1_rs, h1_rs = res[True]
-    g_t, l_t, g1_t, h1_t = res[False]
-    rel = (g_rs - g_t).norm().item() / (g_t.norm().item() + 1e-12)
-    assert rel < 2e-5, rel
-    for k in ("loss_clip", "loss_value"):
-        assert abs(l_rs[k] - l_t[k]) < 1e-5 * (1 + abs(l_t[k])), (k, l_rs[k], l_t[k])
-    from pytorch_dppo_amd.models.actor_critic import fm_index
-
-    def rowmajor(buf, nfeat):   # FM [features][ldT] -> row-major, the call's mb columns
-        r = torch.arange(nfeat, device=DEV).repeat_interleave(mb)
-        c = torch.arange(mb, device=DEV).repeat(nfeat)
-        return eng.decode(buf).reshape(-1)[fm_index(r, c, eng.ldT)].view(nfeat, mb)
-
-    n1p, n1v = model.layer("p_fc1").fan_out, model.layer("v_fc1").fan_out
-    for a_, b_ in ((rowmajor(h1_rs, n1p), rowmajor(h1_t, n1p)), (rowmajor(g1_rs, n1v), rowmajor(g1_t, n1v))):
-        assert (a_ - b_).norm().item() <= 1e-5 * b_.norm().item()
-    g_ref, _ = _torch_grad(model, p, xq, eng, idx.to(DEV))
-    assert (g_rs - g_ref).norm().item() / g_ref.norm().item() < 2e-4
-
-
 def test_s3_other_hidden_sizes_fall_back_to_tile_kernel():
-    """the streaming update is specialised for the reference network's tile counts; any other
+    """the per-head kernels are specialised for the reference network's tile counts; any other
     hidden sizes run the 32-row tile kernel, still at fp32 accuracy"""
     p = ppo_preset(device="gpu", env_name="HalfCheetah-v2", num_envs=64, exploration_size=64 * 8,
                    batch_size=256, dtype="bf16x3", ent_coeff=0.01, hidden=(64, 48))
@@ -593,17 +555,22 @@ def test_head_chains_through_rccl_bit_identical_to_fused(overlap, monkeypatch):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("env_name,mb", [("Humanoid-v2", 512), ("Humanoid-v2", 200), ("HalfCheetah-v2", 256),
-                                         ("Pendulum-v0", 64)])
+@pytest.mark.parametrize("env_name,mb,dtype", [("Humanoid-v2", 512, "bf16x3"), ("Humanoid-v2", 200, "bf16x3"),
+                                               ("HalfCheetah-v2", 256, "bf16x3"), ("Pendulum-v0", 64, "bf16x3"),
+                                               ("Humanoid-v2", 512, "bf16"), ("HalfCheetah-v2", 200, "bf16")])
 @pytest.mark.parametrize("loss", ["ppo", "dppo_ref"])
-def test_head_kernels_match_one_kernel_update(env_name, mb, loss, monkeypatch):
+def test_head_kernels_match_one_kernel_update(env_name, mb, dtype, loss, monkeypatch):
     """split-bf16: the per-head streaming kernels (csrc/mlp_head.hip, 128 rows per workgroup,
-    policy and value chains separately) vs the one-kernel streaming update (DPPO_HEADS=0) on the
+    policy and value chains separately) vs the one-kernel 32-row tile update (csrc/mlp.hip,
+    DPPO_HEADS=0) on the
     same minibatch — gradient, loss sums and the wgrad operands both write (idx gather, ragged last
-    tile, the in-kernel X^T path) — and vs autograd."""
+    tile, the in-kernel X^T path) — and vs autograd.  bf16: both kernels round the same fp32 values
+    to bf16 operands, but their fp32 sums run in different orders, so a value next to a rounding
+    boundary can round differently: relative budgets instead of the split-bf16 ones."""
     from pytorch_dppo_amd.models.actor_critic import fm_index
     kw = dict(device="gpu", env_name=env_name, num_envs=64, exploration_size=64 * 8, batch_size=mb,
-              dtype="bf16x3", ent_coeff=0.01, loss=loss)
+              dtype=dtype, ent_coeff=0.01, loss=loss)
+    bf = dtype == "bf16"
     p = ppo_preset(**kw) if loss == "ppo" else dppo_preset(**kw)
     res = {}
     for heads in ("1", "0"):
@@ -625,19 +592,20 @@ def test_head_kernels_match_one_kernel_update(env_name, mb, loss, monkeypatch):
                       rowmajor(eng.xT, model.num_inputs), eng.mu_prev.clone(), eng.v_prev.clone())
         if heads == "1" and loss == "ppo":
             g_ref, _ = _torch_grad(model, p, xq, eng, idx.to(DEV))
-            assert (eng.grad_flat - g_ref).norm().item() / g_ref.norm().item() < 2e-4
+            assert (eng.grad_flat - g_ref).norm().item() / g_ref.norm().item() < (6e-2 if bf else 2e-4)
     g_h, l_h, h1_h, g1_h, x_h, mp_h, vp_h = res["1"]
     g_o, l_o, h1_o, g1_o, x_o, mp_o, vp_o = res["0"]
     rel = (g_h - g_o).norm().item() / (g_o.norm().item() + 1e-12)
-    assert rel < 2e-5, rel
+    assert rel < (2e-2 if bf else 2e-5), rel
     for k in ("loss_clip", "loss_value", "loss_ent", "approx_kl", "clipfrac"):
-        assert abs(l_h[k] - l_o[k]) < 1e-5 * (1 + abs(l_o[k])), (k, l_h[k], l_o[k])
+        assert abs(l_h[k] - l_o[k]) < (1e-2 if bf else 1e-5) * (1 + abs(l_o[k])), (k, l_h[k], l_o[k])
     for a_, b_ in ((h1_h, h1_o), (g1_h, g1_o)):
-        assert (a_ - b_).norm().item() <= 1e-5 * b_.norm().item()
+        assert (a_ - b_).norm().item() <= (1e-2 if bf else 1e-5) * b_.norm().item()
     assert torch.equal(x_h, x_o)            # x^T is a copy of the observation rows
     if loss == "dppo_ref":                  # train.py:164 model_old <- model, per row (fp32 summation order differs)
-        assert (mp_h - mp_o).abs().max().item() <= 2e-5 * (1 + mp_o.abs().max().item())
-        assert (vp_h - vp_o).abs().max().item() <= 2e-5 * (1 + vp_o.abs().max().item())
+        t = 2e-2 if bf else 2e-5
+        assert (mp_h - mp_o).abs().max().item() <= t * (1 + mp_o.abs().max().item())
+        assert (vp_h - vp_o).abs().max().item() <= t * (1 + vp_o.abs().max().item())
         assert bool((mp_h != 0).any()) and bool((vp_h != 0).any())
 
 
@@ -658,30 +626,6 @@ def test_graph_replay_bit_identical_to_eager(batch):
     assert torch.equal(we.model.flat.data, wg.model.flat.data)
     assert torch.equal(we.engine.adam_m, wg.engine.adam_m)
     assert me["loss_value"] == mg["loss_value"]
-
-
-def test_wgrad_lds_dma_matches_register_path_bitwise():
-    """The LDS-DMA staged wgrad (default) and the register-streamed one accumulate the same
-    k-steps in the same order: gradients must agree bit for bit (fp32 and bf16)."""
-    for dt in ("fp32", "bf16"):
-        p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 8,
-                        batch_size=64 * 8, num_epoch=1, dtype=dt)
-        eng, model, env, st = _engine(p)
-        st.observes(env.observe())
-        eng.rollout()
-        eng.values()
-        eng.gae()
-        eng.begin_update()
-        ext = eng.ext
-        eng.wgrad_waves = 8          # the register-streamed kernel takes 8-wave tiles
-        eng._build_wgrad_plan(model)
-        outs = []
-        for impl in (0, 1):
-            ext.set_wgrad_impl(impl)
-            eng.grad(None)
-            outs.append(eng.grad_flat.clone())
-        ext.set_wgrad_impl(0)
-        assert torch.equal(outs[0], outs[1]), (dt, (outs[0] - outs[1]).abs().max().item())
 
 
 def test_deferred_metrics_match_synchronous():

@@ -20,15 +20,14 @@ def _r(x, m):
     return -(-x // m) * m
 
 
-@pytest.mark.parametrize("waves", [8, 16])
 @pytest.mark.parametrize("env", sorted(LAYERS))
-def test_tiles_cover_each_gradient_once(env, waves):
+def test_tiles_cover_each_gradient_once(env):
     for li, (n, fan_in) in enumerate(LAYERS[env]):
         k = fan_in + 1
         cover = torch.zeros(_r(n, 64), _r(k, 64), dtype=torch.int32)
-        for (tl, n0, k0, nq, kq) in wgrad_tiles(li, n, k, waves):
+        for (tl, n0, k0, nq, kq) in wgrad_tiles(li, n, k):
             assert tl == li
-            assert nq >= 1 and kq >= 1 and nq * kq <= waves and nq + kq <= (8 if waves == 16 else 6)
+            assert nq >= 1 and kq >= 1 and nq * kq <= 8 and nq + kq <= 6
             assert n0 % 64 == 0 and k0 % 64 == 0
             # operand buffers hold _r(rows, WT) rows (engine_hip: g_rows / x_rows)
             assert n0 + 64 * nq <= _r(n, WT) and k0 + 64 * kq <= _r(k, WT)
@@ -43,11 +42,9 @@ def test_humanoid_value_fc1_streams_fewer_rows_than_square_tiles():
     assert rows_per_step == 2304 and rows_per_step < square
 
 
-@pytest.mark.parametrize("waves", [8, 16])
-@pytest.mark.parametrize("aligned", [False, True])
 @pytest.mark.parametrize("heads", [False, True])
 @pytest.mark.parametrize("env", ["Humanoid-v2", "HalfCheetah-v2"])
-def test_plan_tasks_cover_tiles_and_batch_once(env, heads, aligned, waves):
+def test_plan_tasks_cover_tiles_and_batch_once(env, heads):
     """The full task list (HipEngine._build_wgrad_plan run on a CPU stand-in): each output tile's
     tasks cover the batch rows [0, ldT) exactly once with 64-row-aligned chunks, every task owns
     a disjoint slab region, the task count is ~one per CU, and every parameter's gather entry
@@ -61,7 +58,7 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads, aligned, waves):
     model = ActorCritic(spec.obs_dim, spec.act_dim)
     stub = SimpleNamespace(L=model.packed_layout(), ldT=65536, A=spec.act_dim, device=torch.device("cpu"),
                            heads=heads, head_range=[model.head_ranges["policy"], model.head_ranges["value"]],
-                           _slab_index=HipEngine._slab_index, wgrad_aligned=aligned, wgrad_waves=waves)
+                           _slab_index=HipEngine._slab_index)
     HipEngine._build_wgrad_plan(stub, model, target_wgs=256)
     total = 0
     for b in stub.buckets:
