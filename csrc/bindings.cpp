@@ -538,7 +538,7 @@ void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
   TORCH_CHECK(step >= 1, "gather_adam needs the host step number (eager launches only)");
   const int nblk = (int)norm_part.numel();
   check(norm_part, "norm_part", at::kFloat, nblk);
-  TORCH_CHECK(nblk > (nitems + 63) / 64 && nblk <= 4096, "norm_part must hold more blocks than the reduce blocks");
+  TORCH_CHECK(nblk > item_blocks((int)nitems) && nblk <= 4096, "norm_part must hold more blocks than the reduce blocks");
   const float* q = nullptr;
   if (qmul.defined() && qmul.numel() > 0) { check(qmul, "qmul", at::kFloat, n); q = qmul.data_ptr<float>(); }
   launch_gather_adam(slab.data_ptr<float>(), src_off.data_ptr<int>(), src_meta.data_ptr<int>(),

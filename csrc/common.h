@@ -261,30 +261,37 @@ __device__ __forceinline__ float slab_sum(const float* __restrict__ p, int nch, 
 }
 
 // Column sums of the per-workgroup partial rows (the reduce items of the gather kernels): the
-// 256 threads of a block take items j = 64 b + (tid % 64) (consecutive items are consecutive
-// columns: coalesced) in 4 row groups; row group g sums rows g, g + 4, ... in order (16 loads in
-// flight), then thread tid < 64 adds the 4 groups in order — fixed order, deterministic.  Returns
-// true on the threads that own an item (tid < 64, j < nitems) with its sum in `out`.
+// 256 threads of a block take items j = IPB b + (tid % IPB) (consecutive items are consecutive
+// columns: one 128-byte segment per row) in RG = 256 / IPB row groups; row group g sums rows
+// g, g + RG, ... in order (16 loads in flight: 512 partial rows are 4 dependent batches), then
+// thread tid < IPB adds the RG groups in order — fixed order, deterministic.  Returns true on the
+// threads that own an item (tid < IPB, j < nitems) with its sum in `out`.
 // red_dst[j] >= 0: flat gradient index (of the gathered slice); -1 - q: loss_out[q].
 __device__ __forceinline__ bool item_reduce(const float* __restrict__ part, int nprow, int npart,
                                             const int* __restrict__ red_col, int nitems, int b,
                                             float* red, float& out, int& j) {
-  const int tid = threadIdx.x, c = tid & 63, rg = tid >> 6;
-  j = 64 * b + c;
+  constexpr int RG = 256 / ITEM_IPB;
+  const int tid = threadIdx.x, c = tid % ITEM_IPB, rg = tid / ITEM_IPB;
+  j = ITEM_IPB * b + c;
   float s = 0.f;
   if (j < nitems) {
     const float* p = part + red_col[j];
-    for (int r0 = rg; r0 < nprow; r0 += 64) {
+    for (int r0 = rg; r0 < nprow; r0 += 16 * RG) {
       float x[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) x[u] = (r0 + 4 * u < nprow) ? p[(size_t)(r0 + 4 * u) * npart] : 0.f;
+      for (int u = 0; u < 16; ++u) x[u] = (r0 + RG * u < nprow) ? p[(size_t)(r0 + RG * u) * npart] : 0.f;
 #pragma unroll
       for (int u = 0; u < 16; ++u)
-        if (r0 + 4 * u < nprow) s += x[u];
+        if (r0 + RG * u < nprow) s += x[u];
     }
   }
   red[tid] = s;
   __syncthreads();
-  if (tid < 64) out = ((red[tid] + red[64 + tid]) + red[128 + tid]) + red[192 + tid];
-  return tid < 64 && j < nitems;
+  if (tid < ITEM_IPB) {
+    float o = red[tid];
+#pragma unroll
+    for (int g = 1; g < RG; ++g) o += red[g * ITEM_IPB + tid];
+    out = o;
+  }
+  return tid < ITEM_IPB && j < nitems;
 }

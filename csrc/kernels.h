@@ -103,6 +103,10 @@ extern "C" void launch_mlp_head_value(int dt, const MlpArgs& a, hipStream_t s); 
 extern "C" void set_head_kernels(int enable);
 extern "C" int head_kernels_enabled();
 
+// reduce items per block of the gather kernels (common.h item_reduce)
+constexpr int ITEM_IPB = 32;
+inline __host__ __device__ int item_blocks(int nitems) { return (nitems + ITEM_IPB - 1) / ITEM_IPB; }
+
 struct WgradTask {
   int layer;      // 0..5
   int n0, k0;     // output tile origin

@@ -607,15 +607,54 @@ void train_t(const MlpArgs& a, hipStream_t s) {
 
 int g_s3_value_waves = 8;   // split-bf16 value forward: 4 or 8 waves per 32-row workgroup (A/B)
 
+int cu_count() {
+  static int n = 0;
+  if (n <= 0) {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int DT>
+void value_t(const MlpArgs& a, hipStream_t s);
+
+// The reference network's value forward on the value head's 128-row streaming kernel in forward
+// mode (csrc/mlp_head.hip; set_head_kernels(0) keeps the tile kernels).  One workgroup per CU at a
+// time, so a launch costs whole rounds of ncu workgroups: the bench's T*E + E = 69,632 rows are
+// 2.125 rounds, and the 32-workgroup third round costs as much as a full one.  Rows past the last
+// full round (when they are at most a quarter round) go to the 32-row tile kernel instead, whose
+// small workgroups spread over all CUs.
+template <int DT>
+void value_head_t(const MlpArgs& a, hipStream_t s) {
+  const int round = mlp_head_rows() * cu_count();
+  const int full = a.M / round * round;
+  if (full > 0 && full < a.M && a.M - full <= round / 4) {
+    MlpArgs h = a;
+    h.M = full;
+    launch_mlp_head_value(DT, h, s);
+    MlpArgs t = a;
+    t.M = a.M - full;
+    if (t.idx) t.idx += full;
+    else t.row0 += full;
+    t.v_out += full;
+    value_t<DT>(t, s);   // (t.M < one round: takes the tile kernel below)
+    return;
+  }
+  launch_mlp_head_value(DT, a, s);
+}
+
 template <int DT>
 void value_t(const MlpArgs& a, hipStream_t s) {
+  const bool head = DT != DT_F32 && DT != DT_FP8 && mlp_head_applies(a) &&
+                    a.M >= mlp_head_rows() * cu_count() / 4;
   if constexpr (DT == DT_F32) {
     value_launch<DT, 32, 4>(a, s);
   } else if constexpr (DT == DT_S3) {
-    // the reference network: the value head's 128-row streaming kernel in forward mode
-    // (csrc/mlp_head.hip; DPPO_HEADS=0 / set_head_kernels(0) keep this kernel)
-    if (mlp_head_applies(a)) {
-      launch_mlp_head_value(DT_S3, a, s);
+    if (head) {
+      value_head_t<DT>(a, s);
       return;
     }
     // like the update: the 32-row tile takes most of LDS (one workgroup per CU), so a second
@@ -624,8 +663,8 @@ void value_t(const MlpArgs& a, hipStream_t s) {
     else value_launch<DT, 32, 4>(a, s);
   } else {
     if constexpr (DT == DT_BF16) {
-      if (mlp_head_applies(a)) {   // the value head's 128-row streaming kernel, forward mode
-        launch_mlp_head_value(DT_BF16, a, s);
+      if (head) {
+        value_head_t<DT>(a, s);
         return;
       }
     }

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
   const float bc2 = 1.f - powf(b2, step);
   const float step_size = lr / bc1;
   const float rbc2 = 1.f / sqrtf(bc2);
-  const int nrb = (nitems + 63) / 64;   // reduce blocks
+  const int nrb = item_blocks(nitems);   // reduce blocks
   float ss = 0.f;
   // the optimizer-state loads are issued before the gradient is formed (they do not depend on
   // it), so their latency overlaps the slab loads'
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
       }
     }
     __syncthreads();
-    red[threadIdx.x] = threadIdx.x < 64 ? ss : 0.f;
+    red[threadIdx.x] = threadIdx.x < ITEM_IPB ? ss : 0.f;
     __syncthreads();
     for (int w = 32; w > 0; w >>= 1) {
       if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];

@@ -139,7 +139,7 @@ void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((wgrad_kernel<DT, S>), dim3(a.ntasks), dim3(WG_WAVES * 64), lds, s, a);
 }
 
-// Blocks [0, ceil(nitems / 64)): the reduce items (log_std, loss-term sums, the per-head
+// Blocks [0, item_blocks(nitems)): the reduce items (log_std, loss-term sums, the per-head
 // kernels' fused narrow-layer weight gradients): column sums of the per-workgroup partial rows in
 // a fixed order (item_reduce), grad[d] = scale * sum or loss_out[q] (red_dst).
 // Blocks past them: grad[i] = scale * sum_{c < nch} slab[src_off[i] + c * stride], i in
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
                                                           const int* __restrict__ red_dst, int nitems,
                                                           float scale, float* __restrict__ grad, int i_lo,
                                                           int i_hi, float* __restrict__ loss_out) {
-  const int nrb = (nitems + 63) / 64;
+  const int nrb = item_blocks(nitems);
   if ((int)blockIdx.x < nrb) {
     __shared__ float red[256];
     float tot = 0.f;
@@ -193,7 +193,7 @@ extern "C" void launch_grad_gather(const float* slab, const int* src_off, const 
   int grid = (i_hi - i_lo + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
-  grid += (nitems + 63) / 64;
+  grid += item_blocks(nitems);
   hipLaunchKernelGGL(grad_gather_kernel, dim3(grid), dim3(256), 0, s, slab, src_off, src_meta, part, nblk, npart,
                      red_col, red_dst, nitems, scale, grad, i_lo, i_hi, loss_out);
   HIP_CHECK_LAUNCH();

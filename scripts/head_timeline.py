@@ -2,7 +2,9 @@
 
 Lane 0 of every wave of every EVERY-th workgroup stamps s_memtime (shader clock) at the phase
 boundaries; this prints the median cycles per phase (max over the 4 waves) for the policy and
-the value kernel at the bench geometry (Humanoid dims, 65,536-row full batch, split-bf16).
+the value kernel at the bench geometry (Humanoid dims, 65,536-row full batch).
+
+    python scripts/head_timeline.py [bf16x3|bf16]
 """
 import json
 import os
@@ -27,7 +29,7 @@ def main():
     os.environ.setdefault("DPPO_HEADS", "1")
     dev = torch.device("cuda", 0)
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536, batch_size=65536,
-                    dtype="bf16x3")
+                    dtype=sys.argv[1] if len(sys.argv) > 1 else "bf16x3")
     spec = get_spec(p.env_name)
     torch.manual_seed(0)
     model = ActorCritic(spec.obs_dim, spec.act_dim).to(dev)

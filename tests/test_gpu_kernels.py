@@ -87,16 +87,18 @@ def test_value_forward(env_name, dtype, tol):
 
 
 @pytest.mark.parametrize("dtype,tol", [("bf16x3", 2e-5), ("bf16", 3e-2)])
-def test_value_forward_on_head_kernel_matches_tile_kernel(dtype, tol):
+@pytest.mark.parametrize("E,T", [(1000, 9), (2048, 16)])
+def test_value_forward_on_head_kernel_matches_tile_kernel(dtype, tol, E, T):
     """values() on the value head's streaming kernel in forward mode (csrc/mlp_head.hip FWD, 128
-    rows per workgroup) vs mlp.hip's value kernel and the fp32 torch model, at a row count that is
-    not a multiple of 128"""
-    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=1000, exploration_size=1000 * 9,
-                    batch_size=1000 * 9, dtype=dtype)
+    rows per workgroup) vs mlp.hip's value kernel and the fp32 torch model: a row count that is not
+    a multiple of 128, and (2048 x 17 rows on 256 CUs) one past a whole round of workgroups, whose
+    tail rows the 32-row kernel takes"""
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=E, exploration_size=E * T,
+                    batch_size=E * T, dtype=dtype)
     eng, model, _, _ = _engine(p)
     O = model.num_inputs
     M = (eng.T + 1) * eng.E
-    assert M % 128 != 0
+    assert M % 128 != 0 or M > 128 * torch.cuda.get_device_properties(DEV).multi_processor_count
     xb = torch.zeros(M, eng.d0, device=DEV)
     xb[:, :O] = torch.randn(M, O, device=DEV).clamp(-5, 5)
     xb[:, O] = 1.0
