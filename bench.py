@@ -182,6 +182,9 @@ def main():
     total_steps = rows * ctx.world_size * args.steps
     value = total_steps / elapsed
     heads = bool(getattr(w.engine, "heads", False))
+    # the gradient all-reduce in use: native RCCL on the compute stream (csrc/comm.cpp), the
+    # process group's (per-head chains), or none (world size 1, not forced)
+    grad_ar = ("rccl_in_stream" if ctx.native is not None else "process_group") if ctx.collective else "none"
     del w
     variants = {}
     for dt in [d for d in args.variants.split(",") if d and d != args.dtype]:
@@ -204,7 +207,7 @@ def main():
                                               and ctx.backend == "nccl" else 0),
                           "rollout_len": T, "num_epoch": args.num_epoch,
                           "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout, "graphs": args.graphs,
-                          "per_head_chains": heads,
+                          "per_head_kernels": heads, "grad_allreduce": grad_ar,
                           "note": ("value = total env steps/s of all n_gpus workers (one DPPO worker per GPU); "
                                    "the 8-worker node figure of the metric is the n_gpus=8 run; vs_baseline "
                                    "divides by the reference's derived 8-worker CPU node estimate (BASELINE.md)"),

@@ -587,8 +587,11 @@ void pack(torch::Tensor p, torch::Tensor wimg, torch::Tensor w_map, torch::Tenso
 
 }  // namespace
 
+void register_comm(pybind11::module& m);   // csrc/comm.cpp: native RCCL communicator
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X-native DPPO kernels (gfx950 HIP)";
+  register_comm(m);
   m.def("rollout", &rollout);
   m.def("mlp_value", &mlp_value);
   m.def("mlp_train", &mlp_train);

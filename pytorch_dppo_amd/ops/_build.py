@@ -25,6 +25,7 @@ EXT_NAME = "_dppo_hip"
 ARCH = os.environ.get("DPPO_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 DEVICE_SRCS = ["rollout.hip", "mlp.hip", "mlp_head.hip", "wgrad.hip", "optim.hip", "obs.hip"]
+HOST_SRCS = ["bindings.cpp", "comm.cpp"]   # compiled with the torch include paths
 HEADERS = ["common.h", "mlp_core.h", "kernels.h"]
 
 
@@ -44,7 +45,8 @@ def _torch_flags(ext_name: str = EXT_NAME):
                                          f"-DTORCH_EXTENSION_NAME={ext_name}",
                                          "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1"]
     ldflags = [f"-L{p}" for p in libdirs] + [f"-Wl,-rpath,{p}" for p in libdirs] + [
-        "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip"]
+        "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
+        "-lrccl"]   # torch's own librccl.so (first -L): one RCCL in the process (csrc/comm.cpp)
     return cflags, ldflags
 
 
@@ -88,7 +90,7 @@ def build(verbose: bool = False, force: bool = False, variant: str = "", csrc: s
     timed interleaved in one process on one box."""
     os.makedirs(BUILD, exist_ok=True)
     tcflags, ldflags = _torch_flags(EXT_NAME + (f"_{variant}" if variant else ""))
-    jobs = [(s, []) for s in DEVICE_SRCS] + [("bindings.cpp", tcflags)]
+    jobs = [(s, []) for s in DEVICE_SRCS] + [(s, tcflags) for s in HOST_SRCS]
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         objs = list(ex.map(lambda j: _compile(j[0], j[1], verbose, csrc), jobs))
     out = ext_path(variant)

@@ -14,6 +14,14 @@ Reference → here:
 
 On GPU the backend is ``nccl`` (= RCCL on ROCm, xGMI inside a node); on CPU it is ``gloo``.
 There is no custom transport and no multi-backend dispatch on the hot path.
+
+The per-epoch gradient all-reduce and the per-iteration statistics all-reduce of a GPU worker
+run on a NATIVE RCCL communicator (:class:`NativeComm`, ``csrc/comm.cpp``) created from the
+process group once: its collectives are enqueued on the compute stream itself, in stream order.
+torch's ProcessGroupNCCL runs every collective on an internal stream, and each one then costs
+two cross-stream event hops the compute queue idles on (~26 us per all-reduce measured with the
+collectives forced at world size 1: 5.03 vs 4.21 ms per bench iteration with the two-chain
+overlap design that needed them; profiles/r3/rccl_forced_vs_plain.md).
 """
 from __future__ import annotations
 
@@ -26,6 +34,27 @@ import torch
 import torch.distributed as dist
 
 
+class NativeComm:
+    """RCCL communicator over the process group's ranks, collectives on a caller-named stream
+    (default: the current one).  Created collectively: rank 0's ncclUniqueId is broadcast over
+    the existing group."""
+
+    def __init__(self, ext, rank: int, world_size: int):
+        idb = [ext.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(idb, src=0)
+        self.ext = ext
+        self.world_size = world_size
+        self.handle = ext.comm_init(idb[0], world_size, rank)
+
+    def allreduce_(self, t: torch.Tensor, mean: bool = False) -> None:
+        self.ext.comm_allreduce(self.handle, t, mean)
+
+    def destroy(self) -> None:
+        if self.handle is not None:
+            self.ext.comm_destroy(self.handle)
+            self.handle = None
+
+
 @dataclass
 class DistContext:
     rank: int = 0
@@ -36,6 +65,29 @@ class DistContext:
     # run the hot-path collectives even at world size 1, where a sum over one rank is the
     # identity (tests use it to exercise the real RCCL call on the 1-GPU box)
     force_collectives: bool = False
+    native: Optional[NativeComm] = None
+
+    def init_native_comm(self, ext) -> bool:
+        """create the in-stream RCCL communicator (RCCL groups only; DPPO_NATIVE_COMM=0: off)"""
+        if (self.native is None and self.enabled and self.backend == "nccl" and self.device.type == "cuda"
+                and os.environ.get("DPPO_NATIVE_COMM", "1") != "0" and hasattr(ext, "comm_init")):
+            self.native = NativeComm(ext, self.rank, self.world_size)
+        return self.native is not None
+
+    def grad_allreduce_fn(self, mean: bool = False):
+        """the engines' hot-path all-reduce callback for the flat gradient: None when no collective
+        runs; on a native communicator an in-stream sum/mean (attribute ``in_stream``), else the
+        async process-group all-reduce returning its work handle (the engine scales for mean)."""
+        if not self.collective:
+            return None
+        if self.native is not None:
+            nat = self.native
+
+            def ar(t):
+                nat.allreduce_(t, mean)
+            ar.in_stream = True
+            return ar
+        return lambda t: self.allreduce_grads(t, async_op=True)
 
     @property
     def enabled(self) -> bool:
@@ -59,6 +111,9 @@ class DistContext:
         With ``async_op`` the returned work handle's ``wait()`` orders the consumer after
         the collective on the device stream (RCCL runs on its own stream)."""
         if not self.collective:
+            return None
+        if self.native is not None and flat_grad.dtype == torch.float32:
+            self.native.allreduce_(flat_grad, mean)    # in stream order: nothing to wait on
             return None
         work = dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, async_op=async_op)
         if mean:
@@ -89,7 +144,10 @@ class DistContext:
             if extra is not None:
                 parts.append(extra.reshape(-1).to(self.device, torch.float64))
             buf = torch.cat(parts)
-            dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+            if self.native is not None:
+                self.native.allreduce_(buf)          # in stream order
+            else:
+                dist.all_reduce(buf, op=dist.ReduceOp.SUM)
             if extra is not None:
                 extra.copy_(buf[2 * O:].view(extra.shape))
             return count * self.world_size, buf[:O], buf[O:2 * O]
@@ -136,6 +194,12 @@ class DistContext:
                 dist.barrier()
 
     def destroy(self) -> None:
+        if self.native is not None:
+            try:
+                self.native.destroy()
+            except Exception:
+                pass
+            self.native = None
         if dist.is_available() and dist.is_initialized():
             try:
                 dist.destroy_process_group()

@@ -689,6 +689,16 @@ class HipEngine:
         if allreduce is None and self.can_fuse_apply(extra_grad):
             self.grad(idx, apply=True)          # world size 1: gather + Adam in one launch
             return
+        if self.heads and getattr(allreduce, "in_stream", False) and not self.use_graphs:
+            # native RCCL on the compute stream (parallel/dist.py NativeComm): no cross-stream
+            # event hops, so the joint kernels (one wgrad, one gather) then the all-reduce in
+            # stream order, then the whole-vector Adam (+ clip)
+            self._flush_value()
+            idx_t, first, xt_ready = self._minibatch(idx)
+            self._joint_grad(idx_t, first, xt_ready)
+            allreduce(self.grad_flat)
+            self.apply(extra_grad)
+            return
         if not self.heads:
             self.grad(idx)
             if allreduce is not None:
@@ -750,6 +760,19 @@ class HipEngine:
                            [float(p.clip), float(p.ent_coeff)], self.tbufs, self.ldT, part, False, xt_ready)
         if h == 0 and p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])   # train.py:164, before Adam moves it
+
+    def _joint_grad(self, idx_t, first: bool, xt_ready: bool) -> None:
+        """both head kernels (one shared partial buffer), ONE wgrad over both heads' layers, ONE
+        gather of the whole gradient into grad_flat (no optimizer step)"""
+        for h in (0, 1):
+            self._head_kernel(h, idx_t, first, xt_ready, self.part_joint, self.part_dw_joint[h])
+        b = self.joint_bucket
+        self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
+                       b["tasks_host"], b["slab"])
+        src_off, src_meta = self.joint_src
+        rc, rd = self.items["joint"]
+        self.ext.grad_gather(b["slab"], src_off, src_meta, self.part_joint, self.nhead_blk, self.part_joint.shape[1],
+                             rc, rd, 1.0 / self.mb, self.grad_flat, self.loss_sums, self.A, -1)
 
     def _joint_step(self, idx_t, first: bool, xt_ready: bool) -> None:
         """world size 1: policy kernel, value kernel (one shared partial buffer), ONE wgrad over

@@ -63,6 +63,8 @@ class DPPOWorker:
                                     device=self.device, max_episode_length=params.max_episode_length)
         self.stats = RunningObsStats(self.spec.obs_dim, self.device)
         self.engine = build_engine(params, self.model, self.env, self.stats, self.device, action_rank)
+        if ctx.collective and hasattr(self.engine, "ext"):
+            ctx.init_native_comm(self.engine.ext)   # in-stream RCCL (collective: every rank)
         self.iteration = 0
         self.env_steps = 0            # global (all ranks)
         self.updates = 0
@@ -179,9 +181,11 @@ class DPPOWorker:
                     extra = 1.0  # Q1: Shared_grad_buffers start at ones (model.py:51)
                 last = epoch == p.num_epoch - 1 and b == nmb - 1
                 if hasattr(eng, "step"):
-                    # GPU engine: gradient -> (async RCCL all-reduce per head) -> Adam, the heads as
-                    # independent chains whose all-reduces overlap the other head's kernels
-                    ar = (lambda t: self.ctx.allreduce_grads(t, async_op=True)) if self.ctx.collective else None
+                    # GPU engine: gradient -> all-reduce -> Adam.  Native RCCL (the default on an
+                    # RCCL group): in stream order after the joint gather; a process-group
+                    # all-reduce: per-head chains, each head's async all-reduce overlapping the
+                    # other head's kernels (engine_hip.HipEngine.step)
+                    ar = self.ctx.grad_allreduce_fn(mean)
                     eng.step(idx, extra, allreduce=ar, mean=mean)
                     self.updates += 1
                     continue

@@ -484,7 +484,6 @@ def test_fp8_rollout_tracks_fp32_and_engine_trains():
 
 def test_rccl_world1_allreduce_and_training_step():
     """The real RCCL collective path at world size 1 (the 1-GPU box): grads, obs moments."""
-    import torch.distributed as dist
     from pytorch_dppo_amd.parallel.dist import init_single_rank_collective
     from pytorch_dppo_amd.runtime.launcher import free_port
     from pytorch_dppo_amd.runtime.worker import DPPOWorker
@@ -508,53 +507,60 @@ def test_rccl_world1_allreduce_and_training_step():
         assert m["ep_count"] == ep[1]
         if ep[1] > 0:
             assert m["mean_ep_return"] == pytest.approx(ep[0] / ep[1])
+        assert ctx.native is not None          # the worker made the in-stream communicator
     finally:
-        dist.destroy_process_group()
+        ctx.destroy()
 
 
 @pytest.mark.parametrize("overlap", [False, True])
-def test_head_chains_through_rccl_bit_identical_to_fused(overlap, monkeypatch):
-    """Per-head chains with the collective path (policy all-reduce issued before the value kernel,
-    value all-reduce + Adam left pending into the next step — and with --overlap-rollout past
-    the next rollout) through the real RCCL call at world size 1 == the same chains without
-    collectives (DPPO_FUSED_APPLY=0): bit-identical parameters after 2 iterations; and == the
-    joint world-size-1 path (both heads' layers in one wgrad + one gather/Adam) to fp32
-    summation-order tolerance."""
-    import torch.distributed as dist
+@pytest.mark.parametrize("native", [False, True])
+def test_head_chains_through_rccl_bit_identical_to_fused(overlap, native, monkeypatch):
+    """The collective paths through the real RCCL call at world size 1.  Process-group RCCL
+    (DPPO_NATIVE_COMM=0): per-head chains (policy all-reduce issued before the value kernel, value
+    all-reduce + Adam left pending into the next step — and with --overlap-rollout past the next
+    rollout) == the same chains without collectives (DPPO_FUSED_APPLY=0), bit-identical after 2
+    iterations, and == the joint world-size-1 path (one wgrad + one gather/Adam) to fp32
+    summation-order tolerance.  Native in-stream RCCL (csrc/comm.cpp): the joint kernels, the
+    gather, the all-reduce and the whole-vector Adam == the joint world-size-1 path, bit for bit."""
     from pytorch_dppo_amd.parallel.dist import DistContext, init_single_rank_collective
     from pytorch_dppo_amd.runtime.launcher import free_port
     from pytorch_dppo_amd.runtime.worker import DPPOWorker
     monkeypatch.setenv("DPPO_HEADS", "1")
+    monkeypatch.setenv("DPPO_NATIVE_COMM", "1" if native else "0")
     kw = dict(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 8, batch_size=64 * 8,
               num_epoch=3, dtype="bf16x3", seed=3, overlap_rollout=overlap)
     wj = DPPOWorker(dppo_preset(**kw), DistContext(device=DEV))     # joint world-1 path
     for _ in range(2):
         wj.iteration_step()
-    monkeypatch.setenv("DPPO_FUSED_APPLY", "0")
-    w1 = DPPOWorker(dppo_preset(**kw), DistContext(device=DEV))
-    assert w1.engine.heads and len(w1.engine.buckets) == 2 and not w1.engine.can_fuse_apply()
-    for _ in range(2):
-        w1.iteration_step()
-    w1.flush_pending()
-    torch.cuda.synchronize()
-    rel = (w1.model.flat.data - wj.model.flat.data).norm() / wj.model.flat.data.norm()
-    assert rel.item() < 1e-5, rel.item()
+    ref = wj
+    if not native:
+        monkeypatch.setenv("DPPO_FUSED_APPLY", "0")
+        w1 = DPPOWorker(dppo_preset(**kw), DistContext(device=DEV))
+        assert w1.engine.heads and len(w1.engine.buckets) == 2 and not w1.engine.can_fuse_apply()
+        for _ in range(2):
+            w1.iteration_step()
+        w1.flush_pending()
+        torch.cuda.synchronize()
+        rel = (w1.model.flat.data - wj.model.flat.data).norm() / wj.model.flat.data.norm()
+        assert rel.item() < 1e-5, rel.item()
+        ref = w1
     ctx = init_single_rank_collective(DEV, port=free_port())
     ctx.force_collectives = True
     try:
         w2 = DPPOWorker(dppo_preset(**kw), ctx)
+        assert (ctx.native is not None) == native
         for _ in range(2):
             m = w2.iteration_step()
-        if overlap:
+        if overlap and not native:
             assert w2.engine._pending_value is not None   # the last value step waits for the rollout
             w2.flush_pending()
         assert w2.engine._pending_value is None
         torch.cuda.synchronize()
-        assert torch.equal(w1.model.flat.data, w2.model.flat.data)
-        assert torch.equal(w1.engine.adam_v, w2.engine.adam_v)
+        assert torch.equal(ref.model.flat.data, w2.model.flat.data)
+        assert torch.equal(ref.engine.adam_v, w2.engine.adam_v)
         assert math.isfinite(m["loss"]) and m["updates"] == 6
     finally:
-        dist.destroy_process_group()
+        ctx.destroy()
 
 
 @pytest.mark.parametrize("env_name,mb,dtype", [("Humanoid-v2", 512, "bf16x3"), ("Humanoid-v2", 200, "bf16x3"),
