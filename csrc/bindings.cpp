@@ -230,15 +230,27 @@ MlpArgs base_mlp(int dt, const Layout& L, const std::vector<double>& scales, tor
   return a;
 }
 
+// w8 (optional, fp8 mode with dt bf16): the e4m3 image the value head's fc1 reads with qscale
+void set_w8(MlpArgs& a, torch::Tensor w8, torch::Tensor qscale, const Layout& L) {
+  if (w8.defined() && w8.numel() > 0) {
+    check(w8, "w8", at::kByte, wimg_extent(L));
+    check(qscale, "qscale", at::kFloat, 6);
+    a.W8 = w8.data_ptr();
+    a.qscale = qscale.data_ptr<float>();
+  }
+}
+
 void mlp_value(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0, int64_t M, torch::Tensor wimg,
                std::vector<int64_t> layout, std::vector<double> scales, torch::Tensor flat, int64_t A,
-               torch::Tensor v_out, bool check_idx, torch::Tensor qscale) {
+               torch::Tensor v_out, bool check_idx, torch::Tensor qscale, torch::Tensor w8) {
   Layout L = parse_layout(layout);
   MlpArgs a = base_mlp((int)dt, L, scales, x_buf, idx, row0, M, wimg, flat, A, check_idx,
                        std::numeric_limits<int64_t>::max());
   check(v_out, "v_out", at::kFloat, M);
   a.v_out = v_out.data_ptr<float>();
   a.qscale = opt_scales(qscale);
+  TORCH_CHECK(!(w8.defined() && w8.numel() > 0) || dt == 1, "w8: the fp8 mode's bf16 value forward only");
+  set_w8(a, w8, qscale, L);
   launch_mlp_value((int)dt, a, cur_stream());
   after_launch(__func__);
 }
@@ -248,7 +260,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
                int64_t A, torch::Tensor actions, torch::Tensor logp_old, torch::Tensor adv, torch::Tensor ret,
                torch::Tensor v_old, torch::Tensor mu_prev, torch::Tensor v_prev, std::vector<int64_t> opts,
                std::vector<double> fopts, std::vector<torch::Tensor> tbufs, int64_t ldT, torch::Tensor part,
-               bool check_idx, bool xT_ready) {
+               bool check_idx, bool xT_ready, torch::Tensor w8, torch::Tensor qscale) {
   TORCH_CHECK(dt != 2, "the update runs in bf16 when dtype=fp8 (fp8 gradients underflow e4m3)");
   Layout L = parse_layout(layout);
   TORCH_CHECK(A > 0, "A");
@@ -316,6 +328,8 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
     a.tstamp_every = g_tstamp_every;
   }
   a.part = part.data_ptr<float>();
+  TORCH_CHECK(!(w8.defined() && w8.numel() > 0) || (dt == 1 && head >= 0), "w8: the fp8 mode's per-head bf16 update only");
+  set_w8(a, w8, qscale, L);
   if (head >= 0) {
     launch_mlp_head((int)dt, (int)head, a, cur_stream());
   } else {
@@ -482,9 +496,24 @@ void metrics_pack(torch::Tensor ep, torch::Tensor loss8, torch::Tensor norm_part
   after_launch(__func__);
 }
 
+// fp8 mode's shadow image (csrc/kernels.h F8Shadow): empty tensors = off
+F8Shadow f8_shadow(torch::Tensor img, torch::Tensor lid, torch::Tensor qs, int64_t n) {
+  F8Shadow f{nullptr, nullptr, nullptr};
+  if (img.defined() && img.numel() > 0) {
+    check(img, "f8_img", at::kByte, 1);
+    check(lid, "f8_lid", at::kInt, n);
+    check(qs, "f8_qscale", at::kFloat, 6);
+    f.img = img.data_ptr<uint8_t>();
+    f.lid = lid.data_ptr<int>();
+    f.qs = qs.data_ptr<float>();
+  }
+  return f;
+}
+
 void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, double lr, double b1, double b2,
           double eps, double max_norm, torch::Tensor state, torch::Tensor norm_part, torch::Tensor wimg,
-          torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul, int64_t host_step) {
+          torch::Tensor w_map, torch::Tensor wt_map, int64_t dt, torch::Tensor qmul, int64_t host_step,
+          torch::Tensor f8_img, torch::Tensor f8_lid, torch::Tensor f8_qs) {
   // host_step >= 1: the step number of this update (eager launch: one fused kernel when there is
   // no clipping); 0: read the device counter (graph replay)
   const int64_t n = p.numel();
@@ -504,7 +533,7 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, do
   launch_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (int)n, (float)lr,
               (float)b1, (float)b2, (float)eps, (float)max_norm, state.data_ptr<float>(), norm_part.data_ptr<float>(),
               nblk, wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q, (int)host_step,
-              cur_stream());
+              f8_shadow(f8_img, f8_lid, f8_qs, n), cur_stream());
   after_launch(__func__);
 }
 
@@ -516,7 +545,7 @@ void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
                  double scale, torch::Tensor loss_out, torch::Tensor g, torch::Tensor p, torch::Tensor m,
                  torch::Tensor v, double lr, double b1, double b2, double eps, int64_t step, torch::Tensor state,
                  torch::Tensor norm_part, torch::Tensor wimg, torch::Tensor w_map, torch::Tensor wt_map, int64_t dt,
-                 torch::Tensor qmul) {
+                 torch::Tensor qmul, torch::Tensor f8_img, torch::Tensor f8_lid, torch::Tensor f8_qs) {
   const int64_t n = p.numel();
   check(p, "p", at::kFloat, n);
   check(g, "g", at::kFloat, n);
@@ -546,7 +575,8 @@ void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
                      (int)nitems, (int)i_lo, (float)scale, loss_out.data_ptr<float>(), g.data_ptr<float>(),
                      p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (int)n, (float)lr, (float)b1,
                      (float)b2, (float)eps, (int)step, state.data_ptr<float>(), norm_part.data_ptr<float>(), nblk,
-                     wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q, cur_stream());
+                     wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q,
+                     f8_shadow(f8_img, f8_lid, f8_qs, n), cur_stream());
   after_launch(__func__);
 }
 

@@ -52,6 +52,7 @@ struct MlpArgs {
   int M;               // rows in this call (multiple of ROWS handled by masking)
   // packed weights (storage precision) + offsets (elements) of Wp / Wpt per layer
   const void* W;
+  const void* W8;        // fp8 mode: the e4m3 image (the value head's fc1, csrc/mlp_head.hip F8)
   int off_w[6];        // p1 p2 p3 v1 v2 v3 (forward images)
   int off_wt[6];       // transposed images (dgrad)
   int d_in[6];         // padded input width per layer
@@ -103,6 +104,14 @@ extern "C" void launch_mlp_head_value(int dt, const MlpArgs& a, hipStream_t s); 
 extern "C" void set_head_kernels(int enable);
 extern "C" int head_kernels_enabled();
 
+// fp8 mode: the Adam kernels also refresh the e4m3 image the update's fc1 reads (csrc/mlp_head.hip
+// F8), element i as p / qs[lid[i]] with the iteration's per-layer scales; img == nullptr: off
+struct F8Shadow {
+  uint8_t* img;
+  const int* lid;
+  const float* qs;
+};
+
 // reduce items per block of the gather kernels (common.h item_reduce)
 constexpr int ITEM_IPB = 32;
 inline __host__ __device__ int item_blocks(int nitems) { return (nitems + ITEM_IPB - 1) / ITEM_IPB; }
@@ -151,7 +160,7 @@ void set_adam_fused(int on);
 void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, float b1, float b2,
                  float eps, float max_norm, float* state, float* norm_part, int nblk,
                  void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale, int host_step,
-                 hipStream_t s);
+                 const F8Shadow& f8, hipStream_t s);
 // grad_gather (with the partials pass, range [A, n)) + no-clip Adam fused: world size 1 only
 // (no all-reduce between them); nblk = norm_part size, must exceed A + 8
 void launch_gather_adam(const float* slab, const int* src_off, const int* src_meta, const float* part, int npblk,
@@ -159,7 +168,7 @@ void launch_gather_adam(const float* slab, const int* src_off, const int* src_me
                         float* loss_out, float* g, float* p, float* m, float* v,
                         int n, float lr, float b1, float b2, float eps, int step, float* state, float* norm_part,
                         int nblk, void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale,
-                        hipStream_t s);
+                        const F8Shadow& f8, hipStream_t s);
 void launch_pack(const float* p, int n, void* wimg, const int* w_map, const int* wt_map, int dt,
                  const float* img_scale, hipStream_t s);
 // fp8 forward image: qscale[6] = per-layer amax / 416 of p (lid: layer of each parameter, -1

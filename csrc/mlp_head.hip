@@ -121,7 +121,6 @@ template <> struct HeadCfg<0> {   // policy: p_fc1 -> p_fc2 -> mu
   static constexpr int N1 = 8, N1R = 7;     // fc1 tiles held / real (100 features + the bias column)
   static constexpr int K2 = 4;              // fc2 k-steps (fc1 output padded to 128)
   static constexpr int N3 = 2;              // fc3 output tiles (A <= 32)
-  static constexpr int XS = 4;              // X ring slots (k-steps): 2 per stage, 2 ahead
   static constexpr int S3 = 2, SBF = 4;     // weight ring stages (split-bf16 / bf16: 64 KiB)
   static constexpr int NS4 = 2;             // dgrad fc2 stages (4 output tiles each)
   static constexpr int NEED = 1900;         // per-wave scratch floats: loss tile, partials, h2^T image
@@ -132,48 +131,63 @@ template <> struct HeadCfg<1> {   // value: v_fc1 -> v_fc2 -> v
   static constexpr int N1 = 32, N1R = 32;   // 500 features + the bias column: 32 tiles
   static constexpr int K2 = 16;
   static constexpr int N3 = 1;
-  static constexpr int XS = 2;              // 1 k-step per 2 stages, 1 k-step ahead
-  static constexpr int S3 = 3, SBF = 6;     // (96 KiB)
+  static constexpr int S3 = 3, SBF = 6;     // (96 KiB; F8: 4 stages, 64 KiB)
   static constexpr int NS4 = 8;
   static constexpr int NEED = 744;          // loss tile, partials, dW_v partials
 };
 
-template <int DT, int HEAD>
-constexpr int head_stages() { return DT == DT_S3 ? HeadCfg<HEAD>::S3 : HeadCfg<HEAD>::SBF; }
+// F8 (fp8 mode, value head, bf16 update): fc1 reads the e4m3 weight image and e4m3-rounded
+// observations (v_mfma_f32_16x16x32_fp8_fp8): a 1 KiB ring slot holds one tile's fragments of two
+// consecutive k-steps, so the fc1 stream and its LDS reads are half the bf16 bytes.
+template <int DT, int HEAD, bool F8 = false>
+constexpr int head_stages() { return DT == DT_S3 ? HeadCfg<HEAD>::S3 : (F8 ? 4 : HeadCfg<HEAD>::SBF); }
+// X ring slots (k-steps), a power of two.  An observation DMA must be OLDER than the weight batch
+// whose counted wait precedes its read, so it is issued >= S stream steps ahead: X(k + XS) is
+// issued when X(k) is read — policy 2 k-steps per step (XS / 2 >= S), value 2 steps per k-step
+// (2 XS >= S; F8: 1 step per k-step, XS >= S).
+template <int DT, int HEAD, bool F8 = false>
+constexpr int head_xs() { return HEAD == 0 ? (DT == DT_S3 ? 4 : 8) : (DT == DT_S3 ? 2 : 4); }
+template <int DT, int HEAD, bool F8 = false>
+constexpr int x_lead_steps() {
+  return HEAD == 0 ? head_xs<DT, HEAD, F8>() / 2 : (F8 ? 1 : 2) * head_xs<DT, HEAD, F8>();
+}
 template <int DT>
 constexpr int stage_bytes() { return NSLOT * HT<DT>::FB; }
 // per-wave scratch: the X ring (fc1), reused after fc1 for the loss tile and the partials
-template <int DT, int HEAD>
+template <int DT, int HEAD, bool F8 = false>
 constexpr int xr_floats() {
-  constexpr int x = HeadCfg<HEAD>::XS * HeadCfg<HEAD>::RB * HT<DT>::FB / 4;
+  constexpr int x = head_xs<DT, HEAD, F8>() * HeadCfg<HEAD>::RB * HT<DT>::FB / 4;
   return x > HeadCfg<HEAD>::NEED ? x : HeadCfg<HEAD>::NEED;
 }
-template <int DT, int HEAD>
-constexpr int ws_floats() { return xr_floats<DT, HEAD>() + HeadCfg<HEAD>::RB * TILE_F; }
-template <int DT, int HEAD>
+template <int DT, int HEAD, bool F8 = false>
+constexpr int ws_floats() { return xr_floats<DT, HEAD, F8>() + HeadCfg<HEAD>::RB * TILE_F; }
+template <int DT, int HEAD, bool F8 = false>
 constexpr size_t head_lds_bytes() {
-  return (size_t)head_stages<DT, HEAD>() * stage_bytes<DT>() +
-         (size_t)HeadCfg<HEAD>::NW * ws_floats<DT, HEAD>() * sizeof(float);
+  return (size_t)head_stages<DT, HEAD, F8>() * stage_bytes<DT>() +
+         (size_t)HeadCfg<HEAD>::NW * ws_floats<DT, HEAD, F8>() * sizeof(float);
 }
 template <int HEAD>
 constexpr int wrows() { return 16 * HeadCfg<HEAD>::RB; }
-template <int DT>
+template <int DT, bool F8 = false>
 constexpr bool head_lds_ok() {
-  return head_lds_bytes<DT, 0>() <= 160 * 1024 && head_lds_bytes<DT, 1>() <= 160 * 1024 &&
+  return head_lds_bytes<DT, 0>() <= 160 * 1024 && head_lds_bytes<DT, 1, F8>() <= 160 * 1024 &&
          // value: loss tile + partials + its 128 dW_v partials; policy: + the [64][20] h2^T image
-         wrows<1>() * SST + NPF + 32 + 128 <= xr_floats<DT, 1>() &&
+         wrows<1>() * SST + NPF + 32 + 128 <= xr_floats<DT, 1, F8>() &&
          ((wrows<0>() * SST + NPF + 32 + 3) & ~3) + 64 * 20 <= xr_floats<DT, 0>() &&
          // the dW_mu tiles of 4 waves go through the policy ring
-         4 * 32 * 128 * 4 <= head_stages<DT, 0>() * stage_bytes<DT>();
+         4 * 32 * 128 * 4 <= head_stages<DT, 0>() * stage_bytes<DT>() &&
+         // the observation DMAs lead the weight waits
+         x_lead_steps<DT, 0>() >= head_stages<DT, 0>() && x_lead_steps<DT, 1, F8>() >= head_stages<DT, 1, F8>();
 }
-static_assert(head_lds_ok<DT_S3>() && head_lds_ok<DT_BF16>(), "head kernel LDS carving");
+static_assert(head_lds_ok<DT_S3>() && head_lds_ok<DT_BF16>() && head_lds_ok<DT_BF16, true>(),
+              "head kernel LDS carving / observation lead");
 static_assert(HeadCfg<0>::NW * wrows<0>() == ROWS && HeadCfg<1>::NW * wrows<1>() == ROWS, "128 rows per workgroup");
 // loss scratch (after fc1, in the X ring): dL/dmu | dL/dv [rows][SST], then the wave's partials
 static_assert(wrows<0>() * 32 <= HeadCfg<0>::RB * TILE_F, "mu tile fits the transpose tiles");
 static_assert(HeadCfg<0>::NW == 8 && HeadCfg<0>::RB == 1, "the fused dW_mu reduction assumes 8 waves of 16 rows");
 
-template <int HEAD>
-DEV int fc1_stages(int ks1) { return HEAD == 0 ? (ks1 + 1) >> 1 : 2 * ks1; }
+template <int HEAD, bool F8 = false>
+DEV int fc1_stages(int ks1) { return HEAD == 0 ? (ks1 + 1) >> 1 : (F8 ? ks1 : 2 * ks1); }
 
 DEV int rot_ks(int ks, int rot, int ks1) {
   const int k = ks + rot;
@@ -183,10 +197,10 @@ DEV int rot_ks(int ks, int rot, int ks1) {
 // Ring slot q of stream step st: element offset of a weight fragment, or -1 (a slot no MFMA
 // reads; its DMA re-loads slot 0's fragment so every wave issues GL DMAs per step).  FWD (the
 // value forward): the stream ends with the fc3 stage.
-template <int HEAD, bool FWD>
+template <int HEAD, bool FWD, bool F8>
 DEV int step_src(const MlpArgs& a, int st, int q, int rot, int ks1) {
   using C = HeadCfg<HEAD>;
-  const int ns1 = fc1_stages<HEAD>(ks1), ns2 = C::K2 / 2;
+  const int ns1 = fc1_stages<HEAD, F8>(ks1), ns2 = C::K2 / 2;
   const int s_fc3 = ns1 + ns2, s_dg2 = s_fc3 + 1, s_end = FWD ? s_dg2 : s_dg2 + C::NS4;
   if (st >= s_end) st = s_end - 1;
   if (st < ns1) {
@@ -196,7 +210,9 @@ DEV int step_src(const MlpArgs& a, int st, int q, int rot, int ks1) {
       t = q & 7;
       if (t >= C::N1R || ks >= ks1) return -1;
     } else {
-      ks = st >> 1;
+      // (F8: the slot's first k-step of a pair 2j, 2j + 1 — contiguous in the e4m3 image; rot and
+      // ks1 even keep the pair contiguous after the rotation)
+      ks = F8 ? (st & ~1) : st >> 1;
       t = 16 * (st & 1) + q;
     }
     return a.off_w[C::L1] + (int)fm_frag(t, rot_ks(ks, rot, ks1), a.d_in[C::L1], 0);
@@ -362,21 +378,22 @@ DEV float xsum(float x) {   // sum over the lanes that differ only in the bits o
 // FWD (value head only): the forward alone, V(x) of rows [row0, row0 + M) into v_out — the GAE
 // input pass (train.py:87,109-112) at the update kernel's 128 rows per weight stream instead of
 // mlp.hip's 32-row value kernel
-template <int DT, int HEAD, bool FWD = false>
+template <int DT, int HEAD, bool FWD = false, bool F8 = false>
 __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
   static_assert(!FWD || HEAD == 1, "forward mode is the value head's");
+  static_assert(!F8 || (HEAD == 1 && DT == DT_BF16), "the e4m3 fc1 is the bf16 value head's");
   using C = HeadCfg<HEAD>;
   using H = HT<DT>;
   using P = typename H::P;
   using T = typename P::T;
   using Frag = typename H::Frag;
   constexpr int FB = H::FB, SB = stage_bytes<DT>();
-  constexpr int S = head_stages<DT, HEAD>(), XS = C::XS;
+  constexpr int S = head_stages<DT, HEAD, F8>(), XS = head_xs<DT, HEAD, F8>();
   constexpr int NW = C::NW, RB = C::RB, WROWS = 16 * RB;
   constexpr int SPW = NSLOT / NW, GL = H::NI * SPW;   // ring slots / DMA instructions per wave per stage
   constexpr int XDMA = H::NI * RB;                    // DMA instructions of one wave's X fragments of a k-step
   constexpr int TPR = 64 / WROWS;                     // loss lanes per row
-  constexpr int WS_F = ws_floats<DT, HEAD>();
+  constexpr int WS_F = ws_floats<DT, HEAD, F8>();
   constexpr int MPP = DT == DT_S3 ? 3 : 1;            // MFMAs per fragment product
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const int tid = threadIdx.x, lane = tid & 63;
@@ -385,11 +402,11 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   const int m0 = blockIdx.x * ROWS;
   const int A = a.A;
   const int ks1 = a.d_in[0] >> 5;
-  const int ns1 = fc1_stages<HEAD>(ks1);
+  const int ns1 = fc1_stages<HEAD, F8>(ks1);
   char* ring = smem;
   float* scr = reinterpret_cast<float*>(smem + (size_t)S * SB) + wave * WS_F;
   char* xring = reinterpret_cast<char*>(scr);
-  float* tpb = scr + xr_floats<DT, HEAD>();   // RB transpose tiles [16][SST]
+  float* tpb = scr + xr_floats<DT, HEAD, F8>();   // RB transpose tiles [16][SST]
   float* dml = scr;                        // (after fc1) dL/dmu [32][SST] | dL/dv column 32
   float* wpart = scr + WROWS * SST;        // (after fc1) [8 loss terms | 32 dlog_std]
   float* mus = tpb;                        // (loss) mu [32][32] | v [32]
@@ -439,16 +456,19 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   for (int rb = 0; rb < RB; ++rb)
     xsrc[rb] = reinterpret_cast<const char*>(a.x_buf) +
                (size_t)src_of(WROWS * wave + 16 * rb + lr) * (size_t)a.d_in[0] * sizeof(T) + H::xlane(lane);
-  const int rot = (int)(blockIdx.x % (unsigned)ks1);
+  // (F8: an even rotation keeps each fc1 k-step pair contiguous; the launcher checks ks1 even)
+  const int rot = F8 ? 2 * (int)(blockIdx.x % (unsigned)(ks1 >> 1)) : (int)(blockIdx.x % (unsigned)ks1);
   auto code16 = [&](int st, int q) __attribute__((always_inline)) {
-    int c = step_src<HEAD, FWD>(a, st, q, rot, ks1);
-    if (c < 0) c = step_src<HEAD, FWD>(a, st, 0, rot, ks1);
+    int c = step_src<HEAD, FWD, F8>(a, st, q, rot, ks1);
+    if (c < 0) c = step_src<HEAD, FWD, F8>(a, st, 0, rot, ks1);
     if (c < 0) c = a.off_w[C::L1];
     return (uint32_t)(c >> 9);
   };
   const uint32_t cw0 = code16(lane, SPW * wave) | (code16(lane, SPW * wave + 1) << 16);
   const uint32_t cw1 = SPW > 2 ? code16(lane, SPW * wave + 2) | (code16(lane, SPW * wave + 3) << 16) : 0u;
 
+  __amdgpu_buffer_rsrc_t rw8 = rw;
+  if constexpr (F8) rw8 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W8), (short)0, 0x7fffffff, 0x00020000);
   auto issue = [&](int st, int stage) __attribute__((always_inline)) {
     const int l = min(st, MAX_STEPS - 1);
     const uint32_t w01 = __builtin_amdgcn_readlane(cw0, l);
@@ -458,9 +478,14 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
     for (int u = 0; u < SPW; ++u) {
       const uint32_t code = ((u < 2 ? w01 : w23) >> (16 * (u & 1))) & 0xffffu;
+      if (F8 && st < ns1) {   // fc1: two e4m3 fragments (512 B each) of the tile per slot
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw8, stg + u * FB, 16, vw, code * 512u, 0, 0);
+      } else {
 #pragma unroll
-      for (int h = 0; h < H::NI; ++h)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB + 1024 * h, 16, vw, code * (unsigned)FB + 1024u * h, 0, 0);
+        for (int h = 0; h < H::NI; ++h)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, stg + u * FB + 1024 * h, 16, vw, code * (unsigned)FB + 1024u * h,
+                                                   0, 0);
+      }
     }
   };
   // this wave's RB observation fragments of fc1 k-step ks into X ring slot ks % XS
@@ -554,7 +579,44 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     store_T8<DT>(a.xT, tp, SST, lane >> 1, lane & 1, 32 * rot_ks(ks, rot, ks1) + (lane >> 1),
              mw + 16 * rb + 8 * (lane & 1), a.ldT);
   };
-  if constexpr (HEAD == 1) {
+  if constexpr (F8) {
+    // e4m3 fc1: per k-step pair 2 stages (tiles 0-15, 16-31), each slot one tile's two fragments;
+    // the observation fragments (bf16 in the X ring) rounded to e4m3 in registers
+    auto to_f8 = [&](const Frag& x) __attribute__((always_inline)) -> long {
+      const f32x8 v = H::to8(x);
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], hi, true);
+      return (long)(((unsigned long)(unsigned)hi << 32) | (unsigned)lo);
+    };
+    long xq0 = 0, xq1 = 0;
+    for (int j = 0; j < (ks1 >> 1); ++j) {
+      static_for<0, 2>([&](auto sc) __attribute__((always_inline)) {
+        constexpr int sub = decltype(sc)::value;
+        stg = wait_step(sub == 1 ? 2 * XDMA : 0);
+        if constexpr (sub == 0) {
+          xq0 = to_f8(read_x(2 * j, 0));
+          xq1 = to_f8(read_x(2 * j + 1, 0));
+        }
+        const char* base = stg + 8 * lane;
+        static_for<0, 16>([&](auto qc) __attribute__((always_inline)) {
+          constexpr int q = decltype(qc)::value;
+          const long w0 = *reinterpret_cast<const long*>(base + q * FB);
+          const long w1 = *reinterpret_cast<const long*>(base + q * FB + 512);
+          acc1[0][16 * sub + q] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(xq0, w0, acc1[0][16 * sub + q], 0, 0, 0);
+          acc1[0][16 * sub + q] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(xq1, w1, acc1[0][16 * sub + q], 0, 0, 0);
+        });
+        if constexpr (sub == 0) {   // into the slots X[2j], X[2j + 1] just left
+          issue_x(2 * j + XS);
+          issue_x(2 * j + 1 + XS);
+        }
+      });
+    }
+    const float s1 = a.qscale[C::L1];   // the e4m3 image holds W1 / qscale
+#pragma unroll
+    for (int t = 0; t < C::N1; ++t) acc1[0][t] *= s1;
+  } else if constexpr (HEAD == 1) {
     Frag xa[RB];
     for (int ks = 0; ks < ks1; ++ks) {
       static_for<0, 2>([&](auto sc) __attribute__((always_inline)) {
@@ -569,7 +631,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) acc1[rb][t] = P::mma(acc1[rb][t], xa[rb], b);
           });
-        if constexpr (sub == 0) issue_x(ks + 2);   // into the slot X[ks] just left
+        if constexpr (sub == 0) issue_x(ks + XS);   // into the slot X[ks] just left
       });
       if (ks == 1) HD_STAMP(8);
       if (ks == 5) HD_STAMP(9);
@@ -604,8 +666,8 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
           if (two) put_xT(xb[rb], kb, rb);
         }
       }
-      issue_x(ka + 4);   // into the slots X[ka], X[kb] just left
-      issue_x(kb + 4);
+      issue_x(ka + XS);   // into the slots X[ka], X[kb] just left
+      issue_x(kb + XS);
       if (st == 0) HD_STAMP(8);
       if (st == 3) HD_STAMP(9);
     }
@@ -1104,13 +1166,26 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   }   // !FWD
 }
 
+template <int DT, int HEAD, bool FWD = false, bool F8 = false>
+void head_launch_t(const MlpArgs& a, hipStream_t s) {
+  const size_t lds = head_lds_bytes<DT, HEAD, F8>();
+  set_max_lds_once<mlp_head_kernel<DT, HEAD, FWD, F8>>(lds);
+  const int nblk = (a.M + ROWS - 1) / ROWS;
+  hipLaunchKernelGGL((mlp_head_kernel<DT, HEAD, FWD, F8>), dim3(nblk), dim3(HeadCfg<HEAD>::NW * 64), lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
+// the value head in fp8 mode (a.W8: the e4m3 image, a.qscale its per-layer scales) takes the
+// e4m3 fc1 when the k-steps pair up (d_in a multiple of 64)
 template <int DT, int HEAD, bool FWD = false>
 void head_launch(const MlpArgs& a, hipStream_t s) {
-  const size_t lds = head_lds_bytes<DT, HEAD>();
-  set_max_lds_once<mlp_head_kernel<DT, HEAD, FWD>>(lds);
-  const int nblk = (a.M + ROWS - 1) / ROWS;
-  hipLaunchKernelGGL((mlp_head_kernel<DT, HEAD, FWD>), dim3(nblk), dim3(HeadCfg<HEAD>::NW * 64), lds, s, a);
-  HIP_CHECK_LAUNCH();
+  if constexpr (DT == DT_BF16 && HEAD == 1) {
+    if (a.W8 != nullptr && a.qscale != nullptr && ((a.d_in[0] >> 5) & 1) == 0) {
+      head_launch_t<DT, HEAD, FWD, true>(a, s);
+      return;
+    }
+  }
+  head_launch_t<DT, HEAD, FWD>(a, s);
 }
 
 int g_head_enable = 1;

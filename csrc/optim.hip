@@ -171,6 +171,16 @@ DEV float adam_elem(float& m, float& v, float p, float gi, float b1, float b2, f
   return p - step_size * mi / fmaf(sqrtf(vi), rbc2, eps);
 }
 
+// fp8 mode: the e4m3 image the update's fc1 reads, refreshed with every Adam step (scale: the
+// iteration's per-layer qscale, as pack_fp8_kernel; e4m3 conversion saturates)
+DEV void f8_put(const F8Shadow& f8, int i, int wi, int wti, float pi) {
+  if (f8.img != nullptr) {
+    const uint8_t q = Prec<DT_FP8>::cvt(__fdiv_rn(pi, f8.qs[f8.lid[i]]));
+    f8.img[wi] = q;
+    f8.img[wti] = q;
+  }
+}
+
 template <int DT>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int n, float lr,
@@ -178,7 +188,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
                                                    float* __restrict__ state, const float* __restrict__ part,
                                                    int nblk, typename Prec<DT>::T* __restrict__ wimg,
                                                    const int* __restrict__ w_map, const int* __restrict__ wt_map,
-                                                   const float* __restrict__ qmul) {
+                                                   const float* __restrict__ qmul, F8Shadow f8) {
   using P = Prec<DT>;
   __shared__ float red[256];
   float s = 0.f;
@@ -208,6 +218,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
       const float q = qmul ? pi * qmul[i] : pi;
       P::put(wimg, wi, q);
       P::put(wimg, wt_map[i], q);
+      f8_put(f8, i, wi, wt_map[i], pi);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -230,7 +241,7 @@ __global__ __launch_bounds__(256) void adam_noclip_kernel(float* __restrict__ p,
                                                           typename Prec<DT>::T* __restrict__ wimg,
                                                           const int* __restrict__ w_map,
                                                           const int* __restrict__ wt_map,
-                                                          const float* __restrict__ qmul) {
+                                                          const float* __restrict__ qmul, F8Shadow f8) {
   using P = Prec<DT>;
   const float bc1 = 1.f - powf(b1, step);
   const float bc2 = 1.f - powf(b2, step);
@@ -250,6 +261,7 @@ __global__ __launch_bounds__(256) void adam_noclip_kernel(float* __restrict__ p,
       const float q = qmul ? pi * qmul[i] : pi;
       P::put(wimg, wi, q);
       P::put(wimg, wt_map[i], q);
+      f8_put(f8, i, wi, wt_map[i], pi);
     }
   }
   __shared__ float red[256];
@@ -283,7 +295,7 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
     float* __restrict__ g, float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, int n, float lr,
     float b1, float b2, float eps, float step, float* __restrict__ state, float* __restrict__ norm_part,
     typename Prec<DT>::T* __restrict__ wimg, const int* __restrict__ w_map, const int* __restrict__ wt_map,
-    const float* __restrict__ qmul) {
+    const float* __restrict__ qmul, F8Shadow f8) {
   using P = Prec<DT>;
   __shared__ float red[256];
   const float bc1 = 1.f - powf(b1, step);
@@ -304,6 +316,7 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
       const float q = qmul ? pi * qmul[i] : pi;
       P::put(wimg, wi, q);
       P::put(wimg, wt_map[i], q);
+      f8_put(f8, i, wi, wt_map[i], pi);
     }
   };
   if ((int)blockIdx.x < nrb) {
@@ -518,37 +531,37 @@ extern "C" void set_adam_fused(int on) { g_adam_fused = on; }
 extern "C" void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, float b1, float b2,
                             float eps, float max_norm, float* state, float* norm_part, int nblk, void* wimg,
                             const int* w_map, const int* wt_map, int dt, const float* img_scale, int host_step,
-                            hipStream_t s) {
+                            const F8Shadow& f8, hipStream_t s) {
   if (max_norm <= 0.f && g_adam_fused && host_step > 0) {
     const float step = (float)host_step;
     if (dt == DT_F32)
       hipLaunchKernelGGL(adam_noclip_kernel<DT_F32>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
-                         step, state, norm_part, (float*)wimg, w_map, wt_map, img_scale);
+                         step, state, norm_part, (float*)wimg, w_map, wt_map, img_scale, f8);
     else if (dt == DT_BF16)
       hipLaunchKernelGGL(adam_noclip_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
-                         step, state, norm_part, (__bf16*)wimg, w_map, wt_map, img_scale);
+                         step, state, norm_part, (__bf16*)wimg, w_map, wt_map, img_scale, f8);
     else if (dt == DT_S3)
       hipLaunchKernelGGL(adam_noclip_kernel<DT_S3>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
-                         step, state, norm_part, (S3Slot*)wimg, w_map, wt_map, img_scale);
+                         step, state, norm_part, (S3Slot*)wimg, w_map, wt_map, img_scale, f8);
     else
       hipLaunchKernelGGL(adam_noclip_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
-                         step, state, norm_part, (uint8_t*)wimg, w_map, wt_map, img_scale);
+                         step, state, norm_part, (uint8_t*)wimg, w_map, wt_map, img_scale, f8);
     HIP_CHECK_LAUNCH();
     return;
   }
   hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, s, g, n, norm_part, state);
   if (dt == DT_F32)
     hipLaunchKernelGGL(adam_kernel<DT_F32>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
-                       state, norm_part, nblk, (float*)wimg, w_map, wt_map, img_scale);
+                       state, norm_part, nblk, (float*)wimg, w_map, wt_map, img_scale, f8);
   else if (dt == DT_BF16)
     hipLaunchKernelGGL(adam_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
-                       state, norm_part, nblk, (__bf16*)wimg, w_map, wt_map, img_scale);
+                       state, norm_part, nblk, (__bf16*)wimg, w_map, wt_map, img_scale, f8);
   else if (dt == DT_S3)
     hipLaunchKernelGGL(adam_kernel<DT_S3>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
-                       state, norm_part, nblk, (S3Slot*)wimg, w_map, wt_map, img_scale);
+                       state, norm_part, nblk, (S3Slot*)wimg, w_map, wt_map, img_scale, f8);
   else
     hipLaunchKernelGGL(adam_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, max_norm,
-                       state, norm_part, nblk, (uint8_t*)wimg, w_map, wt_map, img_scale);
+                       state, norm_part, nblk, (uint8_t*)wimg, w_map, wt_map, img_scale, f8);
   HIP_CHECK_LAUNCH();
 }
 
@@ -557,22 +570,23 @@ extern "C" void launch_gather_adam(const float* slab, const int* src_off, const 
                                    int i_lo, float scale, float* loss_out, float* g, float* p,
                                    float* m, float* v, int n, float lr, float b1, float b2, float eps, int step,
                                    float* state, float* norm_part, int nblk, void* wimg, const int* w_map,
-                                   const int* wt_map, int dt, const float* img_scale, hipStream_t s) {
+                                   const int* wt_map, int dt, const float* img_scale, const F8Shadow& f8,
+                                   hipStream_t s) {
 #define GA_ARGS slab, src_off, src_meta, part, npblk, npart, red_col, red_dst, nitems, i_lo, scale, loss_out, g, p, m, \
                 v, n, lr, b1, b2, eps, \
                 (float)step, state, norm_part
   if (dt == DT_F32)
     hipLaunchKernelGGL(gather_adam_kernel<DT_F32>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (float*)wimg, w_map, wt_map,
-                       img_scale);
+                       img_scale, f8);
   else if (dt == DT_BF16)
     hipLaunchKernelGGL(gather_adam_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (__bf16*)wimg, w_map,
-                       wt_map, img_scale);
+                       wt_map, img_scale, f8);
   else if (dt == DT_S3)
     hipLaunchKernelGGL(gather_adam_kernel<DT_S3>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (S3Slot*)wimg, w_map,
-                       wt_map, img_scale);
+                       wt_map, img_scale, f8);
   else
     hipLaunchKernelGGL(gather_adam_kernel<DT_FP8>, dim3(nblk), dim3(256), 0, s, GA_ARGS, (uint8_t*)wimg, w_map,
-                       wt_map, img_scale);
+                       wt_map, img_scale, f8);
 #undef GA_ARGS
   HIP_CHECK_LAUNCH();
 }

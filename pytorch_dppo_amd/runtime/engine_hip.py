@@ -225,6 +225,7 @@ class HipEngine:
         self.key_action = rng.base_key(params.seed, rng.STREAM_ACTION, action_rank)
         self.empty = torch.empty(0, dtype=torch.int32, **dev)
         self.no_q = torch.empty(0, **f32)
+        self.no_u8 = torch.empty(0, dtype=torch.uint8, **dev)
         self._first_step = True
         self._loss_dev: Optional[torch.Tensor] = None
         self.local_stats: Optional[RunningObsStats] = None
@@ -354,6 +355,17 @@ class HipEngine:
         src[src < 0] = 0  # reduce items (log_std, and with the per-head kernels mu / v)
         self.src_off = src.to(torch.int32).to(self.device)
         self.src_meta = meta.to(torch.int32).to(self.device)
+
+    def _w8(self):
+        """fp8 mode: (e4m3 image, per-layer scales) for the value head's e4m3 fc1; else off"""
+        return (self.wimg_fwd, self.qscale) if self.fp8 else (self.no_u8, self.no_q)
+
+    def _f8(self, lo: int = 0, hi: Optional[int] = None):
+        """fp8 mode: the Adam kernels' shadow e4m3 image (the update's fc1 reads it, csrc/mlp_head.hip
+        F8) — (image, per-element layer id of the flat slice [lo, hi), per-layer scales); else off"""
+        if not self.fp8:
+            return (self.no_u8, self.empty, self.no_q)
+        return (self.wimg_fwd, self.layer_id[lo:hi], self.qscale)
 
     def _reduce_items(self, model: ActorCritic) -> Dict[str, tuple]:
         """Reduce items of the gather launches: (partial-row column, destination) pairs, the
@@ -607,8 +619,14 @@ class HipEngine:
     @torch.no_grad()
     def values(self) -> None:
         M = (self.T + 1) * self.E
-        self.ext.mlp_value(self.dt_fwd, self.x_buf, self.empty, 0, M, self.wimg_fwd, self.layout, self.scales,
-                           self.model.flat.data, self.A, self.values_buf, False, self.qscale)
+        if self.fp8 and self.heads:
+            # fp8 mode on the per-head path: the value head's streaming forward with the e4m3 fc1
+            # (fc2 / fc3 on the bf16 image; csrc/mlp_head.hip F8)
+            self.ext.mlp_value(self.dt, self.x_buf, self.empty, 0, M, self.wimg, self.layout, self.scales,
+                               self.model.flat.data, self.A, self.values_buf, False, self.qscale, self.wimg_fwd)
+        else:
+            self.ext.mlp_value(self.dt_fwd, self.x_buf, self.empty, 0, M, self.wimg_fwd, self.layout, self.scales,
+                               self.model.flat.data, self.A, self.values_buf, False, self.qscale, self.no_u8)
         if self.p.compat:
             # Q8 (train.py:109-112, ppo.py:119-122): the reference bootstraps R = V(s_T) from the
             # RAW, un-normalised last state.  Rows [T*E, (T+1)*E) of values_buf get V of the env's
@@ -622,7 +640,7 @@ class HipEngine:
             self.x_raw.copy_(self.encode(xr))
             self.ext.mlp_value(self.dt_fwd, self.x_raw, self.empty, 0, self.E, self.wimg_fwd, self.layout,
                                self.scales, self.model.flat.data, self.A, self.values_buf[self.N:], False,
-                               self.qscale)
+                               self.qscale, self.no_u8)
 
     @torch.no_grad()
     def gae(self) -> None:
@@ -757,15 +775,23 @@ class HipEngine:
         self.ext.mlp_train(self.dt, self.x_buf, idx_t, 0, M, self.wimg, self.layout, self.scales,
                            self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
                            self.ret, self.values_buf, self.mu_prev, self.v_prev, opts,
-                           [float(p.clip), float(p.ent_coeff)], self.tbufs, self.ldT, part, False, xt_ready)
+                           [float(p.clip), float(p.ent_coeff)], self.tbufs, self.ldT, part, False, xt_ready,
+                           *self._w8())
         if h == 0 and p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])   # train.py:164, before Adam moves it
+
+    def _joint_heads(self, idx_t, first: bool, xt_ready: bool) -> None:
+        """both head kernels into the shared partial buffer (disjoint columns and operands), in
+        stream order.  (Measured: the policy kernel on a side stream concurrent with the value
+        kernel, joined before the wgrad: 4.57 vs 4.39 ms per iteration, same box — each kernel
+        fills a CU's LDS, so they only time-slice the CUs and the stream hand-offs are extra.)"""
+        for h in (0, 1):
+            self._head_kernel(h, idx_t, first, xt_ready, self.part_joint, self.part_dw_joint[h])
 
     def _joint_grad(self, idx_t, first: bool, xt_ready: bool) -> None:
         """both head kernels (one shared partial buffer), ONE wgrad over both heads' layers, ONE
         gather of the whole gradient into grad_flat (no optimizer step)"""
-        for h in (0, 1):
-            self._head_kernel(h, idx_t, first, xt_ready, self.part_joint, self.part_dw_joint[h])
+        self._joint_heads(idx_t, first, xt_ready)
         b = self.joint_bucket
         self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
                        b["tasks_host"], b["slab"])
@@ -778,8 +804,7 @@ class HipEngine:
         """world size 1: policy kernel, value kernel (one shared partial buffer), ONE wgrad over
         both heads' layers, ONE gather + Adam launch over the whole flat vector"""
         p, M = self.p, self.mb
-        for h in (0, 1):
-            self._head_kernel(h, idx_t, first, xt_ready, self.part_joint, self.part_dw_joint[h])
+        self._joint_heads(idx_t, first, xt_ready)
         b = self.joint_bucket
         self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
                        b["tasks_host"], b["slab"])
@@ -790,7 +815,7 @@ class HipEngine:
                              rc, rd, self.A, 1.0 / M, self.loss_sums, self.grad_flat, self.model.flat.data,
                              self.adam_m, self.adam_v, float(p.lr), float(b1), float(b2), float(p.adam_eps),
                              self.adam_step + 1, self.adam_state, self.norm_part[:self.norm_n_whole], self.wimg,
-                             self.w_map, self.wt_map, self.dt, self.no_q)
+                             self.w_map, self.wt_map, self.dt, self.no_q, *self._f8())
         self.adam_step += 1
         self._norm_n = self.norm_n_whole
 
@@ -816,7 +841,7 @@ class HipEngine:
         self.ext.adam(self.model.flat.data[lo:hi], self.grad_flat[lo:hi], self.adam_m[lo:hi], self.adam_v[lo:hi],
                       float(p.lr), float(b1), float(b2), float(p.adam_eps), 0.0, self.adam_state,
                       self.norm_part[r0:r1], self.wimg, self.w_map[lo:hi], self.wt_map[lo:hi], self.dt, self.no_q,
-                      step_no)
+                      step_no, *self._f8(lo, hi))
 
     def grad(self, idx: Optional[torch.Tensor], apply: bool = False) -> None:
         """one minibatch gradient into grad_flat (no optimizer step; tests / the whole-vector
@@ -850,7 +875,7 @@ class HipEngine:
         self.ext.mlp_train(self.dt, self.x_buf, idx_t, 0, M, self.wimg, self.layout, self.scales,
                            self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
                            self.ret, self.values_buf, self.mu_prev, self.v_prev, opts, fopts, self.tbufs,
-                           self.ldT, self.part, False, xt_ready)
+                           self.ldT, self.part, False, xt_ready, self.no_u8, self.no_q)
         b = self.buckets[0]
         self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
                        b["tasks_host"], b["slab"])
@@ -864,7 +889,7 @@ class HipEngine:
                                  self.model.flat.data, self.adam_m, self.adam_v, float(p.lr), float(b1),
                                  float(b2), float(p.adam_eps), self.adam_step + 1, self.adam_state,
                                  self.norm_part[:self.norm_n_whole], self.wimg, self.w_map, self.wt_map, self.dt,
-                                 self.no_q)
+                                 self.no_q, *self._f8())
             return
         rc, rd = self.items["legacy"]
         self.ext.grad_gather(b["slab"], self.src_off, self.src_meta, self.part, self.ntrain_blk, self.npart,
@@ -911,7 +936,7 @@ class HipEngine:
         self._launch(("adam",), lambda: self.ext.adam(
             self.model.flat.data, self.grad_flat, self.adam_m, self.adam_v, float(p.lr), float(b1), float(b2),
             float(p.adam_eps), mx, self.adam_state, self.norm_part[:self.norm_n_whole], self.wimg, self.w_map,
-            self.wt_map, self.dt, self.no_q, host_step))
+            self.wt_map, self.dt, self.no_q, host_step, *self._f8()))
         self.adam_step += 1
         self._norm_n = self.norm_n_whole
         return None

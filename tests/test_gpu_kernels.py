@@ -973,6 +973,54 @@ def test_fp8_device_refresh_matches_torch_quantisation():
     assert same > 0.9999 and torch.equal(eng.wimg_fwd[w_map], eng.wimg_fwd[wt_map]), same
 
 
+def test_fp8_update_per_layer_error_and_shadow_image():
+    """fp8 mode (BASELINE config 5) on the per-head path: the value head's fc1 runs on the e4m3
+    MFMA (csrc/mlp_head.hip F8: e4m3 weight image x e4m3-rounded observations), in the update and
+    in values().  Per-layer relative error of the gradient vs fp32 autograd on the fp32 rows, the
+    value forward vs the fp32 model, and the shadow e4m3 image the Adam step refreshes (== torch's
+    float8_e4m3fn rounding of p / qscale for the new parameters)."""
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=1024, exploration_size=1024 * 16,
+                    batch_size=1024 * 16, dtype="fp8", ent_coeff=0.01)
+    eng, model, _, _ = _engine(p)
+    assert eng.fp8 and eng.heads
+    eng.refresh_fwd_image()
+    _fill_buffer(eng, model, gen_seed=7)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x = torch.randn(eng.N + eng.E, model.num_inputs, generator=g).clamp(-5, 5).to(DEV)
+    # value forward (fp8 fc1) vs the fp32 model on the fp32 rows
+    eng.values()
+    with torch.no_grad():
+        _, _, v32 = model(x)
+    verr = (eng.values_buf - v32.reshape(-1)).abs().max().item() / v32.abs().max().item()
+    # gradient vs fp32 autograd on the fp32 rows
+    eng.begin_update()
+    eng.grad(None)
+    model.flat.grad = None
+    mu, ls, v = model(x[:eng.N])
+    out = oracle.ppo_loss(mu, ls, v, eng.actions, eng.logp, eng.adv, eng.ret, eng.values_buf[:eng.N],
+                          clip=p.clip, ent_coeff=p.ent_coeff, value_loss=p.value_loss, convention=p.std_convention)
+    out["loss"].backward()
+    g_ref = model.flat.grad.detach().clone()
+    errs = {}
+    for name in ("p_fc1", "p_fc2", "mu", "v_fc1", "v_fc2", "v"):
+        o, n = model.offsets[f"{name}.weight"]
+        errs[name] = (eng.grad_flat[o:o + n] - g_ref[o:o + n]).norm().item() / (g_ref[o:o + n].norm().item() + 1e-12)
+    print("fp8 value forward max rel err", verr, "per-layer gradient rel err", errs)
+    assert verr < 0.05, verr
+    for name, e in errs.items():
+        assert e < (0.06 if name.startswith(("p_", "mu")) else 0.12), (name, e)
+    # the Adam step refreshes the e4m3 shadow image with the iteration's scales
+    eng.apply()
+    L = model.packed_layout()
+    lid = eng.layer_id.long()
+    sel = lid >= 0
+    q = (model.flat.data[sel] / eng.qscale[lid[sel]]).to(torch.float8_e4m3fn).view(torch.uint8)
+    w_map = L.flat_to_w.to(DEV).long()[sel]
+    wt_map = L.flat_to_wt.to(DEV).long()[sel]
+    same = (eng.wimg_fwd[w_map] == q).float().mean().item()
+    assert same > 0.9999 and torch.equal(eng.wimg_fwd[w_map], eng.wimg_fwd[wt_map]), same
+
+
 @pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
 def test_update_reads_rows_past_2gib_of_the_observation_buffer(dtype):
     """A Humanoid buffer of 65,536 envs x 22 (44 at bf16) steps (x_buf 2.3 GB): a minibatch whose
