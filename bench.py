@@ -109,8 +109,6 @@ def main():
     ap.add_argument("--batch-size", type=int, default=0, help="0 = full buffer (reference DPPO)")
     ap.add_argument("--overlap-rollout", action="store_true",
                     help="the last value-head all-reduce + Adam overlap the next rollout (exact: the rollout reads only the policy)")
-    ap.add_argument("--graphs", action="store_true",
-                    help="replay the per-minibatch launch chains as hipGraphs (use_graphs)")
     ap.add_argument("--force-collectives", action="store_true",
                     help="diagnostics: run the hot-path RCCL collectives even at world size 1")
     ap.add_argument("--phase-timing", type=int, default=0,
@@ -145,7 +143,6 @@ def main():
         p = dppo_preset(device="gpu", env_name=args.env_name, num_envs=E, exploration_size=rows,
                         batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=dtype,
                         num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
-                        use_graphs=args.graphs,
                         phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
         w = DPPOWorker(p, ctx)
         m = {}
@@ -206,7 +203,7 @@ def main():
                           "rccl_world_size": (dist.get_world_size() if dist.is_initialized()
                                               and ctx.backend == "nccl" else 0),
                           "rollout_len": T, "num_epoch": args.num_epoch,
-                          "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout, "graphs": args.graphs,
+                          "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout,
                           "per_head_kernels": heads, "grad_allreduce": grad_ar,
                           "note": ("value = total env steps/s of all n_gpus workers (one DPPO worker per GPU); "
                                    "the 8-worker node figure of the metric is the n_gpus=8 run; vs_baseline "

@@ -73,7 +73,6 @@ class Params:
     # head's last step stays pending until after the next rollout (which reads only the policy:
     # exact); CPU engine: the whole last step (option b, a 1-update policy lag)
     overlap_rollout: bool = False
-    use_graphs: bool = False             # replay the per-minibatch launch chains as hipGraphs (GPU engine)
     dist_timeout_s: float = 300.0
     verify_sync_every: int = 0           # debug param-checksum all-reduce period
     adam_betas: tuple = (0.9, 0.999)

@@ -238,11 +238,6 @@ class HipEngine:
                                 and params.obs_norm_update == "rollout")
         self._xT_valid = False   # True once a rollout wrote x^T for the current buffer contents
         self.s12 = torch.zeros(2, O, dtype=torch.float64, **dev)
-        # hipGraph replay of the per-minibatch launch chains (see _launch)
-        self.use_graphs = bool(params.use_graphs)
-        self._graphs: Dict = {}
-        self._graph_warm: set = set()
-        self._capture_stream = torch.cuda.Stream(device=device) if self.use_graphs else None
         stats.device_merge = self._device_merge
         # host-stepped env (--env-backend gym): no in-kernel dynamics; rollout() takes the host
         # path (_rollout_host) and the update runs on the HIP kernels as usual
@@ -684,7 +679,7 @@ class HipEngine:
         no all-reduce between the gradient and the update (the caller checks: world size 1)."""
         p = self.p
         clip = p.max_grad_norm is not None and p.max_grad_norm > 0
-        return (self.fused_apply and not self.use_graphs and not extra_grad and not clip
+        return (self.fused_apply and not extra_grad and not clip
                 and (self.heads or (len(self.buckets) == 1 and self.buckets[0]["partials"])))
 
     def step(self, idx: Optional[torch.Tensor], extra_grad: float = 0.0, allreduce=None,
@@ -707,7 +702,7 @@ class HipEngine:
         if allreduce is None and self.can_fuse_apply(extra_grad):
             self.grad(idx, apply=True)          # world size 1: gather + Adam in one launch
             return
-        if self.heads and getattr(allreduce, "in_stream", False) and not self.use_graphs:
+        if self.heads and getattr(allreduce, "in_stream", False):
             # native RCCL on the compute stream (parallel/dist.py NativeComm): no cross-stream
             # event hops, so the joint kernels (one wgrad, one gather) then the all-reduce in
             # stream order, then the whole-vector Adam (+ clip)
@@ -724,7 +719,7 @@ class HipEngine:
             self.apply(extra_grad)
             return
         idx_t, first, xt_ready = self._minibatch(idx)
-        if clip or extra_grad or self.use_graphs:
+        if clip or extra_grad:
             self._flush_value()
             self._heads_grad(idx_t, first, xt_ready)
             if allreduce is not None:
@@ -863,8 +858,7 @@ class HipEngine:
             self.adam_step += 1
             self._norm_n = self.norm_n_whole
         else:
-            self._launch(("grad", idx is None, first, xt_ready),
-                         lambda: self._launch_grad(idx_t, first, xt_ready))
+            self._launch_grad(idx_t, first, xt_ready)
         return None
 
     def _launch_grad(self, idx_t: torch.Tensor, first: bool, xt_ready: bool, fused_apply: bool = False) -> None:
@@ -897,30 +891,6 @@ class HipEngine:
         if p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])  # train.py:164
 
-    def _launch(self, key, fn) -> None:
-        """Run a fixed launch chain directly, or as a captured hipGraph (``use_graphs``).
-
-        Every kernel in a chain reads its per-step state from device memory (Adam step counter, weight
-        images, minibatch index buffer), and every buffer it touches is allocated once in ``__init__`` and
-        only ever updated in place, so one capture per (chain, static-flag) key replays correctly for the
-        whole run. The first call of a key runs eagerly (warm-up: code objects loaded, LDS attributes
-        set), the second captures and replays.  (The per-head chains run eagerly.)
-        """
-        if not self.use_graphs:
-            fn()
-            return
-        g = self._graphs.get(key)
-        if g is None:
-            if key not in self._graph_warm:
-                self._graph_warm.add(key)
-                fn()
-                return
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=self._capture_stream):
-                fn()
-            self._graphs[key] = g
-        g.replay()
-
     @torch.no_grad()
     def apply(self, extra_grad: float = 0.0) -> None:
         """whole-vector Adam (+ clip) after grad() [+ the all-reduce]"""
@@ -930,13 +900,10 @@ class HipEngine:
             self.grad_flat.add_(extra_grad)
         mx = float(p.max_grad_norm) if (p.max_grad_norm is not None and p.max_grad_norm > 0) else 0.0
         b1, b2 = p.adam_betas
-        # eager: the host knows the step number (one fused kernel without clipping); a captured
-        # graph must not bake it in, so graph replay reads the device counter instead
-        host_step = 0 if self.use_graphs else self.adam_step + 1
-        self._launch(("adam",), lambda: self.ext.adam(
-            self.model.flat.data, self.grad_flat, self.adam_m, self.adam_v, float(p.lr), float(b1), float(b2),
-            float(p.adam_eps), mx, self.adam_state, self.norm_part[:self.norm_n_whole], self.wimg, self.w_map,
-            self.wt_map, self.dt, self.no_q, host_step, *self._f8()))
+        # the host knows the step number: one fused kernel without clipping
+        self.ext.adam(self.model.flat.data, self.grad_flat, self.adam_m, self.adam_v, float(p.lr), float(b1),
+                      float(b2), float(p.adam_eps), mx, self.adam_state, self.norm_part[:self.norm_n_whole], self.wimg,
+                      self.w_map, self.wt_map, self.dt, self.no_q, self.adam_step + 1, *self._f8())
         self.adam_step += 1
         self._norm_n = self.norm_n_whole
         return None
@@ -948,7 +915,7 @@ class HipEngine:
         copy ahead of the next pack)."""
         if self._loss_dev is None:
             return None
-        # every Adam path (fused no-clip, sumsq + clip, graph replay, per head) leaves the per-block
+        # every Adam path (fused no-clip, sumsq + clip, per head) leaves the per-block
         # sums of squares of the gradient it applied in norm_part[:_norm_n]
         self.ext.metrics_pack(ep2, self._loss_dev, self.norm_part[:self._norm_n], self.metrics_buf)
         return self.metrics_buf

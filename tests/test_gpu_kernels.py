@@ -617,25 +617,6 @@ def test_head_kernels_match_one_kernel_update(env_name, mb, dtype, loss, monkeyp
         assert bool((mp_h != 0).any()) and bool((vp_h != 0).any())
 
 
-@pytest.mark.parametrize("batch", ["full", "minibatch"])
-def test_graph_replay_bit_identical_to_eager(batch):
-    """use_graphs replays captured hipGraphs of the grad / Adam chains; the result must be bit-identical
-    to eager launches over several iterations (first-step and later-step keys, minibatch index reuse)."""
-    from pytorch_dppo_amd.parallel.dist import DistContext
-    from pytorch_dppo_amd.runtime.worker import DPPOWorker
-    bs = 64 * 8 if batch == "full" else 128
-    common = dict(device="gpu", env_name="Hopper-v2", num_envs=64, exploration_size=64 * 8, batch_size=bs,
-                  num_epoch=3, dtype="bf16", seed=3)
-    we = DPPOWorker(dppo_preset(use_graphs=False, **common), DistContext(device=DEV))
-    wg = DPPOWorker(dppo_preset(use_graphs=True, **common), DistContext(device=DEV))
-    for _ in range(3):
-        me, mg = we.iteration_step(), wg.iteration_step()
-    assert wg.engine._graphs, "no graph was captured"
-    assert torch.equal(we.model.flat.data, wg.model.flat.data)
-    assert torch.equal(we.engine.adam_m, wg.engine.adam_m)
-    assert me["loss_value"] == mg["loss_value"]
-
-
 def test_deferred_metrics_match_synchronous():
     """iteration_step(defer=True) returns iteration i's metrics during iteration i+1; the values
     must equal the synchronous path's (same seed, same work)."""
