@@ -648,8 +648,9 @@ void value_head_t(const MlpArgs& a, hipStream_t s) {
 
 template <int DT>
 void value_t(const MlpArgs& a, hipStream_t s) {
-  const bool head = DT != DT_F32 && DT != DT_FP8 && mlp_head_applies(a) &&
-                    a.M >= mlp_head_rows() * cu_count() / 4;
+  // (at least one full round of head workgroups: below it the 32-row kernel's small workgroups
+  // fill the chip better)
+  const bool head = DT != DT_F32 && DT != DT_FP8 && mlp_head_applies(a) && a.M >= mlp_head_rows() * cu_count();
   if constexpr (DT == DT_F32) {
     value_launch<DT, 32, 4>(a, s);
   } else if constexpr (DT == DT_S3) {

@@ -87,12 +87,13 @@ def test_value_forward(env_name, dtype, tol):
 
 
 @pytest.mark.parametrize("dtype,tol", [("bf16x3", 2e-5), ("bf16", 3e-2)])
-@pytest.mark.parametrize("E,T", [(1000, 9), (2048, 16)])
+@pytest.mark.parametrize("E,T", [(3001, 15), (2048, 16)])
 def test_value_forward_on_head_kernel_matches_tile_kernel(dtype, tol, E, T):
     """values() on the value head's streaming kernel in forward mode (csrc/mlp_head.hip FWD, 128
-    rows per workgroup) vs mlp.hip's value kernel and the fp32 torch model: a row count that is not
-    a multiple of 128, and (2048 x 17 rows on 256 CUs) one past a whole round of workgroups, whose
-    tail rows the 32-row kernel takes"""
+    rows per workgroup; taken from one full round of workgroups up) vs mlp.hip's value kernel and
+    the fp32 torch model: 3001 x 16 rows (not a multiple of 128, tail > a quarter round: all on the
+    head kernel) and 2048 x 17 rows on 256 CUs (one past a whole round, whose tail rows the 32-row
+    kernel takes)"""
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=E, exploration_size=E * T,
                     batch_size=E * T, dtype=dtype)
     eng, model, _, _ = _engine(p)
@@ -954,14 +955,15 @@ def test_fp8_device_refresh_matches_torch_quantisation():
     assert same > 0.9999 and torch.equal(eng.wimg_fwd[w_map], eng.wimg_fwd[wt_map]), same
 
 
-def test_fp8_update_per_layer_error_and_shadow_image():
+def test_fp8_update_per_layer_error_and_shadow_image(monkeypatch):
     """fp8 mode (BASELINE config 5) on the per-head path: the value head's fc1 runs on the e4m3
     MFMA (csrc/mlp_head.hip F8: e4m3 weight image x e4m3-rounded observations), in the update and
     in values().  Per-layer relative error of the gradient vs fp32 autograd on the fp32 rows, the
     value forward vs the fp32 model, and the shadow e4m3 image the Adam step refreshes (== torch's
     float8_e4m3fn rounding of p / qscale for the new parameters)."""
-    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=1024, exploration_size=1024 * 16,
-                    batch_size=1024 * 16, dtype="fp8", ent_coeff=0.01)
+    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=2048, exploration_size=2048 * 16,
+                    batch_size=2048 * 16, dtype="fp8", ent_coeff=0.01)
+    monkeypatch.setenv("DPPO_HEADS", "1")
     eng, model, _, _ = _engine(p)
     assert eng.fp8 and eng.heads
     eng.refresh_fwd_image()
