@@ -1004,17 +1004,20 @@ def test_fp8_update_per_layer_error_and_shadow_image(monkeypatch):
     assert same > 0.9999 and torch.equal(eng.wimg_fwd[w_map], eng.wimg_fwd[wt_map]), same
 
 
+@pytest.mark.parametrize("heads", ["1", "0"])
 @pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
-def test_update_reads_rows_past_2gib_of_the_observation_buffer(dtype):
+def test_update_reads_rows_past_2gib_of_the_observation_buffer(dtype, heads, monkeypatch):
     """A Humanoid buffer of 65,536 envs x 22 (44 at bf16) steps (x_buf 2.3 GB): a minibatch whose
     rows all lie past the 2 GiB mark gets the gradient of autograd on exactly those rows — the
-    fused update's observation gather addresses the buffer with 64-bit offsets, or refuses the
-    buffer and runs a kernel that does (VERDICT r2 weak #4)."""
+    per-head kernels' observation gather (64-bit per-lane LDS-DMA addresses) and the tile kernel's
+    both address the buffer with 64-bit offsets (VERDICT r2 weak #4)."""
+    monkeypatch.setenv("DPPO_HEADS", heads)
     E, mb = 65536, 512
     T = 22 if dtype == "bf16x3" else 44      # 4 / 2 bytes per element: > 2.2 GB either way
     p = ppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=E, exploration_size=E * T, batch_size=mb,
                    dtype=dtype, ent_coeff=0.01)
     eng, model, _, _ = _engine(p)
+    assert eng.heads == (heads == "1")
     row_bytes = eng.x_buf.element_size() * eng.d0
     first = (1 << 31) // row_bytes + 1
     assert eng.x_buf.numel() * eng.x_buf.element_size() > 2.2e9 and first + mb < eng.N
