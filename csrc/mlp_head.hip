@@ -1053,7 +1053,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) g[u][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
     constexpr unsigned M4 = (4 * s + 3 < C::N1R) ? 0xffffu : ((1u << (4 * ((C::N1R - 4 * s) & 3))) - 1u);
-    for_slots<DT, M4, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    for_slots<DT, M4, 0, 16, (DT == DT_S3 ? 2 : 4)>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) g[q >> 2][rb] = P::mma(g[q >> 2][rb], a2[q & 3][rb], b);

@@ -177,7 +177,7 @@ DEV void f8_put(const F8Shadow& f8, int i, int wi, int wti, float pi) {
   if (f8.img != nullptr) {
     const uint8_t q = Prec<DT_FP8>::cvt(__fdiv_rn(pi, f8.qs[f8.lid[i]]));
     f8.img[wi] = q;
-    f8.img[wti] = q;
+    if (wti >= 0) f8.img[wti] = q;
   }
 }
 
@@ -216,9 +216,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     const int wi = w_map[i];
     if (wi >= 0) {
       const float q = qmul ? pi * qmul[i] : pi;
+      const int wti = wt_map[i];   // -1: no transposed image (first layer of a head)
       P::put(wimg, wi, q);
-      P::put(wimg, wt_map[i], q);
-      f8_put(f8, i, wi, wt_map[i], pi);
+      if (wti >= 0) P::put(wimg, wti, q);
+      f8_put(f8, i, wi, wti, pi);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -259,9 +260,10 @@ __global__ __launch_bounds__(256) void adam_noclip_kernel(float* __restrict__ p,
     const int wi = w_map[i];
     if (wi >= 0) {
       const float q = qmul ? pi * qmul[i] : pi;
+      const int wti = wt_map[i];   // -1: no transposed image (first layer of a head)
       P::put(wimg, wi, q);
-      P::put(wimg, wt_map[i], q);
-      f8_put(f8, i, wi, wt_map[i], pi);
+      if (wti >= 0) P::put(wimg, wti, q);
+      f8_put(f8, i, wi, wti, pi);
     }
   }
   __shared__ float red[256];
@@ -314,9 +316,10 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
     p[i] = pi;
     if (wi >= 0) {
       const float q = qmul ? pi * qmul[i] : pi;
+      const int wti = wt_map[i];   // -1: no transposed image (first layer of a head)
       P::put(wimg, wi, q);
-      P::put(wimg, wt_map[i], q);
-      f8_put(f8, i, wi, wt_map[i], pi);
+      if (wti >= 0) P::put(wimg, wti, q);
+      f8_put(f8, i, wi, wti, pi);
     }
   };
   if ((int)blockIdx.x < nrb) {
@@ -380,7 +383,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ p, 
     if (wi >= 0) {
       const float q = qmul ? p[i] * qmul[i] : p[i];
       P::put(wimg, wi, q);
-      P::put(wimg, wt_map[i], q);
+      if (wt_map[i] >= 0) P::put(wimg, wt_map[i], q);
     }
   }
 }
@@ -436,7 +439,7 @@ __global__ __launch_bounds__(256) void pack_fp8_kernel(const float* __restrict__
     if (wi >= 0) {
       const float q = __fdiv_rn(p[i], sc[lid[i]]);
       P::put(wimg, wi, q);
-      P::put(wimg, wt_map[i], q);
+      if (wt_map[i] >= 0) P::put(wimg, wt_map[i], q);
     }
   }
 }

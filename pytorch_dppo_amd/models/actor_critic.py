@@ -175,9 +175,13 @@ def fm_index(r: torch.Tensor, c: torch.Tensor, cols: int) -> torch.Tensor:
 class PackedLayout:
     """Padded weight images consumed by the MFMA kernels (csrc/mlp.hip, csrc/rollout.hip).
 
-    For each layer (order p_fc1, p_fc2, mu, v_fc1, v_fc2, v) two images in one buffer:
+    For each layer (order p_fc1, p_fc2, mu, v_fc1, v_fc2, v) in one buffer:
       Wp  [d_out][d_in]: Wp[n][k] = W[n][k] (k < K), Wp[n][K] = b[n], zeros elsewhere
-      Wpt [d_in][d_out]: transpose of Wp (dgrad operand)
+      Wpt [d_in][d_out]: transpose of Wp (dgrad operand) — for every layer but the first of each
+                         head: no kernel back-propagates into the observations, so p_fc1 / v_fc1
+                         have no transposed image (``wt_off`` aliases their forward image, and
+                         ``flat_to_wt`` is -1 there: the Adam kernels skip ~80 % of the scattered
+                         transposed-image stores)
     Both are stored FRAGMENT-MAJOR (:func:`fm_index`), so a kernel's B-operand fragment is a
     contiguous 1 KiB read.  The bias sits in column K because every activation tile carries a
     constant-1 column at index K (SURVEY §7.4 hard part 1: padded math == unpadded math),
@@ -187,6 +191,7 @@ class PackedLayout:
     """
 
     ORDER = ("p_fc1", "p_fc2", "mu", "v_fc1", "v_fc2", "v")
+    NO_WT = ("p_fc1", "v_fc1")   # first layer of each head: no dgrad operand
 
     def __init__(self, model: ActorCritic):
         self.layers = [model.layer(n) for n in self.ORDER]
@@ -196,6 +201,9 @@ class PackedLayout:
         for ls in self.layers:
             self.w_off[ls.name] = off
             off += ls.d_out * ls.d_in
+            if ls.name in self.NO_WT:
+                self.wt_off[ls.name] = self.w_off[ls.name]
+                continue
             self.wt_off[ls.name] = off
             off += ls.d_in * ls.d_out
         self.total = off
@@ -207,11 +215,13 @@ class PackedLayout:
             nn_ = torch.arange(ls.fan_out).repeat_interleave(ls.fan_in)
             kk = torch.arange(ls.fan_in).repeat(ls.fan_out)
             w_map[woff:woff + wn] = (self.w_off[ls.name] + fm_index(nn_, kk, ls.d_in)).to(torch.int32)
-            wt_map[woff:woff + wn] = (self.wt_off[ls.name] + fm_index(kk, nn_, ls.d_out)).to(torch.int32)
             boff, bn = model.offsets[f"{ls.name}.bias"]
             nb = torch.arange(ls.fan_out)
             kb = torch.full_like(nb, ls.fan_in)
             w_map[boff:boff + bn] = (self.w_off[ls.name] + fm_index(nb, kb, ls.d_in)).to(torch.int32)
+            if ls.name in self.NO_WT:
+                continue
+            wt_map[woff:woff + wn] = (self.wt_off[ls.name] + fm_index(kk, nn_, ls.d_out)).to(torch.int32)
             wt_map[boff:boff + bn] = (self.wt_off[ls.name] + fm_index(kb, nb, ls.d_out)).to(torch.int32)
         self.flat_to_w = w_map
         self.flat_to_wt = wt_map
@@ -237,5 +247,6 @@ class PackedLayout:
         mt = self.flat_to_wt.to(flat.device).long()
         sel = m >= 0
         out[m[sel]] = flat[sel].float()
-        out[mt[sel]] = flat[sel].float()
+        selt = mt >= 0
+        out[mt[selt]] = flat[selt].float()
         return out.to(dtype)
