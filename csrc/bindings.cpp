@@ -420,12 +420,36 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
 // grad / src_off / src_meta may be one head's slice of the flat vectors; red_dst then indexes
 // the slice.  The item tables are validated on the host when the engine builds them
 // (HipEngine._reduce_items): no per-epoch device sync here.
+// the slab runs of a gather: flattened [lo0, hi0, lo1, hi1, ...] (<= 4, ascending, disjoint, inside
+// [0, n)); every element of a run must have a slab source (src_meta != 0: the engine asserts it
+// when it builds the plan, runtime/engine_hip.py _slab_runs)
+SlabRuns make_runs(const std::vector<int64_t>& v, int64_t n) {
+  TORCH_CHECK(v.size() % 2 == 0 && v.size() / 2 >= 1 && v.size() / 2 <= 4, "slab runs: 1-4 [lo, hi) pairs");
+  SlabRuns r{};
+  r.n = (int)(v.size() / 2);
+  int64_t total = 0, prev = 0;
+  for (int k = 0; k < 4; ++k) {
+    if (k < r.n) {
+      const int64_t lo = v[2 * k], hi = v[2 * k + 1];
+      TORCH_CHECK(prev <= lo && lo <= hi && hi <= n, "slab runs must be ascending, disjoint and inside [0, n)");
+      r.lo[k] = (int)lo;
+      r.start[k] = (int)total;
+      total += hi - lo;
+      prev = hi;
+    } else {
+      r.lo[k] = 0;
+      r.start[k] = INT32_MAX;
+    }
+  }
+  r.total = (int)total;
+  return r;
+}
+
 void grad_gather(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_meta, torch::Tensor part,
                  int64_t nblk, int64_t npart, torch::Tensor red_col, torch::Tensor red_dst, double scale,
-                 torch::Tensor grad, torch::Tensor loss_out, int64_t i_lo, int64_t i_hi) {
+                 torch::Tensor grad, torch::Tensor loss_out, std::vector<int64_t> runs) {
   const int64_t n = grad.numel();
-  if (i_hi < 0) i_hi = n;
-  TORCH_CHECK(0 <= i_lo && i_lo <= i_hi && i_hi <= n, "gather range must lie in [0, n)");
+  const SlabRuns sr = make_runs(runs, n);
   check(grad, "grad", at::kFloat, n);
   check(src_off, "src_off", at::kInt, n);
   check(src_meta, "src_meta", at::kInt, n);
@@ -438,8 +462,7 @@ void grad_gather(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
   TORCH_CHECK(red_dst.numel() == nitems, "red_col / red_dst sizes");
   launch_grad_gather(slab.data_ptr<float>(), src_off.data_ptr<int>(), src_meta.data_ptr<int>(),
                      part.data_ptr<float>(), (int)nblk, (int)npart, red_col.data_ptr<int>(), red_dst.data_ptr<int>(),
-                     (int)nitems, (float)scale, grad.data_ptr<float>(), (int)i_lo, (int)i_hi,
-                     loss_out.data_ptr<float>(), cur_stream());
+                     (int)nitems, (float)scale, grad.data_ptr<float>(), sr, loss_out.data_ptr<float>(), cur_stream());
   after_launch(__func__);
 }
 
@@ -541,7 +564,7 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, do
 // launch (world size 1: nothing runs between them).  Bit-identical parameters to grad_gather ->
 // adam(host_step).  The flat tensors may be one head's slice (red_dst indexes the slice).
 void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_meta, torch::Tensor part,
-                 int64_t npblk, int64_t npart, torch::Tensor red_col, torch::Tensor red_dst, int64_t i_lo,
+                 int64_t npblk, int64_t npart, torch::Tensor red_col, torch::Tensor red_dst, std::vector<int64_t> runs,
                  double scale, torch::Tensor loss_out, torch::Tensor g, torch::Tensor p, torch::Tensor m,
                  torch::Tensor v, double lr, double b1, double b2, double eps, int64_t step, torch::Tensor state,
                  torch::Tensor norm_part, torch::Tensor wimg, torch::Tensor w_map, torch::Tensor wt_map, int64_t dt,
@@ -563,7 +586,8 @@ void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
   const int64_t nitems = red_col.numel();
   check(red_col, "red_col", at::kInt, nitems);
   check(red_dst, "red_dst", at::kInt, nitems);
-  TORCH_CHECK(red_dst.numel() == nitems && 0 <= i_lo && i_lo <= n, "red_col / red_dst / i_lo");
+  TORCH_CHECK(red_dst.numel() == nitems, "red_col / red_dst");
+  const SlabRuns sr = make_runs(runs, n);
   TORCH_CHECK(step >= 1, "gather_adam needs the host step number (eager launches only)");
   const int nblk = (int)norm_part.numel();
   check(norm_part, "norm_part", at::kFloat, nblk);
@@ -572,7 +596,7 @@ void gather_adam(torch::Tensor slab, torch::Tensor src_off, torch::Tensor src_me
   if (qmul.defined() && qmul.numel() > 0) { check(qmul, "qmul", at::kFloat, n); q = qmul.data_ptr<float>(); }
   launch_gather_adam(slab.data_ptr<float>(), src_off.data_ptr<int>(), src_meta.data_ptr<int>(),
                      part.data_ptr<float>(), (int)npblk, (int)npart, red_col.data_ptr<int>(), red_dst.data_ptr<int>(),
-                     (int)nitems, (int)i_lo, (float)scale, loss_out.data_ptr<float>(), g.data_ptr<float>(),
+                     (int)nitems, sr, (float)scale, loss_out.data_ptr<float>(), g.data_ptr<float>(),
                      p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (int)n, (float)lr, (float)b1,
                      (float)b2, (float)eps, (int)step, state.data_ptr<float>(), norm_part.data_ptr<float>(), nblk,
                      wimg.data_ptr(), w_map.data_ptr<int>(), wt_map.data_ptr<int>(), (int)dt, q,

@@ -112,6 +112,24 @@ struct F8Shadow {
   const float* qs;
 };
 
+#define DEV_HOST_INLINE __host__ __device__ inline
+
+// The slab elements of a gather: up to 4 runs [lo, hi) of flat indices, every element with a slab
+// source (src_meta != 0); start[r] = elements before run r (start[n..3] = INT_MAX), total = all.
+// The gathers iterate over them without a data-dependent branch, so every per-element load of a
+// thread issues in one round trip before its slab-chunk loads.
+struct SlabRuns {
+  int n, total;
+  int lo[4], start[4];
+  DEV_HOST_INLINE int flat(int j) const {
+    int i = lo[0] + j;
+#pragma unroll
+    for (int r = 1; r < 4; ++r)
+      if (j >= start[r]) i = lo[r] + (j - start[r]);
+    return i;
+  }
+};
+
 // reduce items per block of the gather kernels (common.h item_reduce)
 constexpr int ITEM_IPB = 32;
 inline __host__ __device__ int item_blocks(int nitems) { return (nitems + ITEM_IPB - 1) / ITEM_IPB; }
@@ -153,7 +171,7 @@ void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
 // with_partials: also log_std grads [0, A) and the 8 loss sums from the per-workgroup partials
 void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part, int nblk,
                         int npart, const int* red_col, const int* red_dst, int nitems, float scale, float* grad,
-                        int i_lo, int i_hi, float* loss_out, hipStream_t s);
+                        const SlabRuns& runs, float* loss_out, hipStream_t s);
 void launch_gae(const float* rewards, const float* values, const float* dones, float* adv, float* ret,
                 int T, int E, float gamma, float lam, int mode, int seg, hipStream_t s);
 void set_adam_fused(int on);
@@ -164,8 +182,8 @@ void launch_adam(float* p, const float* g, float* m, float* v, int n, float lr, 
 // grad_gather (with the partials pass, range [A, n)) + no-clip Adam fused: world size 1 only
 // (no all-reduce between them); nblk = norm_part size, must exceed A + 8
 void launch_gather_adam(const float* slab, const int* src_off, const int* src_meta, const float* part, int npblk,
-                        int npart, const int* red_col, const int* red_dst, int nitems, int i_lo, float scale,
-                        float* loss_out, float* g, float* p, float* m, float* v,
+                        int npart, const int* red_col, const int* red_dst, int nitems, const SlabRuns& runs,
+                        float scale, float* loss_out, float* g, float* p, float* m, float* v,
                         int n, float lr, float b1, float b2, float eps, int step, float* state, float* norm_part,
                         int nblk, void* wimg, const int* w_map, const int* wt_map, int dt, const float* img_scale,
                         const F8Shadow& f8, hipStream_t s);

@@ -293,7 +293,7 @@ template <int DT>
 __global__ __launch_bounds__(256) void gather_adam_kernel(
     const float* __restrict__ slab, const int* __restrict__ src_off, const int* __restrict__ src_meta,
     const float* __restrict__ part, int npblk, int npart, const int* __restrict__ red_col,
-    const int* __restrict__ red_dst, int nitems, int i_lo, float scale, float* __restrict__ loss_out,
+    const int* __restrict__ red_dst, int nitems, SlabRuns runs, float scale, float* __restrict__ loss_out,
     float* __restrict__ g, float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, int n, float lr,
     float b1, float b2, float eps, float step, float* __restrict__ state, float* __restrict__ norm_part,
     typename Prec<DT>::T* __restrict__ wimg, const int* __restrict__ w_map, const int* __restrict__ wt_map,
@@ -308,15 +308,14 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
   float ss = 0.f;
   // the optimizer-state loads are issued before the gradient is formed (they do not depend on
   // it), so their latency overlaps the slab loads'
-  auto update = [&](int i, float gi, float mi, float vi, float pv, int wi) {
+  auto update = [&](int i, float gi, float mi, float vi, float pv, int wi, int wti) {
     g[i] = gi;
     const float pi = adam_elem(mi, vi, pv, gi, b1, b2, step_size, rbc2, eps);
     m[i] = mi;
     v[i] = vi;
     p[i] = pi;
-    if (wi >= 0) {
+    if (wi >= 0) {   // (wti -1: no transposed image, the first layer of a head)
       const float q = qmul ? pi * qmul[i] : pi;
-      const int wti = wt_map[i];   // -1: no transposed image (first layer of a head)
       P::put(wimg, wi, q);
       if (wti >= 0) P::put(wimg, wti, q);
       f8_put(f8, i, wi, wti, pi);
@@ -333,7 +332,7 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
       const int d = red_dst[j];
       if (d >= 0) {
         const float gi = tot * scale;
-        update(d, gi, m[d], v[d], p[d], w_map[d]);
+        update(d, gi, m[d], v[d], p[d], w_map[d], wt_map[d]);
         ss = gi * gi;
       } else {
         loss_out[-1 - d] = tot;
@@ -350,18 +349,20 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
     return;
   }
   const int nb = gridDim.x - nrb;
-  for (int i = i_lo + (blockIdx.x - nrb) * 256 + threadIdx.x; i < n; i += nb * 256) {
+  for (int j = (blockIdx.x - nrb) * 256 + threadIdx.x; j < runs.total; j += nb * 256) {
+    // no data-dependent branch: every per-element load issues in one round trip, then the slab
+    // chunk loads (their addresses need src_off)
+    const int i = runs.flat(j);
     const int mt = src_meta[i];
-    if (mt == 0) continue;   // a reduce item's element (log_std, the fused narrow layers)
     const int o = src_off[i];
     const float mi = m[i], vi = v[i], pv = p[i];
-    const int wi = w_map[i];
+    const int wi = w_map[i], wti = wt_map[i];
     const int nch = mt >> 4;
     const size_t st = (size_t)(mt & 15) << 12;
     const float s = slab_sum(slab + o, nch, st);
     const float gi = s * scale;
     ss = fmaf(gi, gi, ss);
-    update(i, gi, mi, vi, pv, wi);
+    update(i, gi, mi, vi, pv, wi, wti);
   }
   red[threadIdx.x] = ss;
   __syncthreads();
@@ -570,12 +571,12 @@ extern "C" void launch_adam(float* p, const float* g, float* m, float* v, int n,
 
 extern "C" void launch_gather_adam(const float* slab, const int* src_off, const int* src_meta, const float* part,
                                    int npblk, int npart, const int* red_col, const int* red_dst, int nitems,
-                                   int i_lo, float scale, float* loss_out, float* g, float* p,
+                                   const SlabRuns& runs, float scale, float* loss_out, float* g, float* p,
                                    float* m, float* v, int n, float lr, float b1, float b2, float eps, int step,
                                    float* state, float* norm_part, int nblk, void* wimg, const int* w_map,
                                    const int* wt_map, int dt, const float* img_scale, const F8Shadow& f8,
                                    hipStream_t s) {
-#define GA_ARGS slab, src_off, src_meta, part, npblk, npart, red_col, red_dst, nitems, i_lo, scale, loss_out, g, p, m, \
+#define GA_ARGS slab, src_off, src_meta, part, npblk, npart, red_col, red_dst, nitems, runs, scale, loss_out, g, p, m, \
                 v, n, lr, b1, b2, eps, \
                 (float)step, state, norm_part
   if (dt == DT_F32)

@@ -142,17 +142,17 @@ void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
 // Blocks [0, item_blocks(nitems)): the reduce items (log_std, loss-term sums, the per-head
 // kernels' fused narrow-layer weight gradients): column sums of the per-workgroup partial rows in
 // a fixed order (item_reduce), grad[d] = scale * sum or loss_out[q] (red_dst).
-// Blocks past them: grad[i] = scale * sum_{c < nch} slab[src_off[i] + c * stride], i in
-// [i_lo, i_hi) with src_meta[i] != 0 (= nch * 16 + stride / 4096, each tile has its own
-// batch-chunk count).  Fixed chunk order: deterministic; no float atomics anywhere.
+// Blocks past them: grad[i] = scale * sum_{c < nch} slab[src_off[i] + c * stride] for the slab
+// elements i of `runs` (src_meta[i] = nch * 16 + stride / 4096, each tile has its own batch-chunk
+// count).  Fixed chunk order: deterministic; no float atomics anywhere.
 __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restrict__ slab,
                                                           const int* __restrict__ src_off,
                                                           const int* __restrict__ src_meta,
                                                           const float* __restrict__ part,
                                                           int nblk, int npart, const int* __restrict__ red_col,
                                                           const int* __restrict__ red_dst, int nitems,
-                                                          float scale, float* __restrict__ grad, int i_lo,
-                                                          int i_hi, float* __restrict__ loss_out) {
+                                                          float scale, float* __restrict__ grad, SlabRuns runs,
+                                                          float* __restrict__ loss_out) {
   const int nrb = item_blocks(nitems);
   if ((int)blockIdx.x < nrb) {
     __shared__ float red[256];
@@ -166,9 +166,9 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
     return;
   }
   const int nb = gridDim.x - nrb;
-  for (int i = i_lo + (blockIdx.x - nrb) * 256 + threadIdx.x; i < i_hi; i += nb * 256) {
+  for (int j = (blockIdx.x - nrb) * 256 + threadIdx.x; j < runs.total; j += nb * 256) {
+    const int i = runs.flat(j);
     const int mt = src_meta[i];
-    if (mt == 0) continue;   // a reduce item's element
     const int o = src_off[i];
     const int nch = mt >> 4;
     const size_t st = (size_t)(mt & 15) << 12;
@@ -189,12 +189,12 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
 
 extern "C" void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part,
                                    int nblk, int npart, const int* red_col, const int* red_dst, int nitems,
-                                   float scale, float* grad, int i_lo, int i_hi, float* loss_out, hipStream_t s) {
-  int grid = (i_hi - i_lo + 255) / 256;
+                                   float scale, float* grad, const SlabRuns& runs, float* loss_out, hipStream_t s) {
+  int grid = (runs.total + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
   grid += item_blocks(nitems);
   hipLaunchKernelGGL(grad_gather_kernel, dim3(grid), dim3(256), 0, s, slab, src_off, src_meta, part, nblk, npart,
-                     red_col, red_dst, nitems, scale, grad, i_lo, i_hi, loss_out);
+                     red_col, red_dst, nitems, scale, grad, runs, loss_out);
   HIP_CHECK_LAUNCH();
 }

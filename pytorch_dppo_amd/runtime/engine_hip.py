@@ -351,7 +351,7 @@ class HipEngine:
             self.buckets.append({
                 "tasks_host": tasks_host, "tasks": tasks_host.to(self.device),
                 "slab": torch.zeros(base, device=self.device, dtype=torch.float32),
-                "lo": lo, "hi": hi, "partials": partials[bi]})
+                "lo": lo, "hi": hi, "partials": partials[bi], "runs": self._slab_runs(sm, lo)})
         src[src < 0] = 0  # reduce items (log_std, and with the per-head kernels mu / v)
         self.src_off = src.to(torch.int32).to(self.device)
         self.src_meta = meta.to(torch.int32).to(self.device)
@@ -366,6 +366,22 @@ class HipEngine:
         if not self.fp8:
             return (self.no_u8, self.empty, self.no_q)
         return (self.wimg_fwd, self.layer_id[lo:hi], self.qscale)
+
+    @staticmethod
+    def _slab_runs(meta_slice: torch.Tensor, lo: int) -> list:
+        """the gathers' slab runs (csrc/kernels.h SlabRuns): the maximal index runs of a bucket's
+        flat range [lo, hi) whose elements all have a slab source (src_meta > 0), flattened
+        [lo0, hi0, ...] in absolute flat indices; the reduce items between them are not visited"""
+        has = (meta_slice > 0).to(torch.int8).tolist()
+        runs, start = [], None
+        for k, h in enumerate(has + [0]):
+            if h and start is None:
+                start = k
+            elif not h and start is not None:
+                runs += [lo + start, lo + k]
+                start = None
+        assert 2 <= len(runs) <= 8, "a gather takes 1-4 slab runs"
+        return runs
 
     def _reduce_items(self, model: ActorCritic) -> Dict[str, tuple]:
         """Reduce items of the gather launches: (partial-row column, destination) pairs, the
@@ -798,7 +814,7 @@ class HipEngine:
         src_off, src_meta = self.joint_src
         rc, rd = self.items["joint"]
         self.ext.grad_gather(b["slab"], src_off, src_meta, self.part_joint, self.nhead_blk, self.part_joint.shape[1],
-                             rc, rd, 1.0 / self.mb, self.grad_flat, self.loss_sums, self.A, -1)
+                             rc, rd, 1.0 / self.mb, self.grad_flat, self.loss_sums, b["runs"])
 
     def _joint_step(self, idx_t, first: bool, xt_ready: bool) -> None:
         """world size 1: policy kernel, value kernel (one shared partial buffer), ONE wgrad over
@@ -812,7 +828,7 @@ class HipEngine:
         src_off, src_meta = self.joint_src
         rc, rd = self.items["joint"]
         self.ext.gather_adam(b["slab"], src_off, src_meta, self.part_joint, self.nhead_blk, self.part_joint.shape[1],
-                             rc, rd, self.A, 1.0 / M, self.loss_sums, self.grad_flat, self.model.flat.data,
+                             rc, rd, b["runs"], 1.0 / M, self.loss_sums, self.grad_flat, self.model.flat.data,
                              self.adam_m, self.adam_v, float(p.lr), float(b1), float(b2), float(p.adam_eps),
                              self.adam_step + 1, self.adam_state, self.norm_part[:self.norm_n_whole], self.wimg,
                              self.w_map, self.wt_map, self.dt, self.no_q, *self._f8())
@@ -830,7 +846,8 @@ class HipEngine:
         part = self.part_h[h]
         rc, rd = self.items["policy" if h == 0 else "value"]
         self.ext.grad_gather(b["slab"], self.src_off[lo:hi], self.src_meta[lo:hi], part, self.nhead_blk,
-                             part.shape[1], rc, rd, 1.0 / M, self.grad_flat[lo:hi], self.loss_sums, 0, -1)
+                             part.shape[1], rc, rd, 1.0 / M, self.grad_flat[lo:hi], self.loss_sums,
+                             [r - lo for r in b["runs"]])
 
     def _head_adam(self, h: int, step_no: int) -> None:
         """no-clip Adam over head h's flat range (after its all-reduce); its norm region"""
@@ -884,7 +901,7 @@ class HipEngine:
             b1, b2 = p.adam_betas
             rc, rd = self.items["legacy"]
             self.ext.gather_adam(b["slab"], self.src_off, self.src_meta, self.part, self.ntrain_blk,
-                                 self.npart, rc, rd, self.A, 1.0 / M, self.loss_sums, self.grad_flat,
+                                 self.npart, rc, rd, b["runs"], 1.0 / M, self.loss_sums, self.grad_flat,
                                  self.model.flat.data, self.adam_m, self.adam_v, float(p.lr), float(b1),
                                  float(b2), float(p.adam_eps), self.adam_step + 1, self.adam_state,
                                  self.norm_part[:self.norm_n_whole], self.wimg, self.w_map, self.wt_map, self.dt,
@@ -892,7 +909,7 @@ class HipEngine:
             return
         rc, rd = self.items["legacy"]
         self.ext.grad_gather(b["slab"], self.src_off, self.src_meta, self.part, self.ntrain_blk, self.npart,
-                             rc, rd, 1.0 / M, self.grad_flat, self.loss_sums, b["lo"], b["hi"])
+                             rc, rd, 1.0 / M, self.grad_flat, self.loss_sums, b["runs"])
         if p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])  # train.py:164
 

@@ -30,23 +30,23 @@ def main():
     n = eng.model.num_params
     empty_i = torch.empty(0, dtype=torch.int32, device=dev)
 
-    def run(items, i_lo):
+    def run(items, runs):
         c, d = (rc, rd) if items else (empty_i, empty_i)
         ext.gather_adam(b["slab"], src_off, src_meta, eng.part_joint, eng.nhead_blk, eng.part_joint.shape[1], c, d,
-                        i_lo, 1.0 / eng.mb, eng.loss_sums, eng.grad_flat, eng.model.flat.data, eng.adam_m,
+                        runs, 1.0 / eng.mb, eng.loss_sums, eng.grad_flat, eng.model.flat.data, eng.adam_m,
                         eng.adam_v, 0.0, float(b1), float(b2), float(p.adam_eps), 1, eng.adam_state,
                         eng.norm_part[:eng.norm_n_whole], eng.wimg, eng.w_map, eng.wt_map, eng.dt, eng.no_q,
                         *eng._f8())
-    arms = {"full": (True, eng.A), "items_only": (True, n), "slab_only": (False, eng.A)}
+    arms = {"full": (True, b["runs"]), "items_only": (True, [n, n]), "slab_only": (False, b["runs"])}
     res = {}
-    for name, (items, i_lo) in arms.items():
+    for name, (items, runs) in arms.items():
         for _ in range(3):
-            run(items, i_lo)
+            run(items, runs)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(50):
-            run(items, i_lo)
+            run(items, runs)
         e1.record()
         torch.cuda.synchronize()
         res[name] = round(e0.elapsed_time(e1) * 1e3 / 50, 2)

@@ -58,7 +58,7 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads):
     model = ActorCritic(spec.obs_dim, spec.act_dim)
     stub = SimpleNamespace(L=model.packed_layout(), ldT=65536, A=spec.act_dim, device=torch.device("cpu"),
                            heads=heads, head_range=[model.head_ranges["policy"], model.head_ranges["value"]],
-                           _slab_index=HipEngine._slab_index)
+                           _slab_index=HipEngine._slab_index, _slab_runs=HipEngine._slab_runs)
     HipEngine._build_wgrad_plan(stub, model, target_wgs=256)
     total = 0
     for b in stub.buckets:
@@ -85,6 +85,16 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads):
     meta = stub.src_meta
     assert bool(((meta[slab_fed] >> 4) >= 1).all()) and bool(((meta[slab_fed] & 15) >= 1).all())
     assert bool((meta[~slab_fed] == 0).all())
+    # the gathers' slab runs cover exactly the slab-fed elements of each bucket's range
+    for b in stub.buckets:
+        r = b["runs"]
+        covered = torch.zeros(model.num_params, dtype=torch.bool)
+        for k in range(0, len(r), 2):
+            assert b["lo"] <= r[k] < r[k + 1] <= b["hi"]
+            covered[r[k]:r[k + 1]] = True
+        want = torch.zeros(model.num_params, dtype=torch.bool)
+        want[b["lo"]:b["hi"]] = slab_fed[b["lo"]:b["hi"]]
+        assert torch.equal(covered, want)
     if heads:   # per-head buckets: policy [A, v_fc1.weight), value [v_fc1.weight, n)
         (b0, b1) = stub.buckets
         assert (b0["lo"], b0["hi"]) == (spec.act_dim, model.head_ranges["policy"][1]) and b0["partials"]
