@@ -170,6 +170,10 @@ class DistContext:
         return {k: float(x) for k, x in zip(keys, t.tolist())}
 
     def allreduce_tensor_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if (self.collective and self.native is not None and op == "sum" and t.is_contiguous()
+                and t.dtype in (torch.float32, torch.float64)):
+            self.native.allreduce_(t)                # in stream order
+            return t
         if self.collective:
             dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
                                    "min": dist.ReduceOp.MIN}[op])
