@@ -477,6 +477,34 @@ void obs_reduce(torch::Tensor part, int64_t nblk, int64_t O, torch::Tensor s12, 
   after_launch(__func__);
 }
 
+// the per-step obs-norm mode's observe (model.py:68 over one step's E observations): moments about
+// shift -> fixed-order fp64 reduce -> Chan merge into (mean, m2) and the fp32 images; three
+// launches, no host sync (n_a: the stats' count before this batch, tracked on the host)
+void obs_observe(torch::Tensor obs, torch::Tensor shift, torch::Tensor mean, torch::Tensor m2, torch::Tensor mean_f32,
+                 torch::Tensor inv_std, double n_a, torch::Tensor part, torch::Tensor s12, double var_floor) {
+  const int64_t O = mean.numel();
+  TORCH_CHECK(obs.dim() == 2 && obs.size(1) == O && obs.size(0) > 0, "obs must be [E][O]");
+  const int E = (int)obs.size(0);
+  const int nblk = obs_moments_blocks(E);
+  check(obs, "obs", at::kFloat, (int64_t)E * O);
+  check(shift, "shift", at::kFloat, O);
+  check(part, "part", at::kFloat, (int64_t)nblk * 2 * O);
+  check(s12, "s12", at::kDouble, 2 * O);
+  check(mean, "mean", at::kDouble, O);
+  check(m2, "m2", at::kDouble, O);
+  check(mean_f32, "mean_f32", at::kFloat, O);
+  check(inv_std, "inv_std", at::kFloat, O);
+  TORCH_CHECK(shift.data_ptr() != mean_f32.data_ptr(), "shift must be a snapshot, not the stats' own mean image");
+  const hipStream_t s = cur_stream();
+  launch_obs_moments(obs.data_ptr<float>(), E, (int)O, shift.data_ptr<float>(), part.data_ptr<float>(), s);
+  launch_obs_reduce(part.data_ptr<float>(), nblk, (int)O, s12.data_ptr<double>(), nullptr, nullptr, s);
+  launch_obs_merge(s12.data_ptr<double>(), (int)O, (double)E, n_a, shift.data_ptr<float>(), mean.data_ptr<double>(),
+                   m2.data_ptr<double>(), mean_f32.data_ptr<float>(), inv_std.data_ptr<float>(), var_floor, s);
+  after_launch(__func__);
+}
+
+int64_t obs_moments_nblk(int64_t E) { return obs_moments_blocks((int)E); }
+
 void obs_merge(torch::Tensor s12, double count, double n_a, torch::Tensor shift, torch::Tensor mean, torch::Tensor m2,
                torch::Tensor mean_f32, torch::Tensor inv_std, double var_floor) {
   const int64_t O = mean.numel();
@@ -679,6 +707,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_adam_fused", [](int64_t on) { set_adam_fused((int)on); });
   m.def("obs_reduce", &obs_reduce);
   m.def("obs_merge", &obs_merge);
+  m.def("obs_observe", &obs_observe);
+  m.def("obs_moments_nblk", &obs_moments_nblk);
   m.def("adam", &adam);
   m.def("gather_adam", &gather_adam);
   m.def("pack", &pack);

@@ -194,8 +194,12 @@ void launch_pack(const float* p, int n, void* wimg, const int* w_map, const int*
 // floats of per-block maxima)
 void launch_fp8_refresh(const float* p, const int* lid, int n, float* qscale, float* part, void* wimg,
                         const int* w_map, const int* wt_map, hipStream_t s);
+// ep == nullptr: the moments only (epstat unread)
 void launch_obs_reduce(const float* part, int nblk, int O, double* s12, const float* epstat, double* ep,
                        hipStream_t s);
+// [E][O] observations -> [obs_moments_blocks(E)][2][O] fp32 partials about shift
+int obs_moments_blocks(int E);
+void launch_obs_moments(const float* obs, int E, int O, const float* shift, float* part, hipStream_t s);
 void launch_obs_merge(const double* s12, int O, double count, double n_a, const float* shift, double* mean,
                       double* m2, float* mean_f32, float* inv_std, double var_floor, hipStream_t s);
 // out f64[11] = [episode return sum, count | 8 loss sums | gradient L2 norm from the nblk

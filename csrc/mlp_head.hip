@@ -10,15 +10,14 @@
 //    independent of the other head's, so at world size > 1 one head's RCCL all-reduce overlaps
 //    the other head's kernels (runtime/engine_hip.py), the reference's chief sum
 //    (chief.py:13-20) off the critical path;
-//  * a head alone needs half the registers of both, so a wave owns TWO 16-row blocks (32 rows,
-//    128 per 4-wave workgroup): every weight fragment a workgroup pulls from L2 into its LDS
+//  * a head alone needs half the registers of both, so one 128-row workgroup streams a head's
+//    weights once for all its rows: every weight fragment a workgroup pulls from L2 into its LDS
 //    ring feeds 128 rows instead of 64 — half the L2->CU weight bytes per row, the bound of the
-//    64-row kernel (docs/ARCHITECTURE.md: ~20 B/clk per CU of LDS-DMA), and each fragment read
-//    from LDS feeds 6 MFMAs instead of 3.
+//    round-2 64-row kernel (docs/ARCHITECTURE.md: ~20 B/clk per CU of LDS-DMA).
 // The observation rows are read once per head (2 x 100 MB per epoch at the bench geometry).
 //
-// Structure per workgroup (4 waves, one per SIMD, up to 512 VGPRs each; wave w owns rows
-// 32w .. 32w+31 of the workgroup's 128 through the whole chain, activations in registers in the
+// Structure per workgroup (HeadCfg: 8 waves, two per SIMD, 256 registers each; wave w owns rows
+// 16w .. 16w+15 of the workgroup's 128 through the whole chain, activations in registers in the
 // MFMA C layout):
 //   fc1      X (gathered rows, per-wave LDS ring, LDS-DMA with 64-bit per-lane row addresses —
 //            any buffer size) x W1: value 2 stages per k-step (32 output tiles), policy 2 k-steps

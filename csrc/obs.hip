@@ -6,6 +6,9 @@
 //   [RCCL all-reduce of the [2][O] fp64 sums across ranks — done by the worker]
 //   obs_merge  : Chan et al. merge of the batch into (n, mean, M2) fp64 and the fp32 images
 //                (mean, 1/sqrt(max(M2/n, 1e-2))) read by the normalisation prologue.
+//   obs_moments: the same [nblk][2][O] partials from an [E][O] observation batch — the per-step
+//                obs-norm mode (model.py:68 per observation) observes each step's batch before
+//                the step's one-step rollout launch normalises it: moments -> reduce -> merge.
 // Two launches replace ~25 small torch ops (measured ~230 us per iteration).
 #include "kernels.h"
 #include "common.h"
@@ -27,7 +30,7 @@ __global__ __launch_bounds__(OR_WAVES * 64) void obs_reduce_kernel(const float* 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ncol = 2 * O;
   const int ngrp = (ncol + 63) / 64;
-  if ((int)blockIdx.x == ngrp) {   // episode stats
+  if ((int)blockIdx.x == ngrp) {   // episode stats (launched only when ep is given)
     if (wave == 0) {
       double a = 0.0, c = 0.0;
       for (int b = lane; b < nblk; b += 64) { a += epstat[2 * b]; c += epstat[2 * b + 1]; }
@@ -94,11 +97,41 @@ __global__ __launch_bounds__(256) void obs_merge_kernel(const double* __restrict
   inv_std[d] = (float)(1.0 / sqrt(var));
 }
 
+// One workgroup per OM_ROWS consecutive observations: thread = column (coalesced rows), the
+// workgroup's columns in 256-wide passes, OM_ROWS rows summed in order (fp32, about the shift,
+// like the rollout kernel's partials).
+constexpr int OM_ROWS = 64;
+__global__ __launch_bounds__(256) void obs_moments_kernel(const float* __restrict__ obs, int E, int O,
+                                                          const float* __restrict__ shift, float* __restrict__ part) {
+  const int r0 = blockIdx.x * OM_ROWS;
+  const int r1 = min(E, r0 + OM_ROWS);
+  for (int d = threadIdx.x; d < O; d += 256) {
+    const float sh = shift[d];
+    float s1 = 0.f, s2 = 0.f;
+    for (int r = r0; r < r1; ++r) {
+      const float v = obs[(size_t)r * O + d] - sh;
+      s1 += v;
+      s2 = fmaf(v, v, s2);
+    }
+    part[((size_t)blockIdx.x * 2) * O + d] = s1;
+    part[((size_t)blockIdx.x * 2 + 1) * O + d] = s2;
+  }
+}
+
 }  // namespace
+
+extern "C" int obs_moments_blocks(int E) { return (E + OM_ROWS - 1) / OM_ROWS; }
+
+extern "C" void launch_obs_moments(const float* obs, int E, int O, const float* shift, float* part, hipStream_t s) {
+  hipLaunchKernelGGL(obs_moments_kernel, dim3(obs_moments_blocks(E)), dim3(256), 0, s, obs, E, O, shift, part);
+  HIP_CHECK_LAUNCH();
+}
 
 extern "C" void launch_obs_reduce(const float* part, int nblk, int O, double* s12, const float* epstat, double* ep,
                                   hipStream_t s) {
-  hipLaunchKernelGGL(obs_reduce_kernel, dim3((2 * O + 63) / 64 + 1), dim3(OR_WAVES * 64), 0, s, part, nblk, O, s12, epstat, ep);
+  // the extra workgroup (episode stats) only when ep is given
+  hipLaunchKernelGGL(obs_reduce_kernel, dim3((2 * O + 63) / 64 + (ep != nullptr ? 1 : 0)), dim3(OR_WAVES * 64), 0, s,
+                     part, nblk, O, s12, epstat, ep);
   HIP_CHECK_LAUNCH();
 }
 

@@ -134,6 +134,8 @@ class HipEngine:
         self.mom = torch.zeros(nroll, 2, O, **f32)
         self.epstat = torch.zeros(nroll, 2, **f32)
         self.ep_sum = torch.zeros(2, dtype=torch.float64, device=device)
+        self._step_bufs = None     # per-step obs-norm mode: the steps' rollout moments / episode stats
+        self._obs_scratch = None   # obs_observe partials + fp64 sums
         # ---- update geometry ----
         self.mb = params.minibatch_rows()
         # per-head streaming kernels (csrc/mlp_head.hip, 128 rows per workgroup): split-bf16 and
@@ -506,7 +508,8 @@ class HipEngine:
 
     # ------------------------------------------------------------------------------------------
     def _launch_rollout(self, T: int, t_base: int, t0: int, norm: RunningObsStats, shift: torch.Tensor,
-                        xT: Optional[torch.Tensor] = None):
+                        xT: Optional[torch.Tensor] = None, mom: Optional[torch.Tensor] = None,
+                        epstat: Optional[torch.Tensor] = None):
         e = self.env
         kp = e.kernel_params()
         ints = [kp["kind"], self.E, self.O, self.A, e.state_dim, T, t_base, self.E, t0 & 0xFFFFFFFF,
@@ -515,8 +518,21 @@ class HipEngine:
         xt = xT if xT is not None else self.empty_x
         self.ext.rollout(self.dt_fwd, ROLL_ROWS, e.state, e.ep_len, e.ep_ret, self.wimg_fwd, self.layout,
                          self.scales, self.model.flat.data, norm.mean_f32, norm.inv_std_f32, shift, self.x_buf,
-                         self.actions, self.logp, self.rewards, self.dones, self.mom, self.epstat, ints, keys,
+                         self.actions, self.logp, self.rewards, self.dones,
+                         self.mom if mom is None else mom, self.epstat if epstat is None else epstat, ints, keys,
                          float(self.p.reward_clip), self.qscale, xt, self.x_rows[0])
+
+    def _observe_step(self, norm: RunningObsStats, obs: torch.Tensor, shift: torch.Tensor) -> None:
+        """norm.observes(obs) as three device launches (csrc/obs.hip obs_observe), moments about
+        the iteration's shift snapshot."""
+        if self._obs_scratch is None:
+            self._obs_scratch = (torch.zeros(int(self.ext.obs_moments_nblk(self.E)), 2, self.O,
+                                             dtype=torch.float32, device=self.device),
+                                 torch.zeros(2, self.O, dtype=torch.float64, device=self.device))
+        part, s12 = self._obs_scratch
+        self.ext.obs_observe(obs.to(self.device, torch.float32).contiguous(), shift, norm.mean, norm.mean_diff,
+                             norm.mean_f32, norm.inv_std_f32, float(norm.n), part, s12, 1e-2)
+        norm.n += float(obs.shape[0])
 
     @torch.no_grad()
     def _rollout_host(self) -> Dict:
@@ -551,7 +567,7 @@ class HipEngine:
             s1 += a1
             s2 += a2
             if p.obs_norm_update == "step":
-                norm.observes(obs)
+                self._observe_step(norm, obs, shift)
             x = norm.normalize(obs)
             mu, _, _ = self.model(x)
             eps = rng.gauss(self.key_action, eidx[:, None], self.env.t, dims[None, :])
@@ -615,19 +631,27 @@ class HipEngine:
             s1, s2 = self.s12[0], self.s12[1]
             ep = self.ep_sum
         else:
+            # per-step obs-norm mode (the reference's filter updates with every observation before
+            # normalising it, model.py:68 / train.py:84): step t's normalisation needs the stats of
+            # step t's batch, a grid-wide dependency, so each step is one observe (csrc/obs.hip:
+            # moments -> reduce -> merge into the worker-local stats) + a one-step rollout launch.
+            # The steps' rollout moments / episode stats land in per-step slices and ONE reduce
+            # after the loop gives the iteration's totals.  No host sync.
             shift = self.stats.shift().clone()
-            self.local_stats = RunningObsStats(self.O, self.device)
-            self.local_stats.copy_from(self.stats)
-            s1 = torch.zeros(self.O, dtype=torch.float64, device=self.device)
-            s2 = torch.zeros_like(s1)
-            ep = torch.zeros(2, dtype=torch.float64, device=self.device)
-            for t in range(self.T):
-                self.local_stats.observes(self.current_obs())
-                self._launch_rollout(1, t, self.env.t, self.local_stats, shift)
+            ls = self.local_stats = RunningObsStats(self.O, self.device)
+            ls.copy_from(self.stats)
+            T, nroll = self.T, self.mom.shape[0]
+            if self._step_bufs is None or self._step_bufs[0].shape[0] != T:
+                f32 = dict(dtype=torch.float32, device=self.device)
+                self._step_bufs = (torch.zeros(T, nroll, 2, self.O, **f32), torch.zeros(T, nroll, 2, **f32))
+            mom_t, ep_t = self._step_bufs
+            for t in range(T):
+                self._observe_step(ls, self.current_obs(), shift)
+                self._launch_rollout(1, t, self.env.t, ls, shift, mom=mom_t[t], epstat=ep_t[t])
                 self.env.t += 1
-                s1 += self.mom[:, 0].double().sum(0)
-                s2 += self.mom[:, 1].double().sum(0)
-                ep += self.epstat.double().sum(0)
+            self.ext.obs_reduce(mom_t, T * nroll, self.O, self.s12, ep_t, self.ep_sum)
+            s1, s2 = self.s12[0], self.s12[1]
+            ep = self.ep_sum
         # everything stays on the device: no host sync inside the iteration
         return {"count": float(self.N), "s1": s1, "s2": s2, "shift": shift,
                 "ep_return_sum": ep[0], "ep_count": ep[1], "ep2": ep}

@@ -224,6 +224,33 @@ def test_obs_reduce_and_merge_kernels_match_torch_welford(O, nblk, alias):
     assert torch.allclose(dev_st.inv_std_f32, ref.inv_std_f32, rtol=1e-4)
 
 
+@pytest.mark.parametrize("E,O", [(4096, 376), (1031, 37), (45, 17)])
+def test_obs_observe_matches_running_stats(E, O):
+    """obs_observe (the per-step obs-norm mode's observe: moments -> reduce -> merge, three
+    launches) over several steps' batches with drifting means, vs RunningObsStats.observes (fp64
+    torch); E = 4096 / 1031: many 64-row moment blocks, one ragged."""
+    ext = _ext()
+    g = torch.Generator(device="cpu").manual_seed(E + O)
+    ref = RunningObsStats(O, DEV)
+    st = RunningObsStats(O, DEV)
+    shift = st.shift().clone()          # the iteration's snapshot, fixed across the steps
+    nb = int(ext.obs_moments_nblk(E))
+    assert nb == -(-E // 64)
+    part = torch.zeros(nb, 2, O, device=DEV)
+    s12 = torch.zeros(2, O, dtype=torch.float64, device=DEV)
+    for t in range(4):
+        x = (torch.randn(E, O, generator=g) * (1 + t) + 3 * t).to(DEV)
+        ref.observes(x)
+        ext.obs_observe(x, shift, st.mean, st.mean_diff, st.mean_f32, st.inv_std_f32, float(st.n), part, s12, 1e-2)
+        st.n += E
+    assert torch.allclose(st.mean, ref.mean, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(st.mean_diff, ref.mean_diff, rtol=1e-4)
+    assert torch.allclose(st.inv_std_f32, ref.inv_std_f32, rtol=1e-4)
+    with pytest.raises(RuntimeError):   # the shift must not alias the stats being merged into
+        ext.obs_observe(x, st.mean_f32, st.mean, st.mean_diff, st.mean_f32, st.inv_std_f32, float(st.n), part, s12,
+                        1e-2)
+
+
 @pytest.mark.parametrize("T,E,mode,seg", [(33, 1031, 0, 0), (33, 1031, 1, 0), (2048, 1, 0, 0), (2048, 3, 2, 0),
                                           (1000, 5, 2, 0), (7, 2, 2, 0), (33, 1031, 1, 5), (1000, 5, 2, 64),
                                           (2048, 3, 2, 100), (40, 257, 1, 7)])
