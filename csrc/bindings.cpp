@@ -260,7 +260,8 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
                int64_t A, torch::Tensor actions, torch::Tensor logp_old, torch::Tensor adv, torch::Tensor ret,
                torch::Tensor v_old, torch::Tensor mu_prev, torch::Tensor v_prev, std::vector<int64_t> opts,
                std::vector<double> fopts, std::vector<torch::Tensor> tbufs, int64_t ldT, torch::Tensor part,
-               bool check_idx, bool xT_ready, torch::Tensor w8, torch::Tensor qscale) {
+               bool check_idx, bool xT_ready, torch::Tensor w8, torch::Tensor qscale, torch::Tensor q8_amax,
+               int64_t q8_step) {
   TORCH_CHECK(dt != 2, "the update runs in bf16 when dtype=fp8 (fp8 gradients underflow e4m3)");
   Layout L = parse_layout(layout);
   TORCH_CHECK(A > 0, "A");
@@ -292,7 +293,20 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   // rows each transposed buffer must hold (writer side)
   const int64_t need[11] = {L.d_in[0], L.d_in[1], L.d_in[2], L.d_in[4], L.d_in[5],
                             L.n_out[0], L.n_out[1], L.n_out[2], L.n_out[3], L.n_out[4], L.n_out[5]};
-  for (int i = 0; i < 11; ++i) check(tbufs[i], "transposed buffer", storage_type((int)dt), need[i] * ldT);
+  // q8_amax (fp8 mode, per-head bf16 update): the 3 x 4 slot ring of gradient maxima; the
+  // operand buffers then hold e4m3 bytes (csrc/common.h Q8)
+  const bool q8 = q8_amax.defined() && q8_amax.numel() > 0;
+  if (q8) {
+    TORCH_CHECK(dt == 1 && head >= 0, "e4m3 wgrad operands: the fp8 mode's per-head bf16 update only");
+    check(q8_amax, "q8_amax", at::kInt, 3 * Q8_SLOT);
+    unsigned* base = reinterpret_cast<unsigned*>(q8_amax.data_ptr<int>());
+    const int64_t e = ((q8_step % 3) + 3) % 3;   // step -1: the calibration pass
+    a.q8_acc = base + Q8_SLOT * e;
+    a.q8_rd = base + Q8_SLOT * ((e + 2) % 3);
+    a.q8_clr = base + Q8_SLOT * ((e + 1) % 3);
+  }
+  for (int i = 0; i < 11; ++i)
+    check(tbufs[i], "transposed buffer", q8 ? at::kByte : storage_type((int)dt), need[i] * ldT);
   const int npart = (int)opts[4];
   TORCH_CHECK(npart >= 8 + A || (head == 1 && npart >= 8), "npart too small");
   if (head == 0) TORCH_CHECK(part_dw >= 8 + A && part_dw + 32 * 128 <= npart, "part_dw: policy dW_mu block");
@@ -373,8 +387,11 @@ void set_mlp_rows(int64_t rows) {
   set_mlp_rows_override((int)rows);
 }
 
+// dt 2 (fp8 mode): e4m3 operands; q8_amax / q8_step name the slot the update read its gradient
+// scales from, q8_t the gradient tensor of each layer (-1: none), q8_xs the activation scales
 void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor> xT, std::vector<int64_t> g_rows,
-           std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab) {
+           std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab,
+           torch::Tensor q8_amax, int64_t q8_step, std::vector<int64_t> q8_t, std::vector<double> q8_xs) {
   const int wmax = 8, smax = 6;   // quadrants per task: one per wave of the 8-wave workgroup
   TORCH_CHECK(gT.size() == 6 && xT.size() == 6 && g_rows.size() == 6 && x_rows.size() == 6, "6 layers");
   check(tasks, "tasks", at::kInt, WGRAD_TASK_INTS);
@@ -409,7 +426,18 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
   a.tasks = reinterpret_cast<const WgradTask*>(tasks.data_ptr<int>());
   a.ntasks = ntasks;
   a.slab = slab.data_ptr<float>();
-  TORCH_CHECK(dt == 0 || dt == 1 || dt == 3, "wgrad runs in fp32, bf16 or bf16x3 (the fp8 mode's update is bf16)");
+  TORCH_CHECK(dt == 0 || dt == 1 || dt == 2 || dt == 3, "wgrad runs in fp32, bf16, e4m3 or bf16x3");
+  if (dt == 2) {
+    check(q8_amax, "q8_amax", at::kInt, 3 * Q8_SLOT);
+    TORCH_CHECK(q8_t.size() == 6 && q8_xs.size() == 6, "q8_t / q8_xs: one per layer");
+    const int64_t e = ((q8_step % 3) + 3) % 3;
+    a.q8_rd = reinterpret_cast<const unsigned*>(q8_amax.data_ptr<int>()) + Q8_SLOT * ((e + 2) % 3);
+    for (int i = 0; i < ntasks; ++i) {
+      const int l = tp[WGRAD_TASK_INTS * i];
+      TORCH_CHECK(q8_t[l] >= 0 && q8_t[l] < 4 && q8_xs[l] > 0, "e4m3 wgrad task on a layer without operand scales");
+    }
+    for (int i = 0; i < 6; ++i) { a.q8_t[i] = (int)q8_t[i]; a.q8_xs[i] = (float)q8_xs[i]; }
+  }
   launch_wgrad((int)dt, a, cur_stream());
   after_launch(__func__);
 }

@@ -159,6 +159,52 @@ DEV void opnd_store(const V& v, V* p) {
 #endif
 }
 
+// ---- fp8 mode's e4m3 wgrad operands ("Q8", csrc/mlp_head.hip + csrc/wgrad.hip) ----
+// The update writes every wgrad operand (x^T, h1^T, g1^T, g2^T of both heads) as OCP e4m3 bytes
+// scaled by a power of two, and the wgrad kernel multiplies each product tile by the exact
+// inverse.  Activations have fixed ranges: tanh outputs and the bias 1 (x 256 <= 256), the
+// normalised observations clamped to +-5 (x 64 <= 320).  The gradients' scales are DELAYED
+// per-tensor scales: step e stores with the scale of step e-1's amax (the head kernels
+// atomic-max |g| into a 3-slot ring: accumulate e % 3, read (e-1) % 3, clear (e+1) % 3), chosen
+// so the previous amax lands in [64, 128): 3.5x headroom below e4m3's 448 before saturation.
+// The ring is [3 slots][4 tensors][Q8_SUB sub-slots][32 dwords]: each wave max-es into sub-slot
+// (wave id) % Q8_SUB, one 128-byte line each, so the device-scope atomics of ~8k waves spread
+// over 64 lines instead of serialising on one address (measured: one address per tensor made the
+// head kernels 2.7x slower); a reader folds the 64 sub-slots with one load per lane.
+// (ring geometry Q8_SUB / Q8_LINE / Q8_SLOT: csrc/kernels.h, shared with the bindings)
+constexpr float Q8_SX = 64.f, Q8_SH = 256.f;
+DEV uint32_t wave_umax(uint32_t v) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+__host__ __device__ inline float q8_pow2(int e) {   // 2^e, |e| <= 120, exact
+  const uint32_t b = (uint32_t)(e + 127) << 23;
+  float f;
+  __builtin_memcpy(&f, &b, 4);
+  return f;
+}
+// the exponent e of the store scale 2^e for a tensor of max |g| = amax (fp32 bits)
+__host__ __device__ inline int q8_exp(uint32_t amax_bits) {
+  const int ex = (int)((amax_bits >> 23) & 0xffu);
+  if (ex == 0 || ex == 255) return 0;            // zero / denormal / non-finite: scale 1
+  const int e = 6 - (ex - 127);
+  return e < -120 ? -120 : (e > 120 ? 120 : e);
+}
+// 4 fp32 -> 4 e4m3 bytes (x s, saturated to +-448) in one dword, element 0 in the low byte
+DEV uint32_t q8_pack4(const f32x4& v, float s) {
+  const float a = fminf(fmaxf(v[0] * s, -448.f), 448.f), b = fminf(fmaxf(v[1] * s, -448.f), 448.f);
+  const float c = fminf(fmaxf(v[2] * s, -448.f), 448.f), d = fminf(fmaxf(v[3] * s, -448.f), 448.f);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+// the same for values known to stay inside e4m3's range after scaling (activations)
+DEV uint32_t q8_pack4u(const f32x4& v, float s) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * s, v[1] * s, 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[2] * s, v[3] * s, w, true);
+}
+DEV float absmax4(const f32x4& v) { return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))); }
+
 // storage precision of the normalised-observation buffer written by the rollout and read by
 // the value/update kernels: fp8 forward kernels keep it in bf16 (the update runs in bf16)
 template <int DT> struct XStore { static constexpr int DTX = (DT == DT_FP8) ? DT_BF16 : DT; };

@@ -44,6 +44,10 @@ struct RolloutArgs {
   unsigned long long* tstamp;  // DIAGNOSTIC ONLY (null in real runs): [nblk][NW][8] phase cycles
 };
 
+// fp8 mode's gradient-amax ring (csrc/common.h Q8): [3 slots][4 tensors][Q8_SUB sub-slots][Q8_LINE]
+constexpr int Q8_SUB = 64, Q8_LINE = 32;
+constexpr int Q8_SLOT = 4 * Q8_SUB * Q8_LINE;   // dwords per ring slot
+
 struct MlpArgs {
   // input rows: x_buf row-major [*][d1]; row m of this call reads x_buf[idx ? idx[m] : row0 + m]
   const void* x_buf;
@@ -89,6 +93,13 @@ struct MlpArgs {
   int npart;
   int part_dw;            // per-head kernels: column of the fused narrow-layer weight gradient in a
                           // partial row (policy: dW_mu [32][128], value: dW_v [128]; bias = column 100)
+  // fp8 mode's e4m3 wgrad operands (csrc/common.h Q8): null = the operands in the update's
+  // precision.  Slots of the gradient-amax ring (4 tensors g1p, g2p, g1v, g2v x Q8_SUB sub-slots,
+  // fp32 bits): the scales of this step come from q8_rd, its |g| maxima go to q8_acc, q8_clr is
+  // zeroed
+  const unsigned* q8_rd;
+  unsigned* q8_acc;
+  unsigned* q8_clr;
   // DIAGNOSTIC ONLY (scripts/phase_timeline.py; null in every real run): per-wave s_memtime
   // stamps at the phase boundaries of every tstamp_every-th workgroup, [blk][NW][16]
   unsigned long long* tstamp;
@@ -149,6 +160,12 @@ struct WgradArgs {
   const WgradTask* tasks;
   int ntasks;
   float* slab;
+  // e4m3 operands (dt fp8, csrc/common.h Q8): the product tile of layer l is multiplied by
+  // 1 / (2^q8_exp(max of tensor q8_t[l]'s sub-slots in q8_rd) * q8_xs[l]) — the gradient
+  // tensor's delayed scale (the slot the update read) times the activation side's fixed scale
+  const unsigned* q8_rd;
+  int q8_t[6];
+  float q8_xs[6];
 };
 
 extern "C" {

@@ -160,10 +160,11 @@ constexpr int xr_floats() {
 }
 template <int DT, int HEAD, bool F8 = false>
 constexpr int ws_floats() { return xr_floats<DT, HEAD, F8>() + HeadCfg<HEAD>::RB * TILE_F; }
+// (+ Q8: the 2 x Q8_SUB sub-slot maxima of the head's gradient tensors the step's scales come from)
 template <int DT, int HEAD, bool F8 = false>
 constexpr size_t head_lds_bytes() {
   return (size_t)head_stages<DT, HEAD, F8>() * stage_bytes<DT>() +
-         (size_t)HeadCfg<HEAD>::NW * ws_floats<DT, HEAD, F8>() * sizeof(float);
+         (size_t)HeadCfg<HEAD>::NW * ws_floats<DT, HEAD, F8>() * sizeof(float) + 2 * Q8_SUB * sizeof(float);
 }
 template <int HEAD>
 constexpr int wrows() { return 16 * HeadCfg<HEAD>::RB; }
@@ -377,10 +378,12 @@ DEV float xsum(float x) {   // sum over the lanes that differ only in the bits o
 // FWD (value head only): the forward alone, V(x) of rows [row0, row0 + M) into v_out — the GAE
 // input pass (train.py:87,109-112) at the update kernel's 128 rows per weight stream instead of
 // mlp.hip's 32-row value kernel
-template <int DT, int HEAD, bool FWD = false, bool F8 = false>
+// Q8 (fp8 mode, bf16 update): the wgrad operands are stored as scaled e4m3 bytes (csrc/common.h Q8)
+template <int DT, int HEAD, bool FWD = false, bool F8 = false, bool Q8 = false>
 __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
   static_assert(!FWD || HEAD == 1, "forward mode is the value head's");
   static_assert(!F8 || (HEAD == 1 && DT == DT_BF16), "the e4m3 fc1 is the bf16 value head's");
+  static_assert(!Q8 || (DT == DT_BF16 && !FWD), "e4m3 wgrad operands: the fp8 mode's (bf16) update");
   using C = HeadCfg<HEAD>;
   using H = HT<DT>;
   using P = typename H::P;
@@ -545,15 +548,40 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   };
 
   HD_STAMP(0);
+  // Q8: wave 0 DMAs the previous step's sub-slot maxima of the head's two gradient tensors into
+  // LDS — the oldest vector-memory ops of the wave (never behind a counted wait), read after many
+  // barriers at dgrad fc3
+  const uint32_t* q8l = reinterpret_cast<const uint32_t*>(smem + head_lds_bytes<DT, HEAD, F8>() - 2 * Q8_SUB * 4);
+  if constexpr (Q8) {
+    if (wave == 0) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(a.q8_rd + ((2 * HEAD + k) * Q8_SUB + lane) * Q8_LINE),
+            (__attribute__((address_space(3))) void*)(q8l + k * Q8_SUB), 4, 0, 0);
+    }
+  }
   // ---- prime: the first X k-steps, then ring stages 0 .. S-2 ----
 #pragma unroll
   for (int k = 0; k < XS; ++k) issue_x(k);
 #pragma unroll
   for (int st = 0; st < S - 1; ++st) issue(st, st);
 
-  const size_t tsb = (size_t)a.ldT * 16 * sizeof(T);   // bytes of one 16-feature row block of an FM operand
+  // bytes of one 16-feature row block of an FM operand (Q8: one byte per element)
+  const size_t tsb = (size_t)a.ldT * 16 * (Q8 ? 1 : sizeof(T));
   auto lane_base = [&](void* buf, int rb) __attribute__((always_inline)) {
-    return H::eptr(buf, fm_index(lr, mw + 16 * rb + 4 * lg, a.ldT));
+    const size_t i = fm_index(lr, mw + 16 * rb + 4 * lg, a.ldT);
+    return Q8 ? reinterpret_cast<char*>(buf) + i : H::eptr(buf, i);
+  };
+  // a wgrad operand group of 4 consecutive batch rows of one feature (Q8: x s, saturated for the
+  // gradients; the activations' fixed scales keep them in range)
+  auto opnd4 = [&](char* p, const f32x4& v, float s) __attribute__((always_inline)) {
+    if constexpr (Q8) opnd_store(q8_pack4(v, s), reinterpret_cast<uint32_t*>(p));
+    else HT<DT>::store4(p, v);
+  };
+  auto opnd4u = [&](char* p, const f32x4& v, float s) __attribute__((always_inline)) {
+    if constexpr (Q8) opnd_store(q8_pack4u(v, s), reinterpret_cast<uint32_t*>(p));
+    else HT<DT>::store4(p, v);
   };
   void* const h1T = HEAD == 0 ? a.h1pT : a.h1vT;
   void* const g2T = HEAD == 0 ? a.g2pT : a.g2vT;
@@ -575,8 +603,22 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     float4* w = reinterpret_cast<float4*>(tp + lr * SST + 8 * lg);
     w[0] = float4{v[0], v[1], v[2], v[3]};
     w[1] = float4{v[4], v[5], v[6], v[7]};
-    store_T8<DT>(a.xT, tp, SST, lane >> 1, lane & 1, 32 * rot_ks(ks, rot, ks1) + (lane >> 1),
-             mw + 16 * rb + 8 * (lane & 1), a.ldT);
+    if constexpr (Q8) {
+      const int col = lane >> 1, hh = lane & 1;
+      f32x4 x0, x1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x0[j] = tp[(8 * hh + j) * SST + col];
+        x1[j] = tp[(8 * hh + 4 + j) * SST + col];
+      }
+      const uint32_t w0 = q8_pack4u(x0, Q8_SX), w1 = q8_pack4u(x1, Q8_SX);
+      opnd_store(u32x2{w0, w1}, reinterpret_cast<u32x2*>(reinterpret_cast<char*>(a.xT) +
+                                                        fm_index(32 * rot_ks(ks, rot, ks1) + col,
+                                                                 mw + 16 * rb + 8 * hh, a.ldT)));
+    } else {
+      store_T8<DT>(a.xT, tp, SST, lane >> 1, lane & 1, 32 * rot_ks(ks, rot, ks1) + (lane >> 1),
+                   mw + 16 * rb + 8 * (lane & 1), a.ldT);
+    }
   };
   if constexpr (F8) {
     // e4m3 fc1: per k-step pair 2 stages (tiles 0-15, 16-31), each slot one tile's two fragments;
@@ -698,8 +740,8 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       // (the last k-step holds the bias column (1) and zero padding: stored as such)
       const f32x4 s0 = last ? bias_col(h0, c0, n1) : h0, s1 = last ? bias_col(h1, c0 + 16, n1) : h1;
       if constexpr (!FWD) {
-        store_Tt<DT>(bh1[rb], 2 * I, tsb, s0);
-        store_Tt<DT>(bh1[rb], 2 * I + 1, tsb, s1);
+        opnd4u(bh1[rb] + (size_t)(2 * I) * tsb, s0, Q8_SH);
+        opnd4u(bh1[rb] + (size_t)(2 * I + 1) * tsb, s1, Q8_SH);
       }
       tp_put(tpb + rb * TILE_F, s0, s1, lane);
     }
@@ -1004,13 +1046,21 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     for (int rb = 0; rb < RB; ++rb) d2[rb][t] = P::mma(d2[rb][t], ad[rb], b);
   });
   nst = 0;
+  // Q8: this step's store scales of the head's two gradient tensors (g1: 2 HEAD, g2: 2 HEAD + 1)
+  // from the previous step's maxima (scalar loads); the running |g| maxima of this wave
+  float sg1 = 1.f, sg2 = 1.f, am1 = 0.f, am2 = 0.f;
+  if constexpr (Q8) {
+    sg1 = q8_pow2(q8_exp(wave_umax(q8l[lane])));
+    sg2 = q8_pow2(q8_exp(wave_umax(q8l[Q8_SUB + lane])));
+  }
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     const int c = 16 * t + lr;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       d2[rb][t] = c < n2 ? d2[rb][t] * (1.0f - acc2[rb][t] * acc2[rb][t]) : f32x4{0.f, 0.f, 0.f, 0.f};
-      store_Tt<DT>(bg2[rb], t, tsb, d2[rb][t]);
+      if constexpr (Q8) am2 = fmaxf(am2, absmax4(d2[rb][t]));
+      opnd4(bg2[rb] + (size_t)t * tsb, d2[rb][t], sg2);
     }
   }
   nst += 8 * H::SPS * RB;
@@ -1036,7 +1086,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
           const f32x4 h = acc1[rb][tt];
-          store_Tt<DT>(bg1[rb], tt, tsb, gq[decltype(uc)::value][rb] * (1.0f - h * h));
+          const f32x4 gv = gq[decltype(uc)::value][rb] * (1.0f - h * h);
+          if constexpr (Q8) am1 = fmaxf(am1, absmax4(gv));
+          opnd4(bg1[rb] + (size_t)tt * tsb, gv, sg1);
         }
         n += H::SPS * RB;
       }
@@ -1052,7 +1104,10 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) g[u][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
     constexpr unsigned M4 = (4 * s + 3 < C::N1R) ? 0xffffu : ((1u << (4 * ((C::N1R - 4 * s) & 3))) - 1u);
-    for_slots<DT, M4, 0, 16, (DT == DT_S3 ? 2 : 4)>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    // (fragment reads in groups of 2 where the registers are tight: split-bf16, and the value
+    // head with the e4m3 operand stores' scales / maxima)
+    constexpr int G4 = (DT == DT_S3 || (Q8 && HEAD == 1)) ? 2 : 4;
+    for_slots<DT, M4, 0, 16, G4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) g[q >> 2][rb] = P::mma(g[q >> 2][rb], a2[q & 3][rb], b);
@@ -1112,6 +1167,20 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     });
   }
 
+  if constexpr (Q8) {
+    // this step's gradient maxima (max is order-independent: the atomics keep it deterministic)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      am1 = fmaxf(am1, __shfl_xor(am1, o, 64));
+      am2 = fmaxf(am2, __shfl_xor(am2, o, 64));
+    }
+    const int sub = (blockIdx.x * NW + wave) & (Q8_SUB - 1);
+    if (lane == 0) {
+      atomicMax(a.q8_acc + ((2 * HEAD) * Q8_SUB + sub) * Q8_LINE, __float_as_uint(am1));
+      atomicMax(a.q8_acc + ((2 * HEAD + 1) * Q8_SUB + sub) * Q8_LINE, __float_as_uint(am2));
+    }
+    if (blockIdx.x == 0 && tid < 2 * Q8_SUB) a.q8_clr[(2 * HEAD * Q8_SUB + tid) * Q8_LINE] = 0u;
+  }
   // ---------------- per-workgroup partials (deterministic fixed order) ----------------
   WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
   __syncthreads();
@@ -1165,12 +1234,12 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   }   // !FWD
 }
 
-template <int DT, int HEAD, bool FWD = false, bool F8 = false>
+template <int DT, int HEAD, bool FWD = false, bool F8 = false, bool Q8 = false>
 void head_launch_t(const MlpArgs& a, hipStream_t s) {
   const size_t lds = head_lds_bytes<DT, HEAD, F8>();
-  set_max_lds_once<mlp_head_kernel<DT, HEAD, FWD, F8>>(lds);
+  set_max_lds_once<mlp_head_kernel<DT, HEAD, FWD, F8, Q8>>(lds);
   const int nblk = (a.M + ROWS - 1) / ROWS;
-  hipLaunchKernelGGL((mlp_head_kernel<DT, HEAD, FWD, F8>), dim3(nblk), dim3(HeadCfg<HEAD>::NW * 64), lds, s, a);
+  hipLaunchKernelGGL((mlp_head_kernel<DT, HEAD, FWD, F8, Q8>), dim3(nblk), dim3(HeadCfg<HEAD>::NW * 64), lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
@@ -1178,6 +1247,18 @@ void head_launch_t(const MlpArgs& a, hipStream_t s) {
 // e4m3 fc1 when the k-steps pair up (d_in a multiple of 64)
 template <int DT, int HEAD, bool FWD = false>
 void head_launch(const MlpArgs& a, hipStream_t s) {
+  if constexpr (DT == DT_BF16 && !FWD) {
+    if (a.q8_rd != nullptr) {   // fp8 mode: e4m3 wgrad operands (+ the value head's e4m3 fc1)
+      if constexpr (HEAD == 1) {
+        if (a.W8 != nullptr && a.qscale != nullptr && ((a.d_in[0] >> 5) & 1) == 0) {
+          head_launch_t<DT, HEAD, FWD, true, true>(a, s);
+          return;
+        }
+      }
+      head_launch_t<DT, HEAD, FWD, false, true>(a, s);
+      return;
+    }
+  }
   if constexpr (DT == DT_BF16 && HEAD == 1) {
     if (a.W8 != nullptr && a.qscale != nullptr && ((a.d_in[0] >> 5) & 1) == 0) {
       head_launch_t<DT, HEAD, FWD, true>(a, s);

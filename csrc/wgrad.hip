@@ -30,8 +30,13 @@ constexpr int WG_SLOTS = 24;   // fragment slots per stage: (nq + kq) * 4 <= 24 
 // it the vmcnt arithmetic — is task-independent).  S-deep ring, counted vmcnt and a raw
 // s_barrier keep S-1 steps of DMA in flight across the barrier (cdna_hip_programming.md
 // 'Pipelining across barriers'): no VGPRs hold in-flight data.
+// bytes per operand slot: one fragment (32 batch rows of 16 features); e4m3 (DT_FP8) two
+// fragments of consecutive k-steps (64 batch rows, 1 KiB: one DMA instruction, and the pair is
+// contiguous in the FM layout), so a kernel "k-step" there covers 64 rows
 template <int DT>
-constexpr int wgrad_frag_bytes() { return 512 * Prec<DT>::BYTES; }
+constexpr int wgrad_frag_bytes() { return DT == DT_FP8 ? 1024 : 512 * Prec<DT>::BYTES; }
+template <int DT>
+constexpr int wgrad_step_rows() { return DT == DT_FP8 ? 64 : 32; }
 template <int DT, int S>
 constexpr size_t wgrad_lds_bytes() { return (size_t)S * WG_SLOTS * wgrad_frag_bytes<DT>(); }
 
@@ -47,7 +52,7 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const char* g = reinterpret_cast<const char*>(a.gT[tk.layer]);
   const char* x = reinterpret_cast<const char*>(a.xT[tk.layer]);
-  const int nk = (tk.m1 - tk.m0) >> 5;
+  const int nk = (tk.m1 - tk.m0) / wgrad_step_rows<DT>();
   const int ks0 = tk.m0 >> 5;
   const int NF = 4 * tk.nq, F = NF + 4 * tk.kq;
   // slot f of a stage holds fragment f: f < NF -> dY^T row tile n0/16 + f, else X^T row tile
@@ -74,6 +79,10 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
         glds16(src[q] + (size_t)kk * FB + go, st + dst[q] + h * 1024);
       }
   };
+  // Q8: this lane's sub-slot maximum of the layer's gradient tensor, loaded before any DMA (the
+  // oldest vector-memory op: it never holds up a counted wait), folded in the epilogue
+  uint32_t q8v = 0;
+  if constexpr (DT == DT_FP8) q8v = a.q8_rd[(a.q8_t[tk.layer] * Q8_SUB + lane) * Q8_LINE];
   const bool active = wave < tk.nq * tk.kq;
   const int wn = wave / tk.kq, wk = wave - (wave / tk.kq) * tk.kq;
   f32x4 acc[4][4];
@@ -90,6 +99,27 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
     if (active) {
       const char* st = smem + (k % S) * SB;
       Frag af[4], bf[4];
+      if constexpr (DT == DT_FP8) {
+        // two e4m3 k-steps per slot: lane l's 8 bytes of k-step 2kk at l * 8, of 2kk + 1 512 on
+        long a0[4], a1[4], b0[4], b1[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const char* pa = st + (wn * 4 + i) * FB + lane * 8;
+          const char* pb = st + (NF + wk * 4 + i) * FB + lane * 8;
+          a0[i] = *reinterpret_cast<const long*>(pa);
+          a1[i] = *reinterpret_cast<const long*>(pa + 512);
+          b0[i] = *reinterpret_cast<const long*>(pb);
+          b1[i] = *reinterpret_cast<const long*>(pb + 512);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a0[i], b0[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a1[i], b1[j], acc[i][j], 0, 0, 0);
+          }
+        continue;
+      }
       auto lds_frag = [&](int f) {
         if constexpr (IsSplit<DT>::value) {
           const char* b = st + f * FB + (lane >> 5) * 1024 + (lane & 31) * 16;
@@ -113,6 +143,13 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   if (!active) return;
   const int KE = tk.kq * 64;
   float* out = a.slab + tk.slab;
+  if constexpr (DT == DT_FP8) {   // undo the operands' scales (powers of two: exact)
+    const float inv = q8_pow2(-q8_exp(wave_umax(q8v))) / a.q8_xs[tk.layer];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] *= inv;
+  }
   const int col = wk * 64 + (lane & 15);
   const int rbase = wn * 64 + (lane >> 4) * 4;
 #pragma unroll
@@ -131,7 +168,7 @@ __global__ __launch_bounds__(WG_WAVES * 64) void wgrad_kernel(WgradArgs a) {
   else wgrad_lds_body<DT, S, 3>(a, tk, smem);
 }
 
-// ring depth: fp32 and split-bf16 3 stages (144 KiB), bf16 4 (96 KiB)
+// ring depth: fp32 and split-bf16 3 stages (144 KiB), bf16 and e4m3 4 (96 KiB)
 template <int DT, int S>
 void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
   const size_t lds = wgrad_lds_bytes<DT, S>();
@@ -183,6 +220,7 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
   if (a.ntasks <= 0) return;
   if (dt == DT_F32) launch_wgrad_lds<DT_F32, 3>(a, s);
   else if (dt == DT_S3) launch_wgrad_lds<DT_S3, 3>(a, s);
+  else if (dt == DT_FP8) launch_wgrad_lds<DT_FP8, 4>(a, s);
   else launch_wgrad_lds<DT_BF16, 4>(a, s);
   HIP_CHECK_LAUNCH();
 }

@@ -94,7 +94,10 @@ def build(verbose: bool = False, force: bool = False, variant: str = "", csrc: s
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         objs = list(ex.map(lambda j: _compile(j[0], j[1], verbose, csrc), jobs))
     out = ext_path(variant)
-    key = _digest(objs, " ".join(ldflags))
+    # the object names carry their source digests (hipcc's object bytes are not reproducible
+    # across machines), so the stamp names the sources + flags the .so was built from
+    key = hashlib.sha256((" ".join(os.path.basename(o) for o in objs) + " "
+                          + " ".join(ldflags)).encode()).hexdigest()[:16]
     stamp = out + ".stamp"
     if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
         return out

@@ -53,6 +53,9 @@ def decode(s: torch.Tensor, dt: int) -> torch.Tensor:
 def set_elements(buf: torch.Tensor, idx: torch.Tensor, value: float, dt: int) -> None:
     """buf.view(-1)[idx] = value in the storage format of ``dt`` (in place)."""
     flat = buf.view(-1)
+    if dt == 2:       # the e4m3 byte of value (the caller applies the buffer's scale)
+        flat[idx] = torch.tensor(float(value)).to(torch.float8_e4m3fn).view(torch.uint8).item()
+        return
     if dt != DT_S3:
         flat[idx] = value
         return

@@ -34,6 +34,8 @@ from ..utils.obs_stats import RunningObsStats
 
 STORAGE = storage.STORAGE
 NPART_FIXED = 8
+Q8_SX, Q8_SH = 64.0, 256.0   # fixed e4m3 operand scales of the observations / tanh activations (csrc/common.h)
+Q8_SUB = 64                  # sub-slots per tensor of the gradient-amax ring (csrc/kernels.h)
 WT = 128            # operand-buffer row padding (csrc/kernels.h WGRAD_TILE)
 
 
@@ -147,6 +149,16 @@ class HipEngine:
         ncu = (torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 256)
         self.heads = (mode != "0" and bool(self.ext.head_applies(self.dt, self.layout, A))
                       and (mode == "1" or params.minibatch_rows() >= 128 * ncu))
+        # fp8 mode on the per-head path: the wgrad operands (x^T, h1^T, g1^T, g2^T of both heads)
+        # are e4m3 bytes with power-of-two scales — fixed for the activations, delayed per-tensor
+        # for the gradients (csrc/common.h Q8) — and the wgrad runs on the e4m3 MFMA: half the
+        # operand bytes of the bf16 update's HBM round trip.  DPPO_Q8=0: bf16 operands.
+        self.q8 = self.fp8 and self.heads and os.environ.get("DPPO_Q8", "1") != "0"
+        # the gradient-amax ring: 3 slots x 4 tensors x 64 sub-slot lines of 32 dwords (csrc/kernels.h)
+        self.q8_amax = torch.zeros(3 * 4 * Q8_SUB * 32, dtype=torch.int32, device=device)
+        self._q8_next = 0          # step counter of the amax ring
+        self._q8_step = 0
+        self._q8_cal = [False, False]   # per head: the calibration pass ran
         # operand rows: a multiple of the update kernel's row tile (every row it writes has a
         # column) and of 64 (wgrad consumes k-steps in pairs, csrc/wgrad.hip)
         self.ldT = _r(self.mb, 128 if self.heads else 64)
@@ -179,7 +191,8 @@ class HipEngine:
         g_rows = [lp1.fan_out, lp2.fan_out, lmu.fan_out, lv1.fan_out, lv2.fan_out, lv.fan_out]
         self.x_rows = [_r(r, WT) for r in x_rows]
         self.g_rows = [_r(r, WT) for r in g_rows]
-        mk = lambda rows: torch.zeros(rows, self.ldT, dtype=self.sdtype, **dev)
+        opd = torch.uint8 if self.q8 else self.sdtype
+        mk = lambda rows: torch.zeros(rows, self.ldT, dtype=opd, **dev)
         self.xT = mk(self.x_rows[0])                       # shared by p_fc1 and v_fc1
         self.h1pT, self.h2pT = mk(self.x_rows[1]), mk(self.x_rows[2])
         self.h1vT, self.h2vT = mk(self.x_rows[4]), mk(self.x_rows[5])
@@ -195,7 +208,10 @@ class HipEngine:
         cols = torch.arange(self.ldT, device=device)
         for buf, r in ((self.h1pT, lp1.fan_out), (self.h2pT, lp2.fan_out), (self.h1vT, lv1.fan_out),
                        (self.h2vT, lv2.fan_out)):
-            storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), 1.0, self.dt)
+            if self.q8:       # e4m3 bytes of the activation scale (Q8_SH = 256: exact)
+                storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), Q8_SH, 2)
+            else:
+                storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), 1.0, self.dt)
         self._build_wgrad_plan(model)
         if self.heads:
             # the joint (one-bucket) plan of world size 1 beside the per-head buckets
@@ -241,8 +257,9 @@ class HipEngine:
         self.empty_x = torch.empty(0, dtype=self.sdtype, **dev)
         self.x_raw: Optional[torch.Tensor] = None   # compat Q8: raw bootstrap rows (values())
         # the rollout can emit the full-batch x^T operand when the update is one full-batch step
+        # (Q8: the policy kernel writes the e4m3 x^T in the first full-batch step instead)
         self.xT_from_rollout = (self.mb == self.N and self.ldT == self.N and E % 16 == 0 and self.N % 32 == 0
-                                and params.obs_norm_update == "rollout")
+                                and params.obs_norm_update == "rollout" and not self.q8)
         self._xT_valid = False   # True once a rollout wrote x^T for the current buffer contents
         self.s12 = torch.zeros(2, O, dtype=torch.float64, **dev)
         stats.device_merge = self._device_merge
@@ -357,6 +374,20 @@ class HipEngine:
         src[src < 0] = 0  # reduce items (log_std, and with the per-head kernels mu / v)
         self.src_off = src.to(torch.int32).to(self.device)
         self.src_meta = meta.to(torch.int32).to(self.device)
+
+    def q8_maxima(self) -> torch.Tensor:
+        """[3 slots][4 tensors] gradient maxima (g1p, g2p, g1v, g2v) of the amax ring (diagnostics)"""
+        return self.q8_amax.view(3, 4, Q8_SUB, 32)[..., 0].view(torch.float32).amax(-1)
+
+    def _wgrad(self, b: Dict) -> None:
+        """one wgrad launch over bucket b's tasks (Q8: e4m3 operands, the step's scales)"""
+        if self.q8:
+            self.ext.wgrad(native.DT_CODE["fp8"], self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT,
+                           b["tasks"], b["tasks_host"], b["slab"], self.q8_amax, self._q8_step,
+                           [0, 1, -1, 2, 3, -1], [Q8_SX, Q8_SH, 1.0, Q8_SX, Q8_SH, 1.0])
+        else:
+            self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
+                           b["tasks_host"], b["slab"], self.empty, 0, [-1] * 6, [1.0] * 6)
 
     def _w8(self):
         """fp8 mode: (e4m3 image, per-layer scales) for the value head's e4m3 fc1; else off"""
@@ -715,6 +746,7 @@ class HipEngine:
             idx_t = self.idx_dev
         first, xt_ready = bool(self._first_step), bool(idx is None and self._xT_valid)
         self._first_step = False
+        self._q8_step, self._q8_next = self._q8_next, self._q8_next + 1
         self._loss_dev = self.loss_sums
         return idx_t, first, xt_ready
 
@@ -812,11 +844,22 @@ class HipEngine:
         p, M = self.p, self.mb
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
                 1 if p.std_convention == "var" else 0, 1 if first else 0, part.shape[1], h, part_dw]
-        self.ext.mlp_train(self.dt, self.x_buf, idx_t, 0, M, self.wimg, self.layout, self.scales,
-                           self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
-                           self.ret, self.values_buf, self.mu_prev, self.v_prev, opts,
-                           [float(p.clip), float(p.ent_coeff)], self.tbufs, self.ldT, part, False, xt_ready,
-                           *self._w8())
+
+        def launch(q8_step):
+            self.ext.mlp_train(self.dt, self.x_buf, idx_t, 0, M, self.wimg, self.layout, self.scales,
+                               self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
+                               self.ret, self.values_buf, self.mu_prev, self.v_prev, opts,
+                               [float(p.clip), float(p.ent_coeff)], self.tbufs, self.ldT, part, False, xt_ready,
+                               *self._w8(), self.q8_amax if self.q8 else self.empty, q8_step)
+        if self.q8 and not self._q8_cal[h]:
+            # the first step of this engine: one pass as step -1 only to record the gradient maxima
+            # the step-0 scales come from (its stores and partials are overwritten by the real one;
+            # the reference loss's mu_prev / v_prev writes are idempotent)
+            launch(-1)
+            self._q8_cal[h] = True
+        launch(self._q8_step)
+        if h == 0 and idx_t is self.empty:
+            self._xT_valid = True   # the policy kernel wrote x^T of this buffer (full batch)
         if h == 0 and p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])   # train.py:164, before Adam moves it
 
@@ -833,8 +876,7 @@ class HipEngine:
         gather of the whole gradient into grad_flat (no optimizer step)"""
         self._joint_heads(idx_t, first, xt_ready)
         b = self.joint_bucket
-        self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                       b["tasks_host"], b["slab"])
+        self._wgrad(b)
         src_off, src_meta = self.joint_src
         rc, rd = self.items["joint"]
         self.ext.grad_gather(b["slab"], src_off, src_meta, self.part_joint, self.nhead_blk, self.part_joint.shape[1],
@@ -846,8 +888,7 @@ class HipEngine:
         p, M = self.p, self.mb
         self._joint_heads(idx_t, first, xt_ready)
         b = self.joint_bucket
-        self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                       b["tasks_host"], b["slab"])
+        self._wgrad(b)
         b1, b2 = p.adam_betas
         src_off, src_meta = self.joint_src
         rc, rd = self.items["joint"]
@@ -864,8 +905,7 @@ class HipEngine:
         M = self.mb
         self._head_kernel(h, idx_t, first, xt_ready, self.part_h[h], self.part_dw[h])
         b = self.buckets[h]
-        self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                       b["tasks_host"], b["slab"])
+        self._wgrad(b)
         lo, hi = self.head_range[h]
         part = self.part_h[h]
         rc, rd = self.items["policy" if h == 0 else "value"]
@@ -915,10 +955,9 @@ class HipEngine:
         self.ext.mlp_train(self.dt, self.x_buf, idx_t, 0, M, self.wimg, self.layout, self.scales,
                            self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
                            self.ret, self.values_buf, self.mu_prev, self.v_prev, opts, fopts, self.tbufs,
-                           self.ldT, self.part, False, xt_ready, self.no_u8, self.no_q)
+                           self.ldT, self.part, False, xt_ready, self.no_u8, self.no_q, self.empty, 0)
         b = self.buckets[0]
-        self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                       b["tasks_host"], b["slab"])
+        self._wgrad(b)
         if fused_apply:
             if p.loss == "dppo_ref":   # train.py:164: the pre-update log_std, before Adam moves it
                 self.log_std_old.copy_(self.model.flat.data[:self.A])

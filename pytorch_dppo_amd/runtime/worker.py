@@ -333,7 +333,11 @@ class DPPOWorker:
         return {"adam_m": eng.adam_m.detach().cpu(), "adam_v": eng.adam_v.detach().cpu(),
                 "adam_step": eng.adam_step, "obs_stats": self.stats.state_dict(),
                 "iteration": self.iteration, "env_steps": self.env_steps, "updates": self.updates,
-                "config": self.p.to_dict(), "world_size": self.ctx.world_size}
+                "config": self.p.to_dict(), "world_size": self.ctx.world_size,
+                # fp8 mode's e4m3 wgrad operands: the gradient-maxima ring the next step's delayed
+                # scales come from (a resumed run continues bit-identically)
+                **({"q8_amax": eng.q8_amax.detach().cpu(), "q8_next": eng._q8_next}
+                   if getattr(eng, "q8", False) else {})}
 
     def load_trainer_state(self, st: Dict) -> None:
         eng = self.engine
@@ -345,5 +349,9 @@ class DPPOWorker:
         self.env_steps = int(st["env_steps"])
         self.updates = int(st["updates"])
         self._stats_initialised = True
+        if getattr(eng, "q8", False) and "q8_amax" in st:
+            eng.q8_amax.copy_(st["q8_amax"].to(eng.q8_amax.device))
+            eng._q8_next = int(st["q8_next"])
+            eng._q8_cal = [True, True]
         if hasattr(eng, "params_changed"):
             eng.params_changed()
