@@ -51,7 +51,7 @@ METRIC = "env steps/sec (whole node), MuJoCo Humanoid-v2, 8 DPPO workers"
 # (8 workers).  We divide by the UPPER end (conservative).
 BASELINE_VALUE = 1.6e3
 # JSON "dtype" labels: bf16x3 IS fp32-accurate compute (split-bf16 operands, fp32 accumulate)
-DTYPE_LABEL = {"bf16x3": "fp32_3xbf16", "fp32": "fp32", "bf16": "bf16", "fp8": "fp8_e4m3_fwd+bf16_update"}
+DTYPE_LABEL = {"bf16x3": "fp32_3xbf16", "fp32": "fp32", "bf16": "bf16", "fp8": "fp8_e4m3_fwd+wgrad+bf16_update"}
 
 
 def _free_port() -> int:

@@ -262,7 +262,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
                std::vector<double> fopts, std::vector<torch::Tensor> tbufs, int64_t ldT, torch::Tensor part,
                bool check_idx, bool xT_ready, torch::Tensor w8, torch::Tensor qscale, torch::Tensor q8_amax,
                int64_t q8_step) {
-  TORCH_CHECK(dt != 2, "the update runs in bf16 when dtype=fp8 (fp8 gradients underflow e4m3)");
+  TORCH_CHECK(dt != 2, "the fp8 mode's update runs in bf16 (its e4m3 parts: the value fc1 image w8 and the wgrad operands q8_amax)");
   Layout L = parse_layout(layout);
   TORCH_CHECK(A > 0, "A");
   check(actions, "actions", at::kFloat, A);

@@ -84,8 +84,10 @@ class HipEngine:
         self.device = device
         # dtype fp8 (BASELINE config 5): the forward GEMMs of the rollout policy and of the value
         # pass run on the OCP e4m3 MFMA (v_mfma_f32_16x16x32_fp8_fp8) with per-layer weight
-        # scales; the update (loss, dgrad, wgrad) runs in bf16 because per-row gradients of
-        # magnitude ~1/batch underflow e4m3.  fp32 / bf16 use one precision throughout.
+        # scales; on the per-head path the value head's fc1 in the update and every weight-gradient
+        # GEMM (e4m3 operands with power-of-two scales, delayed per-tensor for the gradients: self.q8)
+        # too; the loss, dgrad and the rest of the update run in bf16.  fp32 / bf16 use one
+        # precision throughout.
         self.fp8 = params.dtype == "fp8"
         self.dt = native.DT_CODE["bf16"] if self.fp8 else native.DT_CODE[params.dtype]
         self.dt_fwd = native.DT_CODE[params.dtype]
