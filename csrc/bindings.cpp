@@ -408,9 +408,11 @@ void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor>
     TORCH_CHECK(nq >= 1 && kq >= 1 && nq * kq <= wmax && nq + kq <= smax, "task quadrants beyond the workgroup");
     TORCH_CHECK(t[1] >= 0 && t[2] >= 0 && t[1] % 16 == 0 && t[2] % 16 == 0, "task tile origin");
     TORCH_CHECK(t[1] + 64 * nq <= g_rows[t[0]] && t[2] + 64 * kq <= x_rows[t[0]], "task tile beyond operand rows");
-    // the kernel consumes 32-row k-steps in pairs: every range is a positive multiple of 64 rows
-    TORCH_CHECK(t[3] >= 0 && t[4] <= ld && t[4] > t[3] && (t[4] - t[3]) % 64 == 0 && t[3] % 32 == 0,
-                "task batch range (must be a positive multiple of 64 rows)");
+    // the kernel consumes 32-row k-steps in pairs (e4m3: in fours): every range is a positive
+    // multiple of 64 (128) rows
+    const int kq_rows = dt == 2 ? 128 : 64;
+    TORCH_CHECK(t[3] >= 0 && t[4] <= ld && t[4] > t[3] && (t[4] - t[3]) % kq_rows == 0 && t[3] % 32 == 0,
+                "task batch range (must be a positive multiple of 64 rows, 128 for e4m3)");
     TORCH_CHECK(t[5] >= 0, "task slab offset");
     slab_need = std::max<int64_t>(slab_need, (int64_t)t[5] + (int64_t)(64 * nq) * (64 * kq));
   }

@@ -30,13 +30,15 @@ constexpr int WG_SLOTS = 24;   // fragment slots per stage: (nq + kq) * 4 <= 24 
 // it the vmcnt arithmetic — is task-independent).  S-deep ring, counted vmcnt and a raw
 // s_barrier keep S-1 steps of DMA in flight across the barrier (cdna_hip_programming.md
 // 'Pipelining across barriers'): no VGPRs hold in-flight data.
-// bytes per operand slot: one fragment (32 batch rows of 16 features); e4m3 (DT_FP8) two
-// fragments of consecutive k-steps (64 batch rows, 1 KiB: one DMA instruction, and the pair is
-// contiguous in the FM layout), so a kernel "k-step" there covers 64 rows
+// bytes per operand slot: one fragment (32 batch rows of 16 features); e4m3 (DT_FP8) four
+// fragments of consecutive k-steps (128 batch rows, 2 KiB: two DMA instructions; they are
+// contiguous in the FM layout), one v_mfma_scale_f32_16x16x128_f8f6f4 per tile pair — twice the
+// bf16 MFMA rate — so a kernel "k-step" there covers 128 rows
 template <int DT>
-constexpr int wgrad_frag_bytes() { return DT == DT_FP8 ? 1024 : 512 * Prec<DT>::BYTES; }
+constexpr int wgrad_frag_bytes() { return DT == DT_FP8 ? 2048 : 512 * Prec<DT>::BYTES; }
 template <int DT>
-constexpr int wgrad_step_rows() { return DT == DT_FP8 ? 64 : 32; }
+constexpr int wgrad_step_rows() { return DT == DT_FP8 ? 128 : 32; }
+typedef __attribute__((ext_vector_type(8))) int i32x8;
 template <int DT, int S>
 constexpr size_t wgrad_lds_bytes() { return (size_t)S * WG_SLOTS * wgrad_frag_bytes<DT>(); }
 
@@ -100,24 +102,28 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
       const char* st = smem + (k % S) * SB;
       Frag af[4], bf[4];
       if constexpr (DT == DT_FP8) {
-        // two e4m3 k-steps per slot: lane l's 8 bytes of k-step 2kk at l * 8, of 2kk + 1 512 on
-        long a0[4], a1[4], b0[4], b1[4];
+        // four e4m3 k-steps per slot: lane l's 8 bytes of k-step 4kk + j at j * 512 + l * 8.  The
+        // 16x16x128 operand of lane l is those 32 bytes in j order — rows {32 j + 8 (l >> 4) + e}
+        // for BOTH operands, so the MFMA's k sum runs over every row of the 128 exactly once
+        // (E8M0 scales 127 = 1: the power-of-two operand scales are undone in the epilogue)
+        auto rd = [&](int f) {
+          const char* p = st + f * FB + lane * 8;
+          const long x0 = *reinterpret_cast<const long*>(p), x1 = *reinterpret_cast<const long*>(p + 512);
+          const long x2 = *reinterpret_cast<const long*>(p + 1024), x3 = *reinterpret_cast<const long*>(p + 1536);
+          return i32x8{(int)x0, (int)(x0 >> 32), (int)x1, (int)(x1 >> 32), (int)x2, (int)(x2 >> 32), (int)x3,
+                       (int)(x3 >> 32)};
+        };
+        i32x8 a8[4], b8[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const char* pa = st + (wn * 4 + i) * FB + lane * 8;
-          const char* pb = st + (NF + wk * 4 + i) * FB + lane * 8;
-          a0[i] = *reinterpret_cast<const long*>(pa);
-          a1[i] = *reinterpret_cast<const long*>(pa + 512);
-          b0[i] = *reinterpret_cast<const long*>(pb);
-          b1[i] = *reinterpret_cast<const long*>(pb + 512);
+          a8[i] = rd(wn * 4 + i);
+          b8[i] = rd(NF + wk * 4 + i);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a0[i], b0[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a1[i], b1[j], acc[i][j], 0, 0, 0);
-          }
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8[i], b8[j], acc[i][j], 0, 0, 0, 127, 0, 127);
         continue;
       }
       auto lds_frag = [&](int f) {
@@ -168,7 +174,7 @@ __global__ __launch_bounds__(WG_WAVES * 64) void wgrad_kernel(WgradArgs a) {
   else wgrad_lds_body<DT, S, 3>(a, tk, smem);
 }
 
-// ring depth: fp32 and split-bf16 3 stages (144 KiB), bf16 and e4m3 4 (96 KiB)
+// ring depth: fp32, split-bf16 and e4m3 3 stages (144 KiB), bf16 4 (96 KiB)
 template <int DT, int S>
 void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
   const size_t lds = wgrad_lds_bytes<DT, S>();
@@ -220,7 +226,7 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
   if (a.ntasks <= 0) return;
   if (dt == DT_F32) launch_wgrad_lds<DT_F32, 3>(a, s);
   else if (dt == DT_S3) launch_wgrad_lds<DT_S3, 3>(a, s);
-  else if (dt == DT_FP8) launch_wgrad_lds<DT_FP8, 4>(a, s);
+  else if (dt == DT_FP8) launch_wgrad_lds<DT_FP8, 3>(a, s);
   else launch_wgrad_lds<DT_BF16, 4>(a, s);
   HIP_CHECK_LAUNCH();
 }

@@ -71,7 +71,23 @@ class DistContext:
         """create the in-stream RCCL communicator (RCCL groups only; DPPO_NATIVE_COMM=0: off)"""
         if (self.native is None and self.enabled and self.backend == "nccl" and self.device.type == "cuda"
                 and os.environ.get("DPPO_NATIVE_COMM", "1") != "0" and hasattr(ext, "comm_init")):
-            self.native = NativeComm(ext, self.rank, self.world_size)
+            # every rank must take the same path (a rank on the process group and another on the
+            # native communicator would never meet in a collective): a rank whose communicator
+            # fails reports it and ALL ranks fall back to the process group's collectives
+            nat, err = None, None
+            try:
+                nat = NativeComm(ext, self.rank, self.world_size)
+            except Exception as e:   # noqa: BLE001 — the fallback is collective, the cause is printed
+                err = e
+            ok = torch.tensor([0.0 if nat is None else 1.0], device=self.device)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if ok.item() == 1.0:
+                self.native = nat
+            else:
+                if nat is not None:
+                    nat.destroy()
+                print(f"[dppo rank {self.rank}] native RCCL communicator unavailable "
+                      f"({err if err is not None else 'on another rank'}); using the process group", flush=True)
         return self.native is not None
 
     def grad_allreduce_fn(self, mean: bool = False):

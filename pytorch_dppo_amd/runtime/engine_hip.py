@@ -329,7 +329,8 @@ class HipEngine:
             tasks, tile_off, base = [], {}, 0
             for t, n in zip(tiles, nch):
                 size = t[3] * t[4] * 64 * 64
-                mc = _r(-(-self.ldT // n), 64)        # even number of 32-row k-steps per task
+                # even number of 32-row k-steps per task (e4m3: a multiple of 4)
+                mc = _r(-(-self.ldT // n), 128 if getattr(self, "q8", False) else 64)
                 chunks = [(c0, min(c0 + mc, self.ldT)) for c0 in range(0, self.ldT, mc)]
                 tile_off[t] = (base, len(chunks), size)
                 for ci, (m0, m1) in enumerate(chunks):

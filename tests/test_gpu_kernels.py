@@ -540,6 +540,37 @@ def test_rccl_world1_allreduce_and_training_step():
         ctx.destroy()
 
 
+def test_native_comm_failure_falls_back_to_process_group(monkeypatch):
+    """A rank whose native RCCL communicator cannot be created (here: comm_init raises) makes
+    every rank fall back to the process group's collectives (one MIN all-reduce of the outcome):
+    the worker trains through ProcessGroupNCCL instead of failing or hanging a 2-path world."""
+    from pytorch_dppo_amd.parallel.dist import init_single_rank_collective
+    from pytorch_dppo_amd.runtime.launcher import free_port
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    ext = _ext()
+
+    class Broken:
+        def __getattr__(self, k):
+            if k == "comm_init":
+                def fail(*a):
+                    raise RuntimeError("RCCL ncclCommInitRank failed: test")
+                return fail
+            return getattr(ext, k)
+    ctx = init_single_rank_collective(DEV, port=free_port())
+    ctx.force_collectives = True
+    try:
+        assert ctx.init_native_comm(Broken()) is False and ctx.native is None
+        p = dppo_preset(device="gpu", env_name="Walker2d-v2", num_envs=64, exploration_size=64 * 4,
+                        batch_size=128, num_epoch=2, dtype="bf16")
+        monkeypatch.setenv("DPPO_NATIVE_COMM", "0")   # (the worker's own attempt would succeed)
+        w = DPPOWorker(p, ctx)
+        assert ctx.native is None
+        m = w.iteration_step()
+        assert math.isfinite(m["loss"]) and m["updates"] == 4
+    finally:
+        ctx.destroy()
+
+
 @pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("native", [False, True])
 def test_head_chains_through_rccl_bit_identical_to_fused(overlap, native, monkeypatch):

@@ -42,13 +42,14 @@ def test_humanoid_value_fc1_streams_fewer_rows_than_square_tiles():
     assert rows_per_step == 2304 and rows_per_step < square
 
 
-@pytest.mark.parametrize("heads", [False, True])
+@pytest.mark.parametrize("heads,q8", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("env", ["Humanoid-v2", "HalfCheetah-v2"])
-def test_plan_tasks_cover_tiles_and_batch_once(env, heads):
+def test_plan_tasks_cover_tiles_and_batch_once(env, heads, q8):
     """The full task list (HipEngine._build_wgrad_plan run on a CPU stand-in): each output tile's
     tasks cover the batch rows [0, ldT) exactly once with 64-row-aligned chunks, every task owns
     a disjoint slab region, the task count is ~one per CU, and every parameter's gather entry
-    (offset, chunk count, stride) matches its tile."""
+    (offset, chunk count, stride) matches its tile.  q8 (fp8 mode's e4m3 wgrad): 128-row chunks
+    (the kernel's 16x16x128 MFMA consumes four 32-row k-steps at a time)."""
     from types import SimpleNamespace
     from pytorch_dppo_amd.envs import get_spec
     from pytorch_dppo_amd.models.actor_critic import ActorCritic
@@ -57,7 +58,7 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads):
     spec = get_spec(env)
     model = ActorCritic(spec.obs_dim, spec.act_dim)
     stub = SimpleNamespace(L=model.packed_layout(), ldT=65536, A=spec.act_dim, device=torch.device("cpu"),
-                           heads=heads, head_range=[model.head_ranges["policy"], model.head_ranges["value"]],
+                           heads=heads, q8=q8, head_range=[model.head_ranges["policy"], model.head_ranges["value"]],
                            _slab_index=HipEngine._slab_index, _slab_runs=HipEngine._slab_runs)
     HipEngine._build_wgrad_plan(stub, model, target_wgs=256)
     total = 0
@@ -68,7 +69,8 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads):
         used = torch.zeros(b["slab"].numel(), dtype=torch.int32)
         rows = {}
         for (li, n0, k0, m0, m1, off, nq, kq) in t:
-            assert m0 % 64 == 0 and (m1 - m0) % 64 == 0 and 0 <= m0 < m1 <= stub.ldT
+            al = 128 if q8 else 64
+            assert m0 % al == 0 and (m1 - m0) % al == 0 and 0 <= m0 < m1 <= stub.ldT
             used[off:off + 64 * nq * 64 * kq] += 1
             rows.setdefault((li, n0, k0), []).append((m0, m1))
         assert bool((used == 1).all())
