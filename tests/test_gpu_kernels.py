@@ -1129,6 +1129,50 @@ def test_fp8_e4m3_wgrad_operands_match_bf16_operands(monkeypatch):
             (name, stored, e, amax[1, kk].item())
 
 
+@pytest.mark.parametrize("case", ["ppo_minibatch_clip", "dppo_ref"])
+def test_fp8_e4m3_operands_on_other_update_paths(case, monkeypatch):
+    """The e4m3 wgrad operands on the other per-head update paths: an index-gathered minibatch of
+    half the buffer with global-norm clipping (ppo preset: the policy kernel writes x^T of the
+    gathered rows every step), and the reference DPPO loss (mu_prev / v_prev writes, also in the
+    calibration pass).  Per-layer gradients within 5 % of the bf16-operand path, two full steps
+    finite and the replicated parameters moving."""
+    E, T = 2048, 32
+    if case == "ppo_minibatch_clip":
+        p = ppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=E, exploration_size=E * T,
+                       batch_size=E * T // 2, dtype="fp8")
+    else:
+        p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=E, exploration_size=E * T // 2,
+                        batch_size=E * T // 2, dtype="fp8", loss="dppo_ref", std_convention="var")
+    monkeypatch.setenv("DPPO_HEADS", "1")
+    engs = {}
+    for q8 in ("1", "0"):
+        monkeypatch.setenv("DPPO_Q8", q8)
+        e, m, _, _ = _engine(p)
+        assert e.heads and e.q8 == (q8 == "1")
+        e.refresh_fwd_image()
+        _fill_buffer(e, m, gen_seed=9)
+        engs[q8] = (e, m)
+    g = torch.Generator(device="cpu").manual_seed(4)
+    idx = None if case == "dppo_ref" else torch.randperm(engs["1"][0].N, generator=g)[:engs["1"][0].mb].to(DEV)
+    for q8, (e, m) in engs.items():
+        e.begin_update()
+        e.grad(idx)
+    torch.cuda.synchronize()
+    (eq, mq), (eb, _) = engs["1"], engs["0"]
+    for name in ("p_fc1", "p_fc2", "v_fc1", "v_fc2"):
+        o, n = mq.offsets[f"{name}.weight"]
+        gb = eb.grad_flat[o:o + n]
+        err = (eq.grad_flat[o:o + n] - gb).norm().item() / (gb.norm().item() + 1e-12)
+        assert err < 0.05, (case, name, err)
+    p0 = mq.flat.data.clone()
+    for _ in range(2):
+        eq.step(idx)
+    eq.finish_steps()
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(mq.flat.data).all()) and not torch.equal(p0, mq.flat.data)
+    assert float(eq.q8_maxima().max()) > 0
+
+
 @pytest.mark.parametrize("heads", ["1", "0"])
 @pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
 def test_update_reads_rows_past_2gib_of_the_observation_buffer(dtype, heads, monkeypatch):
