@@ -184,6 +184,7 @@ class HipEngine:
         self.part_joint = torch.zeros(self.nhead_blk, np_pol + 128, **f32)
         self.part_dw_joint = [self.part_dw[0], np_pol]
         self.head_range = [model.head_ranges["policy"], model.head_ranges["value"]]
+        self.head_order = (0, 1)     # launch order of the joint head kernels (A/B: scripts/ab_iter.py)
         if os.environ.get("DPPO_MLP_ROWS"):     # diagnostics: force the fused-kernel row tile
             self.ext.set_mlp_rows(int(os.environ["DPPO_MLP_ROWS"]))
         self.sync_tile()
@@ -871,7 +872,7 @@ class HipEngine:
         stream order.  (Measured: the policy kernel on a side stream concurrent with the value
         kernel, joined before the wgrad: 4.57 vs 4.39 ms per iteration, same box — each kernel
         fills a CU's LDS, so they only time-slice the CUs and the stream hand-offs are extra.)"""
-        for h in (0, 1):
+        for h in self.head_order:
             self._head_kernel(h, idx_t, first, xt_ready, self.part_joint, self.part_dw_joint[h])
 
     def _joint_grad(self, idx_t, first: bool, xt_ready: bool) -> None:

@@ -49,6 +49,7 @@ def main():
         "A": lambda: use_ext("A"), "B": lambda: use_ext("b"), "C": lambda: use_ext("c"),
         "x_cached": lambda: ext.set_x_stream(0), "x_stream": lambda: ext.set_x_stream(1),
         "s3w8": lambda: ext.set_s3_train_waves(8), "s3w4": lambda: ext.set_s3_train_waves(4),
+        "pv": lambda: setattr(w.engine, "head_order", (0, 1)), "vp": lambda: setattr(w.engine, "head_order", (1, 0)),
     }
     for _ in range(2):
         w.iteration_step()
