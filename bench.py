@@ -6,9 +6,15 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 Both forms run N ranks: without a torchrun world (no WORLD_SIZE) and N > 1 the first form
-starts the N ranks itself as a child torch.distributed.run tree and exits with its status; under
-torchrun WORLD_SIZE must equal --gpus and every local rank needs its own GPU (RCCL), else the
-bench exits non-zero instead of reporting a different world as N GPUs.
+starts the N ranks itself as a child torch.distributed.run tree and exits with its status (the
+parent makes no HIP call at all: the ranks check the devices); under torchrun WORLD_SIZE must
+equal --gpus and every local rank needs its own GPU (RCCL), else the bench exits non-zero
+instead of reporting a different world as N GPUs.
+
+Multi-rank runs use the in-stream gradient all-reduce (csrc/comm.cpp: the native RCCL
+communicator on the compute stream, bounded by --dist-timeout-s with ncclCommAbort on a dead
+peer) and the per-rank heartbeat; ``--dist-backend gloo`` runs the same engine branch for ranks
+that share one GPU (the 1-GPU box's rehearsal of the N-GPU path).
 
 One DPPO worker per GPU (one process per GPU, RCCL over xGMI).  A *step* is one full DPPO
 iteration of the reference algorithm on every worker (train.py:60-178 + chief.py):
@@ -45,6 +51,7 @@ import torch.distributed as dist  # noqa: E402
 from pytorch_dppo_amd.config import dppo_preset  # noqa: E402
 from pytorch_dppo_amd.parallel.dist import init_distributed, init_single_rank_collective  # noqa: E402
 from pytorch_dppo_amd.runtime.worker import DPPOWorker  # noqa: E402
+from pytorch_dppo_amd.utils.heartbeat import start_heartbeat  # noqa: E402
 
 METRIC = "env steps/sec (whole node), MuJoCo Humanoid-v2, 8 DPPO workers"
 # BASELINE.md derived estimate for the reference on this metric: 0.8-1.6e3 steps/s per node
@@ -76,17 +83,16 @@ def launch_ranks(n: int, argv) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def check_world(gpus: int) -> None:
+def check_world(gpus: int, backend: str) -> None:
     """a torchrun world must be the one --gpus names, with a device per local rank (RCCL: one
-    process per GPU).  ``DPPO_DIST_BACKEND=gloo`` (diagnostics: ranks sharing one GPU) skips the
-    device count."""
+    process per GPU).  ``--dist-backend gloo`` (ranks sharing one GPU) skips the device count."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != gpus:
         raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {gpus}: refusing to report a "
                          f"{world}-rank run as {gpus} GPUs")
     local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     ndev = torch.cuda.device_count()
-    if os.environ.get("DPPO_DIST_BACKEND", "nccl") == "nccl" and ndev < local:
+    if backend != "gloo" and ndev < local:
         raise SystemExit(f"bench: {local} local ranks but only {ndev} visible GPU(s) (RCCL needs one "
                          f"process per GPU)")
 
@@ -116,25 +122,34 @@ def main():
                          "each timed event record idles the GPU ~10 us)")
     ap.add_argument("--verify-sync", action="store_true",
                     help="after the timed steps, check every rank holds bit-identical parameters")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="auto/nccl: RCCL, one rank per GPU; gloo: ranks sharing one GPU (rehearsal of the "
+                         "multi-rank engine path on a 1-GPU box)")
+    ap.add_argument("--grad-comm", default="auto", choices=["auto", "native", "process_group"],
+                    help="gradient all-reduce: in-stream communicator (auto/native) or torch's process group")
+    ap.add_argument("--dist-timeout-s", type=float, default=300.0,
+                    help="bound of every wait on peers (collective watchdog; abort + non-zero exit)")
+    ap.add_argument("--heartbeat-timeout-s", type=float, default=60.0)
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # the N-GPU node run from a plain `python bench.py --gpus N`: N child ranks, this process
-        # exits with their status (it never initialises the GPU itself)
-        ndev = torch.cuda.device_count()
-        if os.environ.get("DPPO_DIST_BACKEND", "nccl") == "nccl" and ndev < args.gpus:
-            raise SystemExit(f"bench: --gpus {args.gpus} but only {ndev} visible GPU(s)")
+        # exits with their status.  It makes no HIP call at all — not even a device count: the
+        # ranks check the visible devices themselves (check_world) and fail the run if short.
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
-    check_world(args.gpus)
+    check_world(args.gpus, args.dist_backend)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
-        ctx = init_distributed("gpu")
+        ctx = init_distributed("gpu", timeout_s=args.dist_timeout_s, backend=args.dist_backend,
+                               grad_comm=args.grad_comm)
     else:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        ctx = init_single_rank_collective(dev, port=int(os.environ.get("MASTER_PORT", "29561")))
+        ctx = init_single_rank_collective(dev, port=int(os.environ.get("MASTER_PORT", "29561")),
+                                          timeout_s=args.dist_timeout_s, grad_comm=args.grad_comm)
     ctx.force_collectives = args.force_collectives
+    hb = start_heartbeat(ctx, 5.0, args.heartbeat_timeout_s)   # None at world size 1
     E, T = args.num_envs, args.rollout_len
     rows = E * T
 
@@ -143,6 +158,8 @@ def main():
         p = dppo_preset(device="gpu", env_name=args.env_name, num_envs=E, exploration_size=rows,
                         batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=dtype,
                         num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
+                        dist_backend=args.dist_backend, grad_comm=args.grad_comm,
+                        dist_timeout_s=args.dist_timeout_s,
                         phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
         w = DPPOWorker(p, ctx)
         m = {}
@@ -152,7 +169,7 @@ def main():
                 print(dtype, "warmup", i, json.dumps({k: round(v, 4) if isinstance(v, float) else v
                                                       for k, v in m.items()}), file=sys.stderr, flush=True)
         ctx.barrier()
-        torch.cuda.synchronize()
+        ctx.sync()                 # torch.cuda.synchronize, bounded by the collective watchdog
         t0 = time.perf_counter()
         # the production loop (run_worker): each iteration's metrics are read one iteration later,
         # so the host enqueues the next rollout while the device still runs this update.  Every
@@ -163,7 +180,7 @@ def main():
                 print(dtype, "step", i, json.dumps({k: round(v, 4) if isinstance(v, float) else v
                                                     for k, v in mi.items()}), file=sys.stderr, flush=True)
         ctx.barrier()
-        torch.cuda.synchronize()
+        ctx.sync()
         el = torch.tensor([time.perf_counter() - t0], device=ctx.device, dtype=torch.float64)
         m = w.finish_metrics() or m
         if args.verify_sync:
@@ -176,12 +193,19 @@ def main():
         return float(el.item()), p, w, m
 
     elapsed, p, w, m = run(args.dtype)
+    if ctx.rank == 0 and ctx.world_size > 1:
+        print(f"bench: grad_allreduce {'in_stream' if ctx.native is not None else 'process_group'} "
+              f"backend {ctx.backend} world {ctx.world_size}", file=sys.stderr, flush=True)
     total_steps = rows * ctx.world_size * args.steps
     value = total_steps / elapsed
     heads = bool(getattr(w.engine, "heads", False))
-    # the gradient all-reduce in use: native RCCL on the compute stream (csrc/comm.cpp), the
-    # process group's (per-head chains), or none (world size 1, not forced)
-    grad_ar = ("rccl_in_stream" if ctx.native is not None else "process_group") if ctx.collective else "none"
+    # the gradient all-reduce in use: native RCCL on the compute stream (csrc/comm.cpp), the gloo
+    # adapter of the same in-stream engine branch, the process group's (per-head chains), or none
+    # (world size 1, not forced)
+    grad_ar = "none"
+    if ctx.collective:
+        grad_ar = ("process_group" if ctx.native is None else
+                   "rccl_in_stream" if ctx.backend == "nccl" else "gloo_in_stream")
     del w
     variants = {}
     for dt in [d for d in args.variants.split(",") if d and d != args.dtype]:
@@ -205,6 +229,11 @@ def main():
                           "rollout_len": T, "num_epoch": args.num_epoch,
                           "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout,
                           "per_head_kernels": heads, "grad_allreduce": grad_ar,
+                          # --overlap-rollout on the in-stream path: the last value-head all-reduce +
+                          # Adam run on a side stream (second communicator) beside the next rollout
+                          "overlap_value_step": ("side_stream" if args.overlap_rollout and ctx.native_side is not None
+                                                 else "pending_work" if args.overlap_rollout and ctx.collective
+                                                 else "none"),
                           "note": ("value = total env steps/s of all n_gpus workers (one DPPO worker per GPU); "
                                    "the 8-worker node figure of the metric is the n_gpus=8 run; vs_baseline "
                                    "divides by the reference's derived 8-worker CPU node estimate (BASELINE.md)"),
@@ -212,6 +241,8 @@ def main():
                                                           "ms_update", "ms_obs_stats") if k in m}},
                "variants": variants}
         print(json.dumps(out), flush=True)
+    if hb is not None:
+        hb.stop()
     ctx.destroy()
 
 

@@ -81,11 +81,25 @@ class Params:
     log_csv: str = ""                    # learning-curve CSV (rank 0), the figs/*.png analogue
     profile_dir: str = ""                # torch.profiler chrome traces (host + HIP timeline) per rank
     profile_iters: str = "2:4"           # [start:stop) iterations captured when profile_dir is set
-    heartbeat_s: float = 0.0             # >0: per-rank heartbeat in the rendezvous store every N s
-    heartbeat_timeout_s: float = 120.0   # a peer silent this long is reported dead and this rank exits
+    heartbeat_s: float = -1.0            # per-rank heartbeat in the rendezvous store every N s (<0: auto =
+                                         # 5 s whenever world_size > 1; 0: off)
+    heartbeat_timeout_s: float = 60.0    # a peer silent this long is reported dead: abort + exit 75
     check_finite: bool = False           # debug: stop with the failing phase when loss/params go non-finite
     phase_timing: int = 1                # per-phase HIP-event timing every N iterations (0 = off; each
                                          # event record idles the GPU ~10 us, see PhaseTimer)
+    # ---- execution options (the GPU engine's paths; A/B switches of earlier rounds) ----------
+    dist_backend: str = "auto"           # auto: nccl (RCCL) on gpu, gloo on cpu | nccl | gloo (GPU ranks
+                                         # sharing one device: the 1-GPU box's multi-rank runs)
+    grad_comm: str = "auto"              # auto: in-stream communicator when available (csrc/comm.cpp RCCL;
+                                         # gloo adapter) | native (required) | process_group (torch's)
+    update_kernels: str = "auto"         # auto | heads (per-head streaming kernels, csrc/mlp_head.hip) |
+                                         # tile (one-kernel update, csrc/mlp.hip)
+    fused_apply: bool = True             # world size 1: gradient gather + Adam in one launch
+    fp8_wgrad_operands: bool = True      # dtype fp8 on the per-head path: e4m3 wgrad operands (else bf16)
+    stats_stream: str = "off"            # off | on | auto (on when an all-reduce sits in the chain): the
+                                         # obs-stat reduce / all-reduce / merge on a side stream
+    wgrad_wgs: int = 0                   # wgrad tasks per launch (0: one per CU of the device)
+    mlp_rows: int = 0                    # diagnostics: force the tile update kernel's row tile (0: auto)
 
     # ------------------------------------------------------------------------------------
     def __post_init__(self):
@@ -119,6 +133,16 @@ class Params:
             self.std_convention = "var"
         if self.obs_norm_update not in ("step", "rollout"):
             raise ValueError("obs_norm_update must be step|rollout")
+        for name, ok in (("dist_backend", ("auto", "nccl", "gloo")), ("grad_comm", ("auto", "native", "process_group")),
+                         ("update_kernels", ("auto", "heads", "tile")), ("stats_stream", ("off", "on", "auto"))):
+            if getattr(self, name) not in ok:
+                raise ValueError(f"{name} must be {'|'.join(ok)}, got {getattr(self, name)}")
+
+    def heartbeat_interval(self, world_size: int) -> float:
+        """the heartbeat period in effect: heartbeat_s, or 5 s (auto) whenever there are peers"""
+        if self.heartbeat_s >= 0:
+            return float(self.heartbeat_s)
+        return 5.0 if world_size > 1 else 0.0
 
     # alias with the correct spelling
     @property

@@ -25,8 +25,11 @@ overlap design that needed them; profiles/r3/rccl_forced_vs_plain.md).
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
+import sys
+import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -34,25 +37,104 @@ import torch
 import torch.distributed as dist
 
 
+class CollectiveError(RuntimeError):
+    """a hot-path collective failed or timed out (dead / hung peer); the communicators are aborted"""
+
+
 class NativeComm:
     """RCCL communicator over the process group's ranks, collectives on a caller-named stream
-    (default: the current one).  Created collectively: rank 0's ncclUniqueId is broadcast over
-    the existing group."""
+    (default: the current one), ``csrc/comm.cpp``.  Non-blocking underneath: creation and a
+    stalled enqueue are bounded by ``timeout_s`` (then aborted); ``status()`` is the asynchronous
+    error state the host wait loops poll (:meth:`DistContext.wait_event`)."""
+    in_stream = True
 
-    def __init__(self, ext, rank: int, world_size: int):
-        idb = [ext.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(idb, src=0)
+    def __init__(self, ext, handle: int, world_size: int):
         self.ext = ext
         self.world_size = world_size
-        self.handle = ext.comm_init(idb[0], world_size, rank)
+        self.handle = handle
 
-    def allreduce_(self, t: torch.Tensor, mean: bool = False) -> None:
-        self.ext.comm_allreduce(self.handle, t, mean)
+    @classmethod
+    def create(cls, ext, rank: int, world_size: int, timeout_s: float,
+               device: Optional[torch.device] = None) -> Optional["NativeComm"]:
+        """Collective over the default group.  Rank 0 ALWAYS takes part in the id broadcast — it
+        sends an error token when it cannot make an id — so a failure on any rank is seen by all:
+        every rank returns None together (after a MIN all-reduce of the outcome) or every rank
+        returns a communicator."""
+        token = [None]
+        if rank == 0:
+            try:
+                token[0] = ext.comm_unique_id()
+            except Exception as e:   # noqa: BLE001 — the error travels in the token
+                token[0] = ("error", f"{type(e).__name__}: {e}")
+        dist.broadcast_object_list(token, src=0)
+        tok = token[0]
+        if isinstance(tok, tuple):
+            print(f"[dppo rank {rank}] native RCCL communicator unavailable (rank 0: {tok[1]}); "
+                  f"using the process group", flush=True)
+            return None
+        handle, err = None, None
+        try:
+            handle = ext.comm_init(tok, world_size, rank, float(timeout_s))   # bounded (comm.cpp)
+        except Exception as e:   # noqa: BLE001 — the fallback is collective, the cause is printed
+            err = e
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        ok = torch.tensor([0.0 if handle is None else 1.0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok.item() == 1.0:
+            return cls(ext, handle, world_size)
+        if handle is not None:
+            ext.comm_abort(handle)
+        print(f"[dppo rank {rank}] native RCCL communicator unavailable "
+              f"({err if err is not None else 'on another rank'}); using the process group", flush=True)
+        return None
+
+    def allreduce_(self, t: torch.Tensor, mean: bool = False, stream: Optional[torch.cuda.Stream] = None) -> None:
+        self.ext.comm_allreduce(self.handle, t, mean, 0 if stream is None else stream.cuda_stream)
+
+    def status(self) -> int:
+        """0 ok, 7 in progress, -1 aborted / destroyed, else an RCCL error code"""
+        return int(self.ext.comm_status(self.handle)) if self.handle is not None else -1
+
+    def abort(self) -> None:
+        if self.handle is not None:
+            self.ext.comm_abort(self.handle)
 
     def destroy(self) -> None:
         if self.handle is not None:
-            self.ext.comm_destroy(self.handle)
-            self.handle = None
+            h, self.handle = self.handle, None
+            if self.ext.comm_status(h) == -1:
+                return                      # aborted: nothing to finalise
+            self.ext.comm_destroy(h)
+
+
+class GlooStreamComm:
+    """The native communicator's interface on a gloo group: the in-stream (production) engine
+    branch for ranks that SHARE one GPU (RCCL refuses two ranks on one device), so 2-rank runs
+    on the 1-GPU box take the exact code path an N-GPU RCCL run takes — joint kernels → gather →
+    all-reduce → whole-vector Adam, and the side-stream value step of ``--overlap-rollout``.
+    gloo copies device tensors through the host and its wait blocks: stream order is kept, only
+    the overlap is not real.  ``mean``: the sum, then a stream-ordered scale (ncclAvg's result)."""
+    in_stream = True
+
+    def __init__(self, world_size: int):
+        self.world_size = world_size
+        self.handle = 0
+
+    def allreduce_(self, t: torch.Tensor, mean: bool = False, stream: Optional[torch.cuda.Stream] = None) -> None:
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        with ctx:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            if mean:
+                t.mul_(1.0 / self.world_size)
+
+    def status(self) -> int:
+        return 0
+
+    def abort(self) -> None:
+        pass
+
+    def destroy(self) -> None:
+        pass
 
 
 @dataclass
@@ -65,45 +147,119 @@ class DistContext:
     # run the hot-path collectives even at world size 1, where a sum over one rank is the
     # identity (tests use it to exercise the real RCCL call on the 1-GPU box)
     force_collectives: bool = False
-    native: Optional[NativeComm] = None
+    # the in-stream communicator of the hot path (NativeComm on RCCL, GlooStreamComm on a gloo
+    # group of GPU ranks) and the second one the side-stream value step of --overlap-rollout uses
+    # (two communicators: their collectives may run concurrently on different streams)
+    native: Optional[object] = None
+    native_side: Optional[object] = None
+    timeout_s: float = 300.0             # Params.dist_timeout_s: the bound of every wait on peers
+    grad_comm: str = "auto"              # Params.grad_comm: auto | native | process_group
 
-    def init_native_comm(self, ext) -> bool:
-        """create the in-stream RCCL communicator (RCCL groups only; DPPO_NATIVE_COMM=0: off)"""
-        if (self.native is None and self.enabled and self.backend == "nccl" and self.device.type == "cuda"
-                and os.environ.get("DPPO_NATIVE_COMM", "1") != "0" and hasattr(ext, "comm_init")):
-            # every rank must take the same path (a rank on the process group and another on the
-            # native communicator would never meet in a collective): a rank whose communicator
-            # fails reports it and ALL ranks fall back to the process group's collectives
-            nat, err = None, None
-            try:
-                nat = NativeComm(ext, self.rank, self.world_size)
-            except Exception as e:   # noqa: BLE001 — the fallback is collective, the cause is printed
-                err = e
-            ok = torch.tensor([0.0 if nat is None else 1.0], device=self.device)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if ok.item() == 1.0:
-                self.native = nat
-            else:
-                if nat is not None:
-                    nat.destroy()
-                print(f"[dppo rank {self.rank}] native RCCL communicator unavailable "
-                      f"({err if err is not None else 'on another rank'}); using the process group", flush=True)
+    def init_native_comm(self, ext, side: bool = False) -> bool:
+        """create the in-stream communicator(s) (collective: every rank calls it).  RCCL groups:
+        NativeComm (bounded, collective-safe creation; on failure every rank falls back to the
+        process group together unless grad_comm == "native").  gloo groups of GPU ranks:
+        GlooStreamComm.  ``side``: also the side-stream communicator."""
+        if self.native is not None or not self.enabled or self.device.type != "cuda" or self.grad_comm == "process_group":
+            return self.native is not None
+        if self.backend == "gloo":
+            self.native = GlooStreamComm(self.world_size)
+            self.native_side = GlooStreamComm(self.world_size) if side else None
+        elif self.backend == "nccl" and hasattr(ext, "comm_init"):
+            self.native = NativeComm.create(ext, self.rank, self.world_size, self.timeout_s, self.device)
+            if self.native is not None and side:
+                self.native_side = NativeComm.create(ext, self.rank, self.world_size, self.timeout_s, self.device)
+        if self.native is None and self.grad_comm == "native":
+            raise RuntimeError("grad_comm=native but the native communicator could not be created")
         return self.native is not None
 
     def grad_allreduce_fn(self, mean: bool = False):
         """the engines' hot-path all-reduce callback for the flat gradient: None when no collective
-        runs; on a native communicator an in-stream sum/mean (attribute ``in_stream``), else the
-        async process-group all-reduce returning its work handle (the engine scales for mean)."""
+        runs; on an in-stream communicator ``ar(t, stream=None)`` — a stream-ordered sum/mean on the
+        current stream, or on ``stream`` through the side communicator (attributes ``in_stream``,
+        ``side``: a side communicator exists) — else the async process-group all-reduce returning
+        its work handle (the engine scales for mean)."""
         if not self.collective:
             return None
         if self.native is not None:
-            nat = self.native
+            nat, side = self.native, self.native_side
 
-            def ar(t):
-                nat.allreduce_(t, mean)
+            def ar(t, stream=None):
+                (nat if stream is None else side).allreduce_(t, mean, stream)
             ar.in_stream = True
+            ar.side = side is not None
             return ar
         return lambda t: self.allreduce_grads(t, async_op=True)
+
+    # -- failure detection (SURVEY §5.3) ------------------------------------------------------
+    def _comms(self):
+        return [c for c in (self.native, self.native_side) if c is not None]
+
+    def comm_error(self) -> Optional[str]:
+        """the first asynchronous error of the in-stream communicators, or None"""
+        for c in self._comms():
+            st = c.status()
+            if st not in (0, 7):
+                return f"RCCL communicator state {st}" if st != -1 else "communicator aborted"
+        return None
+
+    def abort(self, reason: str = "") -> None:
+        """abort every communicator of this rank (their kernels exit: nothing stays spinning on
+        the GPU for a dead peer) — called before a rank gives up on its peers"""
+        if reason:
+            print(f"[dppo rank {self.rank}] aborting collectives: {reason}", file=sys.stderr, flush=True)
+        for c in self._comms():
+            try:
+                c.abort()
+            except Exception:   # noqa: BLE001 — best effort on the way out
+                pass
+        if self.backend == "nccl" and self.enabled:
+            try:
+                from torch.distributed.distributed_c10d import _abort_process_group
+                _abort_process_group()
+            except Exception:   # noqa: BLE001
+                pass
+
+    def wait_event(self, ev, timeout_s: Optional[float] = None) -> None:
+        """Host wait for a device event that may sit behind in-stream collectives: the
+        communicators' watchdog.  Polls the event and ncclCommGetAsyncError; an asynchronous
+        error, or no completion within ``timeout_s`` (default dist_timeout_s), aborts the
+        communicators (ncclCommAbort) and raises CollectiveError — the reference's dead-worker
+        deadlock (chief.py:13, Q21) becomes a non-zero exit."""
+        if ev is None:
+            return
+        if not self._comms():
+            ev.synchronize()
+            return
+        to = self.timeout_s if timeout_s is None else float(timeout_s)
+        t0 = time.monotonic()
+        n = 0
+        while not ev.query():
+            n += 1
+            if n % 64 == 0:
+                err = self.comm_error()
+                if err is not None:
+                    self.abort(err)
+                    raise CollectiveError(f"rank {self.rank}: {err}")
+                el = time.monotonic() - t0
+                if el > to:
+                    msg = f"rank {self.rank}: device work behind the collectives did not complete in {to:.0f} s"
+                    self.abort(msg)
+                    raise CollectiveError(msg)
+                if el > 0.02:
+                    time.sleep(2e-4)     # spin first (latency), then yield the core
+
+    def sync(self) -> None:
+        """device synchronise through the watchdog (torch.cuda.synchronize without communicators)"""
+        if self.device.type != "cuda":
+            return
+        if not self._comms():
+            torch.cuda.synchronize(self.device)
+            return
+        ev = torch.cuda.Event()
+        ev.record()
+        self.wait_event(ev)
+        torch.cuda.synchronize(self.device)   # (the other streams: the event covered the current one)
 
     @property
     def enabled(self) -> bool:
@@ -214,12 +370,12 @@ class DistContext:
                 dist.barrier()
 
     def destroy(self) -> None:
-        if self.native is not None:
+        for c in self._comms():
             try:
-                self.native.destroy()
-            except Exception:
+                c.destroy()
+            except Exception:   # noqa: BLE001
                 pass
-            self.native = None
+        self.native = self.native_side = None
         if dist.is_available() and dist.is_initialized():
             try:
                 dist.destroy_process_group()
@@ -234,31 +390,33 @@ def _env_int(name: str, default: int) -> int:
 
 def init_distributed(device: str = "cpu", rank: Optional[int] = None, world_size: Optional[int] = None,
                      master_addr: str = "127.0.0.1", master_port: Optional[int] = None,
-                     timeout_s: float = 300.0) -> DistContext:
+                     timeout_s: float = 300.0, backend: str = "auto", grad_comm: str = "auto") -> DistContext:
     """Initialise from torchrun env vars or explicit args; one process per GPU.
 
-    GPU → backend 'nccl' (RCCL over xGMI), CPU → 'gloo'.  world_size 1 → no process group
-    unless ``force`` is wanted by a caller (RCCL at world size 1 is exercised by bench.py).
+    ``backend`` (Params.dist_backend): auto = 'nccl' (RCCL over xGMI) on GPU, 'gloo' on CPU;
+    'gloo' on GPU is for ranks sharing one GPU (RCCL refuses two ranks on one device: the 1-GPU
+    box's multi-rank tests), with the in-stream engine path on GlooStreamComm.  world_size 1 →
+    no process group (bench.py / the launcher make a world-1 RCCL group themselves).
     """
     rank = _env_int("RANK", 0) if rank is None else rank
     world_size = _env_int("WORLD_SIZE", 1) if world_size is None else world_size
     local_rank = _env_int("LOCAL_RANK", rank)
+    if backend not in ("auto", "nccl", "gloo"):
+        raise ValueError(f"unsupported backend {backend}")
     if device == "gpu":
         ndev = torch.cuda.device_count()
         if ndev == 0:
             raise RuntimeError("device=gpu but no HIP device visible")
         torch.cuda.set_device(local_rank % ndev)
         dev = torch.device("cuda", local_rank % ndev)
-        # DPPO_DIST_BACKEND=gloo: diagnostics only — several ranks sharing one GPU (RCCL refuses
-        # two ranks on one device), to exercise the multi-rank GPU engine path on a 1-GPU box
-        backend = os.environ.get("DPPO_DIST_BACKEND", "nccl")
+        backend = "nccl" if backend == "auto" else backend
     else:
         dev = torch.device("cpu")
+        if backend == "nccl":
+            raise ValueError("the nccl (RCCL) backend needs device=gpu")
         backend = "gloo"
     ctx = DistContext(rank=rank, world_size=world_size, local_rank=local_rank, backend=backend,
-                      device=dev)
-    if backend not in ("nccl", "gloo"):
-        raise ValueError(f"unsupported backend {backend}")
+                      device=dev, timeout_s=float(timeout_s), grad_comm=grad_comm)
     if world_size > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", master_addr)
         if master_port is not None:
@@ -272,11 +430,13 @@ def init_distributed(device: str = "cpu", rank: Optional[int] = None, world_size
     return ctx
 
 
-def init_single_rank_collective(device: torch.device, port: int = 29541) -> DistContext:
+def init_single_rank_collective(device: torch.device, port: int = 29541, timeout_s: float = 300.0,
+                                grad_comm: str = "auto") -> DistContext:
     """A world-size-1 RCCL group so the real collective path runs on a 1-GPU box."""
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(port))
     if not dist.is_initialized():
-        dist.init_process_group(backend="nccl", rank=0, world_size=1, device_id=device)
+        dist.init_process_group(backend="nccl", rank=0, world_size=1, device_id=device,
+                                timeout=datetime.timedelta(seconds=timeout_s))
     return DistContext(rank=0, world_size=1, local_rank=device.index or 0, backend="nccl",
-                       device=device)
+                       device=device, timeout_s=float(timeout_s), grad_comm=grad_comm)

@@ -20,8 +20,8 @@ in the MFMA operand precision (fp32 / bf16), the bias folded into column K.
 """
 from __future__ import annotations
 
+import contextlib
 import math
-import os
 from typing import Dict, Optional
 
 import torch
@@ -146,16 +146,16 @@ class HipEngine:
         # the reference network, at minibatches of at least one full round of 128-row workgroups
         # (one per CU): below that the two-head tile kernel's smaller workgroups fill the chip better
         # (measured, 16,384 rows: 0.716 vs 0.836 ms per iteration at bf16, 1.61 vs 1.71 at bf16x3;
-        # 65,536 rows: 4.2 vs 4.9 ms at bf16x3).  DPPO_HEADS=1 / 0 force the per-head / tile path.
-        mode = os.environ.get("DPPO_HEADS", "auto")
+        # 65,536 rows: 4.2 vs 4.9 ms at bf16x3).  Params.update_kernels heads / tile force one path.
+        mode = params.update_kernels
         ncu = (torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 256)
-        self.heads = (mode != "0" and bool(self.ext.head_applies(self.dt, self.layout, A))
-                      and (mode == "1" or params.minibatch_rows() >= 128 * ncu))
+        self.heads = (mode != "tile" and bool(self.ext.head_applies(self.dt, self.layout, A))
+                      and (mode == "heads" or params.minibatch_rows() >= 128 * ncu))
         # fp8 mode on the per-head path: the wgrad operands (x^T, h1^T, g1^T, g2^T of both heads)
         # are e4m3 bytes with power-of-two scales — fixed for the activations, delayed per-tensor
         # for the gradients (csrc/common.h Q8) — and the wgrad runs on the e4m3 MFMA: half the
-        # operand bytes of the bf16 update's HBM round trip.  DPPO_Q8=0: bf16 operands.
-        self.q8 = self.fp8 and self.heads and os.environ.get("DPPO_Q8", "1") != "0"
+        # operand bytes of the bf16 update's HBM round trip.  fp8_wgrad_operands=False: bf16 operands.
+        self.q8 = self.fp8 and self.heads and bool(params.fp8_wgrad_operands)
         # the gradient-amax ring: 3 slots x 4 tensors x 64 sub-slot lines of 32 dwords (csrc/kernels.h)
         self.q8_amax = torch.zeros(3 * 4 * Q8_SUB * 32, dtype=torch.int32, device=device)
         self._q8_next = 0          # step counter of the amax ring
@@ -185,8 +185,8 @@ class HipEngine:
         self.part_dw_joint = [self.part_dw[0], np_pol]
         self.head_range = [model.head_ranges["policy"], model.head_ranges["value"]]
         self.head_order = (0, 1)     # launch order of the joint head kernels (A/B: scripts/ab_iter.py)
-        if os.environ.get("DPPO_MLP_ROWS"):     # diagnostics: force the fused-kernel row tile
-            self.ext.set_mlp_rows(int(os.environ["DPPO_MLP_ROWS"]))
+        if params.mlp_rows:                     # diagnostics: force the fused-kernel row tile
+            self.ext.set_mlp_rows(int(params.mlp_rows))
         self.sync_tile()
         # transposed operand buffers (feature-major), heights padded to the wgrad tile
         lp1, lp2, lmu, lv1, lv2, lv = ls
@@ -244,9 +244,12 @@ class HipEngine:
         self.norm_part = torch.zeros(max(n_whole, np_ + nv_), **f32)
         self.norm_n_whole = n_whole
         self._norm_n = n_whole       # entries the last Adam path wrote (metrics_pack sums them)
-        self._pending_value = None   # (all-reduce work, step, mean) of a value step not yet applied
-        # world-size-1 fast path: grad_gather + no-clip Adam in one launch (DPPO_FUSED_APPLY=0: off)
-        self.fused_apply = os.environ.get("DPPO_FUSED_APPLY", "1") != "0"
+        # a value-head step not yet applied: ("work", all-reduce work, step, mean) on the
+        # process-group chains, or ("side", None, step, mean) when it runs on the side stream
+        self._pending_value = None
+        self._side: Optional[torch.cuda.Stream] = None   # the side stream of the overlapped value step
+        # world-size-1 fast path: grad_gather + no-clip Adam in one launch (fused_apply=False: off)
+        self.fused_apply = bool(params.fused_apply)
         self.idx_dev = torch.zeros(self.ldT, dtype=torch.int32, **dev)
         self.key_action = rng.base_key(params.seed, rng.STREAM_ACTION, action_rank)
         self.empty = torch.empty(0, dtype=torch.int32, **dev)
@@ -285,10 +288,10 @@ class HipEngine:
         those four layers in ONE bucket over [A, n).  The narrow output layers mu and v, log_std
         and the loss terms are the head kernels' reduce items (partial-row columns, _reduce_items),
         so their elements carry src_meta 0.  One-kernel path: every layer in one bucket.  Each
-        bucket is chunked for ~target_wgs workgroups (default WGRAD_TARGET_WGS, env
-        DPPO_WGRAD_WGS) with its own fp32 partial slab."""
+        bucket is chunked for ~target_wgs workgroups (default Params.wgrad_wgs, 0: one per CU)
+        with its own fp32 partial slab."""
         if target_wgs is None:
-            target_wgs = int(os.environ.get("DPPO_WGRAD_WGS", WGRAD_TARGET_WGS))
+            target_wgs = int(self.p.wgrad_wgs or WGRAD_TARGET_WGS)
         if target_wgs <= 0:
             target_wgs = (torch.cuda.get_device_properties(self.device).multi_processor_count
                           if self.device.type == "cuda" else 256)
@@ -311,22 +314,27 @@ class HipEngine:
         meta = torch.zeros(model.num_params, dtype=torch.int64)
         self.buckets = []
         max_chunks = max(1, self.ldT // 64)            # a task covers >= 64 batch rows
+        # Batch chunks PER TILE, in proportion to the tile's operand stream ((nq + kq) * 64 rows
+        # per k-step): every task then streams about the same bytes, and the task count is
+        # ~target_wgs = one workgroup per CU (the kernel is bound by each CU's operand stream, so
+        # every CU gets one equal share; largest-remainder rounding).  The chunk counts are
+        # dealt over the tiles of ALL buckets together, so the per-head buckets and the joint one
+        # split every tile identically: each weight-gradient element is the same fixed-order sum
+        # on every path (the process-group chains == the in-stream joint path, bit for bit).
+        all_tiles = []  # (layer, n0, k0, nq, kq)
+        for li in sorted({li for layers in groups for li in layers}):
+            l = ls[li]
+            all_tiles += wgrad_tiles(li, l.fan_out, l.fan_in + 1)
+        costs = [t[3] + t[4] for t in all_tiles]
+        raw = [target_wgs * c / sum(costs) for c in costs]
+        nch_all = [max(1, int(r)) for r in raw]
+        rest = sorted(range(len(all_tiles)), key=lambda t: raw[t] - int(raw[t]), reverse=True)
+        for t in rest[:max(0, target_wgs - sum(nch_all))]:
+            nch_all[t] += 1
+        nch_of = {t: min(max_chunks, n) for t, n in zip(all_tiles, nch_all)}
         for bi, (layers, (lo, hi)) in enumerate(zip(groups, ranges)):
-            tiles = []  # (layer, n0, k0, nq, kq)
-            for li in layers:
-                l = ls[li]
-                tiles += wgrad_tiles(li, l.fan_out, l.fan_in + 1)
-            # Batch chunks PER TILE, in proportion to the tile's operand stream ((nq + kq) * 64
-            # rows per k-step): every task then streams about the same bytes, and the task count
-            # is ~target_wgs = one workgroup per CU (the kernel is bound by each CU's operand
-            # stream, so every CU gets one equal share; largest-remainder rounding).
-            costs = [t[3] + t[4] for t in tiles]
-            raw = [target_wgs * c / sum(costs) for c in costs]
-            nch = [max(1, int(r)) for r in raw]
-            rest = sorted(range(len(tiles)), key=lambda t: raw[t] - int(raw[t]), reverse=True)
-            for t in rest[:max(0, target_wgs - sum(nch))]:
-                nch[t] += 1
-            nch = [min(max_chunks, n) for n in nch]
+            tiles = [t for t in all_tiles if t[0] in layers]
+            nch = [nch_of[t] for t in tiles]
             tasks, tile_off, base = [], {}, 0
             for t, n in zip(tiles, nch):
                 size = t[3] * t[4] * 64 * 64
@@ -635,7 +643,11 @@ class HipEngine:
         it (and the caller's merge, issued on the same stream) overlaps the value forward and
         the update; the caller orders its stream after that work before reading the stats."""
         # fp8: the weights changed during the previous update (Adam rewrites only the bf16 image);
-        # before either path, so values() / GAE of a host-env rollout see the current weights too
+        # before either path, so values() / GAE of a host-env rollout see the current weights too.
+        # The refresh reads every layer: a value step still running on the side stream
+        # (--overlap-rollout) is joined first, so fp8 runs that step in order.
+        if self.fp8 or self.host_env:
+            self._flush_value()
         self.refresh_fwd_image()
         if self.host_env:
             ro = self._rollout_host()
@@ -655,6 +667,10 @@ class HipEngine:
                                  self.xT if self.xT_from_rollout else None)
             self._xT_valid = self.xT_from_rollout
             self.env.t += self.T
+            # --overlap-rollout: the previous iteration's last value-head step (side stream) ran
+            # beside the rollout kernel just enqueued (which reads only the policy); join it here,
+            # before the reduce rewrites the episode stats its metrics pack read
+            self._flush_value()
             # one launch: moments [nblk][2][O] -> s12, episode stats [nblk][2] -> ep_sum
             if stats_stream is not None:
                 stats_stream.wait_stream(torch.cuda.current_stream(self.device))
@@ -672,6 +688,7 @@ class HipEngine:
             # moments -> reduce -> merge into the worker-local stats) + a one-step rollout launch.
             # The steps' rollout moments / episode stats land in per-step slices and ONE reduce
             # after the loop gives the iteration's totals.  No host sync.
+            self._flush_value()
             shift = self.stats.shift().clone()
             ls = self.local_stats = RunningObsStats(self.O, self.device)
             ls.copy_from(self.stats)
@@ -693,6 +710,7 @@ class HipEngine:
 
     @torch.no_grad()
     def values(self) -> None:
+        self._flush_value()          # the value head must hold its last step
         M = (self.T + 1) * self.E
         if self.fp8 and self.heads:
             # fp8 mode on the per-head path: the value head's streaming forward with the e4m3 fc1
@@ -764,33 +782,43 @@ class HipEngine:
                 and (self.heads or (len(self.buckets) == 1 and self.buckets[0]["partials"])))
 
     def step(self, idx: Optional[torch.Tensor], extra_grad: float = 0.0, allreduce=None,
-             mean: bool = False) -> None:
+             mean: bool = False, last: bool = False) -> None:
         """ONE synchronous global step (train.py:133-175 + chief.py:13-20): the minibatch
-        gradient, its sum (``mean``: average) over ranks, and the Adam step.  ``allreduce(t)``
-        returns an async work handle (the worker's collective), None at world size 1.
+        gradient, its sum (``mean``: average) over ranks, and the Adam step.
 
-        Per-head kernels: each head is its own chain (kernel -> wgrad -> gather -> Adam).  At
-        world size 1 the gather and the Adam step are one launch per head.  With a collective,
-        the policy range's all-reduce is issued as soon as it is gathered and runs while the value
-        head's kernels compute; the value range's all-reduce runs while the policy Adam and the
-        NEXT step's policy kernels compute — its Adam is applied just before the value kernel of
-        the next step (or by finish_steps()).  Each head's Adam step e still precedes that head's
-        kernel of step e+1, so the parameters are exactly the synchronous ones.  Clipping (a
-        global norm over both heads), the Q1 extra gradient and hipGraph replay take the
-        whole-vector path."""
+        ``allreduce``: the worker's collective (parallel/dist.py grad_allreduce_fn), None at world
+        size 1.  In-stream communicators (``allreduce.in_stream``: the native RCCL one — the
+        default on an RCCL group — or the gloo adapter) reduce in stream order and do the mean
+        themselves: joint kernels (one wgrad, one gather) → all-reduce → whole-vector Adam.
+        With ``last`` (the iteration's final step) under --overlap-rollout and a side
+        communicator, the value head's all-reduce + Adam go to a side stream instead and overlap
+        the next rollout, which reads only the policy (exact; joined in rollout()/values()).
+
+        Process-group collectives (``allreduce(t)`` returns an async work handle): per-head
+        chains.  The policy range's all-reduce is issued as soon as it is gathered and runs while
+        the value head's kernels compute; the value range's all-reduce runs while the policy Adam
+        and the NEXT step's policy kernels compute — its Adam is applied just before the value
+        kernel of the next step (or by finish_steps()).  Each head's Adam step e still precedes
+        that head's kernel of step e+1, so the parameters are exactly the synchronous ones.
+        Clipping (a global norm over both heads), the Q1 extra gradient and the one-kernel tile
+        update take the whole-vector path."""
         p = self.p
         clip = p.max_grad_norm is not None and p.max_grad_norm > 0
         if allreduce is None and self.can_fuse_apply(extra_grad):
             self.grad(idx, apply=True)          # world size 1: gather + Adam in one launch
             return
-        if self.heads and getattr(allreduce, "in_stream", False):
-            # native RCCL on the compute stream (parallel/dist.py NativeComm): no cross-stream
-            # event hops, so the joint kernels (one wgrad, one gather) then the all-reduce in
-            # stream order, then the whole-vector Adam (+ clip)
+        if getattr(allreduce, "in_stream", False):
             self._flush_value()
-            idx_t, first, xt_ready = self._minibatch(idx)
-            self._joint_grad(idx_t, first, xt_ready)
-            allreduce(self.grad_flat)
+            if self.heads:
+                idx_t, first, xt_ready = self._minibatch(idx)
+                self._joint_grad(idx_t, first, xt_ready)
+            else:
+                self.grad(idx)
+            if (last and p.overlap_rollout and self.heads and getattr(allreduce, "side", False)
+                    and not clip and not extra_grad):
+                self._split_step_side(allreduce)
+                return
+            allreduce(self.grad_flat)           # sum / mean in stream order: no host-side scaling
             self.apply(extra_grad)
             return
         if not self.heads:
@@ -807,7 +835,7 @@ class HipEngine:
                 self._reduce_wait(allreduce(self.grad_flat), self.grad_flat, mean)
             self.apply(extra_grad)
             return
-        if allreduce is None:                   # (DPPO_FUSED_APPLY=0: the two-launch chains, no collective)
+        if allreduce is None:                   # (fused_apply=False: the two-launch chains, no collective)
             allreduce = lambda t: None          # noqa: E731
         step_no = self.adam_step + 1
         (plo, phi), (vlo, vhi) = self.head_range
@@ -815,9 +843,28 @@ class HipEngine:
         wp = allreduce(self.grad_flat[plo:phi])
         self._flush_value()
         self._head_chain(1, idx_t, first, xt_ready)
-        self._pending_value = (allreduce(self.grad_flat[vlo:vhi]), step_no, mean)
+        self._pending_value = ("work", allreduce(self.grad_flat[vlo:vhi]), step_no, mean)
         self._reduce_wait(wp, self.grad_flat[plo:phi], mean)
         self._head_adam(0, step_no)
+        self.adam_step += 1
+        self._norm_n = self.norm_regions[1][1]
+
+    def _split_step_side(self, allreduce) -> None:
+        """the joint gradient is gathered: policy all-reduce + Adam in stream order, then the
+        value range's all-reduce (the side communicator) + Adam on the side stream, fenced by the
+        stream dependency; rollout() / values() / finish_steps() join it (_flush_value)."""
+        (plo, phi), (vlo, vhi) = self.head_range
+        step_no = self.adam_step + 1
+        allreduce(self.grad_flat[plo:phi])
+        self._head_adam(0, step_no)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        side = self._side
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            allreduce(self.grad_flat[vlo:vhi], stream=side)
+            self._head_adam(1, step_no)
+        self._pending_value = ("side", None, step_no, False)
         self.adam_step += 1
         self._norm_n = self.norm_regions[1][1]
 
@@ -825,11 +872,22 @@ class HipEngine:
         """apply a value-head step still waiting for its all-reduce (end of the epochs)"""
         self._flush_value()
 
+    def metrics_stream(self) -> Optional[torch.cuda.Stream]:
+        """the stream the iteration's metrics are packed and staged on: the side stream while the
+        last value step runs there (its Adam writes the value head's norm partials), else None"""
+        pend = self._pending_value
+        return self._side if (pend is not None and pend[0] == "side") else None
+
     def _flush_value(self) -> None:
         pend, self._pending_value = self._pending_value, None
         if pend is None:
             return
-        work, step_no, mean = pend
+        kind, work, step_no, mean = pend
+        if kind == "side":
+            # everything enqueued on the side stream so far: the value step AND the metrics
+            # pack / staging copy behind it (their buffers are rewritten after this point)
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            return
         vlo, vhi = self.head_range[1]
         self._reduce_wait(work, self.grad_flat[vlo:vhi], mean)
         self._head_adam(1, step_no)
@@ -1005,8 +1063,18 @@ class HipEngine:
         if self._loss_dev is None:
             return None
         # every Adam path (fused no-clip, sumsq + clip, per head) leaves the per-block
-        # sums of squares of the gradient it applied in norm_part[:_norm_n]
-        self.ext.metrics_pack(ep2, self._loss_dev, self.norm_part[:self._norm_n], self.metrics_buf)
+        # sums of squares of the gradient it applied in norm_part[:_norm_n].  A value step left
+        # pending on the process-group chains has not written its region yet: the norm is the
+        # policy head's for that step.  One on the side stream: the pack runs there, after it.
+        pend = self._pending_value
+        n = self.norm_regions[0][1] if (pend is not None and pend[0] == "work") else self._norm_n
+        side = self.metrics_stream()
+        if side is not None:
+            # everything the pack reads that the compute stream wrote after the value step was
+            # forked (the side-stream obs-stat merge's episode sums are joined there at the end)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+        with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+            self.ext.metrics_pack(ep2, self._loss_dev, self.norm_part[:n], self.metrics_buf)
         return self.metrics_buf
 
     def loss_vector(self) -> Optional[torch.Tensor]:

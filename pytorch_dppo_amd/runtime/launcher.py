@@ -56,7 +56,7 @@ def run_worker(params: Params, ctx: DistContext, max_iters: Optional[int] = None
         from .evaluator import EvaluatorHandle
         ev = EvaluatorHandle(params)
     history = []
-    hb = start_heartbeat(ctx, params.heartbeat_s, params.heartbeat_timeout_s)
+    hb = start_heartbeat(ctx, params.heartbeat_interval(ctx.world_size), params.heartbeat_timeout_s)
     prof = _Profiler(params, ctx)
     try:
         n = 0
@@ -77,6 +77,7 @@ def run_worker(params: Params, ctx: DistContext, max_iters: Optional[int] = None
             prof.after(n)
             n += 1
             if ev is not None and w.iteration % params.eval_every == 0:
+                w.quiesce()     # a value step still on the side stream writes what the snapshot reads
                 ev.push(w.model.state_dict(), w.stats.state_dict(), w.iteration)
             if params.checkpoint_dir and params.checkpoint_every and w.iteration % params.checkpoint_every == 0:
                 save(w, ctx, params.checkpoint_dir)
@@ -133,6 +134,9 @@ class _Profiler:
 
 
 def save(w, ctx: DistContext, path: str) -> None:
+    # every deferred step applied BEFORE the weights are copied out: model.pt and the Adam state
+    # of trainer_state.pt must describe the same step
+    w.flush_pending()
     env_state = w.engine.env_state() if hasattr(w.engine, "env_state") else None
     ckpt.save_checkpoint(path, w.model.state_dict(), w.trainer_state(), ctx.rank, env_state)
     ctx.barrier()
@@ -144,7 +148,8 @@ def _spawn_entry(rank: int, world: int, port: int, params_dict, ret_q=None):
     os.environ.setdefault("OMP_NUM_THREADS", "1")   # main.py:42
     torch.set_num_threads(1)
     params = Params.from_dict(params_dict)
-    ctx = init_distributed(params.device, rank=rank, world_size=world, timeout_s=params.dist_timeout_s)
+    ctx = init_distributed(params.device, rank=rank, world_size=world, timeout_s=params.dist_timeout_s,
+                           backend=params.dist_backend, grad_comm=params.grad_comm)
     try:
         w, hist = run_worker(params, ctx)
         if ret_q is not None and rank == 0:
@@ -158,11 +163,13 @@ def _spawn_entry(rank: int, world: int, port: int, params_dict, ret_q=None):
 
 def launch(params: Params) -> None:
     if "WORLD_SIZE" in os.environ and "RANK" in os.environ:
-        ctx = init_distributed(params.device, timeout_s=params.dist_timeout_s)
+        ctx = init_distributed(params.device, timeout_s=params.dist_timeout_s, backend=params.dist_backend,
+                               grad_comm=params.grad_comm)
         try:
             if params.device == "gpu" and ctx.world_size == 1:
                 from ..parallel.dist import init_single_rank_collective
-                ctx = init_single_rank_collective(ctx.device)
+                ctx = init_single_rank_collective(ctx.device, timeout_s=params.dist_timeout_s,
+                                                  grad_comm=params.grad_comm)
             run_worker(params, ctx)
         finally:
             ctx.destroy()
@@ -171,10 +178,11 @@ def launch(params: Params) -> None:
     if params.device == "gpu":
         world = min(world, max(1, torch.cuda.device_count()))
     if world == 1:
-        ctx = init_distributed(params.device, rank=0, world_size=1)
+        ctx = init_distributed(params.device, rank=0, world_size=1, backend=params.dist_backend)
         if params.device == "gpu":
             from ..parallel.dist import init_single_rank_collective
-            ctx = init_single_rank_collective(ctx.device, port=free_port())
+            ctx = init_single_rank_collective(ctx.device, port=free_port(), timeout_s=params.dist_timeout_s,
+                                              grad_comm=params.grad_comm)
         try:
             run_worker(params, ctx)
         finally:

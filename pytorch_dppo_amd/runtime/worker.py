@@ -15,9 +15,11 @@ busy-spin (Q14) disappear: a step costs compute + one collective.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import math
 import os
+import sys
 import time
 from typing import Dict, Optional
 
@@ -64,7 +66,9 @@ class DPPOWorker:
         self.stats = RunningObsStats(self.spec.obs_dim, self.device)
         self.engine = build_engine(params, self.model, self.env, self.stats, self.device, action_rank)
         if ctx.collective and hasattr(self.engine, "ext"):
-            ctx.init_native_comm(self.engine.ext)   # in-stream RCCL (collective: every rank)
+            # in-stream communicator (collective: every rank); --overlap-rollout also gets the
+            # side-stream one its deferred value step uses
+            ctx.init_native_comm(self.engine.ext, side=bool(params.overlap_rollout))
         self.iteration = 0
         self.env_steps = 0            # global (all ranks)
         self.updates = 0
@@ -73,16 +77,23 @@ class DPPOWorker:
         self._stats_initialised = False
         self.last_metrics: Dict = {}
         self._perm_gen = torch.Generator(device="cpu")
+        # DPPO_DEBUG_FAULT="rank:iteration:epoch" (fault-injection tests): that rank
+        # exits abruptly (status 13) at that epoch, as a crashed worker would
+        self._fault = None
+        spec = os.environ.get("DPPO_DEBUG_FAULT", "")
+        if spec:
+            fr, fi, fe = (int(x) for x in spec.split(":"))
+            if fr == ctx.rank:
+                self._fault = (fi, fe)
         self._pending = None          # (async all-reduce work, extra) under --overlap-rollout
         self._staged = None           # metrics of the last deferred iteration (iteration_step(defer=True))
         # GPU engine: optional side stream for the observation-statistics reduce + all-reduce +
-        # merge (DPPO_STATS_STREAM=1 on, auto: when an RCCL all-reduce sits in that chain, 0 off =
+        # merge (Params.stats_stream on, auto: when an all-reduce sits in that chain, off =
         # default).  Measured slower on the 1-GPU box: 26.06-26.35 vs 26.43-26.55 M env steps/s
         # plain, 24.55-24.79 vs 24.85-25.17 M with the RCCL calls forced — the reduce/merge
         # kernels take CU slots from the LDS-bound value forward and the hand-offs cost more
         # than the ~15 us (+ all-reduce latency) they hide.
-        mode = os.environ.get("DPPO_STATS_STREAM", "0")
-        want = {"1": True, "0": False}.get(mode, bool(ctx.collective))
+        want = {"on": True, "off": False}.get(params.stats_stream, bool(ctx.collective))
         self._stats_stream = None
         if want and self.device.type == "cuda" and hasattr(self.engine, "s12"):
             self._stats_stream = torch.cuda.Stream(device=self.device)
@@ -180,13 +191,18 @@ class DPPOWorker:
                 if p.compat and self.updates == 0:
                     extra = 1.0  # Q1: Shared_grad_buffers start at ones (model.py:51)
                 last = epoch == p.num_epoch - 1 and b == nmb - 1
+                if self._fault == (self.iteration, epoch):
+                    print(f"[dppo rank {self.ctx.rank}] DPPO_DEBUG_FAULT: exiting at iteration {self.iteration} "
+                          f"epoch {epoch}", file=sys.stderr, flush=True)
+                    os._exit(13)
                 if hasattr(eng, "step"):
-                    # GPU engine: gradient -> all-reduce -> Adam.  Native RCCL (the default on an
-                    # RCCL group): in stream order after the joint gather; a process-group
-                    # all-reduce: per-head chains, each head's async all-reduce overlapping the
-                    # other head's kernels (engine_hip.HipEngine.step)
+                    # GPU engine: gradient -> all-reduce -> Adam.  In-stream communicator (the
+                    # default: native RCCL, or the gloo adapter): in stream order after the joint
+                    # gather (the last step's value half on the side stream under
+                    # --overlap-rollout); a process-group all-reduce: per-head chains, each head's
+                    # async all-reduce overlapping the other head's kernels (HipEngine.step)
                     ar = self.ctx.grad_allreduce_fn(mean)
-                    eng.step(idx, extra, allreduce=ar, mean=mean)
+                    eng.step(idx, extra, allreduce=ar, mean=mean, last=last)
                     self.updates += 1
                     continue
                 deferred = p.overlap_rollout and last and not mean and self.ctx.collective
@@ -244,10 +260,14 @@ class DPPOWorker:
         else:
             flat, loss_dev = self._stage_parts(ro)
         if dev.type == "cuda":
-            host = torch.empty(flat.numel(), dtype=torch.float64, pin_memory=True)
-            host.copy_(flat, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
+            # the stream the metrics were packed on (the side stream while the overlapped value
+            # step runs there)
+            side = eng.metrics_stream() if hasattr(eng, "metrics_stream") else None
+            with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                host = torch.empty(flat.numel(), dtype=torch.float64, pin_memory=True)
+                host.copy_(flat, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
         else:
             host, ev = flat, None
         return {"host": host, "event": ev, "phases": self.timer.collect(), "has_loss": loss_dev is not None,
@@ -269,7 +289,7 @@ class DPPOWorker:
     def _resolve_metrics(self, st: Dict) -> Dict:
         p = self.p
         if st["event"] is not None:
-            st["event"].synchronize()
+            self.ctx.wait_event(st["event"])     # bounded by dist_timeout_s (collective watchdog)
         v = st["host"].tolist()
         ep_ret, ep_cnt = v[0], v[1]
         if st["has_loss"]:
@@ -285,6 +305,7 @@ class DPPOWorker:
              "ep_count": ep_cnt, "mean_ep_return": (ep_ret / ep_cnt) if ep_cnt > 0 else float("nan"),
              "grad_norm": gnorm, **losses, **phases}
         if p.verify_sync_every and st["iteration"] % p.verify_sync_every == 0:
+            self.quiesce()                       # the checksum reads the value head too
             m["replicas_in_sync"] = self.ctx.verify_replicas(self.model.flat.data)
         if p.check_finite:
             self._check_finite(m)
@@ -302,6 +323,13 @@ class DPPOWorker:
             bad.append("obs_stats.mean")
         if bad:
             raise FloatingPointError(f"rank {self.ctx.rank} iteration {int(it)}: non-finite {bad}")
+
+    def quiesce(self) -> None:
+        """the GPU engine's deferred value-head step (side stream / pending all-reduce) applied:
+        the parameters are the synchronous ones (snapshots, checksums); the CPU engine's deferred
+        whole step (its documented 1-update lag) is left alone"""
+        if hasattr(self.engine, "finish_steps"):
+            self.engine.finish_steps()
 
     def flush_pending(self) -> None:
         """complete a deferred (overlapped) all-reduce + Adam step, if any."""

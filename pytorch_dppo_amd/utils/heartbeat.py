@@ -45,7 +45,8 @@ def _own_store_client(default_store, timeout_s: float):
 
 class Heartbeat:
     def __init__(self, store, rank: int, world_size: int, interval_s: float, timeout_s: float,
-                 on_dead: Optional[Callable[[List[int]], None]] = None, prefix: str = "dppo/hb/"):
+                 on_dead: Optional[Callable[[List[int]], None]] = None, prefix: str = "dppo/hb/",
+                 abort: Optional[Callable[[str], None]] = None):
         if interval_s <= 0:
             raise ValueError("interval_s must be > 0")
         self.store = store
@@ -55,6 +56,7 @@ class Heartbeat:
         self.timeout_s = float(max(timeout_s, 2 * interval_s))
         self.on_dead = on_dead or self._default_on_dead
         self.prefix = prefix
+        self.abort = abort
         self.beats = 0
         self.dead: List[int] = []
         self._stop = threading.Event()
@@ -121,8 +123,16 @@ class Heartbeat:
         self.on_dead(list(dead))
 
     def _default_on_dead(self, dead: List[int]) -> None:
-        print(f"[heartbeat] rank {self.rank}: rank(s) {dead} silent for > {self.timeout_s:.0f} s; "
-              f"exiting instead of waiting in a collective", file=sys.stderr, flush=True)
+        msg = (f"[heartbeat] rank {self.rank}: rank(s) {dead} silent for > {self.timeout_s:.0f} s; "
+               f"exiting instead of waiting in a collective")
+        print(msg, file=sys.stderr, flush=True)
+        if self.abort is not None:
+            # ncclCommAbort first: a collective waiting on the dead peer must leave the GPU
+            # before this process does
+            try:
+                self.abort(msg)
+            except Exception:   # noqa: BLE001 — exiting regardless
+                pass
         os._exit(75)
 
 
@@ -134,4 +144,5 @@ def start_heartbeat(ctx, interval_s: float, timeout_s: float,
         return None
     from torch.distributed import distributed_c10d as c10d
     store = _own_store_client(c10d._get_default_store(), timeout_s)
-    return Heartbeat(store, ctx.rank, ctx.world_size, interval_s, timeout_s, on_dead).start()
+    return Heartbeat(store, ctx.rank, ctx.world_size, interval_s, timeout_s, on_dead,
+                     abort=getattr(ctx, "abort", None)).start()

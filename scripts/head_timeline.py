@@ -26,10 +26,9 @@ EVERY = 8
 
 
 def main():
-    os.environ.setdefault("DPPO_HEADS", "1")
     dev = torch.device("cuda", 0)
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536, batch_size=65536,
-                    dtype=sys.argv[1] if len(sys.argv) > 1 else "bf16x3")
+                    dtype=sys.argv[1] if len(sys.argv) > 1 else "bf16x3", update_kernels="heads")
     spec = get_spec(p.env_name)
     torch.manual_seed(0)
     model = ActorCritic(spec.obs_dim, spec.act_dim).to(dev)

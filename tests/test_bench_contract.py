@@ -50,11 +50,10 @@ def test_bench_json_line_one_gpu():
 @pytest.mark.gpu
 def test_bench_json_line_two_ranks():
     from pytorch_dppo_amd.runtime.launcher import free_port
-    env = dict(os.environ, DPPO_DIST_BACKEND="gloo")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", *TINY,
-                        "--variants", "", "--verify-sync"], cwd=ROOT, env=env, capture_output=True, text=True,
-                       timeout=300)
+                        "--variants", "", "--verify-sync", "--dist-backend", "gloo"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     _check(_json_line(r.stdout), 2, [])
     assert "replicas_in_sync True" in r.stderr
@@ -63,10 +62,10 @@ def test_bench_json_line_two_ranks():
 @pytest.mark.gpu
 def test_plain_bench_gpus_two_launches_two_ranks():
     """the driver's form `python bench.py --gpus N` (no torchrun): bench.py starts N ranks itself"""
-    env = dict(os.environ, DPPO_DIST_BACKEND="gloo")
+    env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
-    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY, "--variants", "", "--verify-sync"],
-                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY, "--variants", "", "--verify-sync",
+                        "--dist-backend", "gloo"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
     _check(d, 2, [])
@@ -104,12 +103,16 @@ def test_bench_refuses_world_size_mismatch():
 
 
 def test_bench_refuses_more_rccl_ranks_than_gpus():
-    """RCCL needs one GPU per local rank: on a box with fewer visible GPUs, plain --gpus N and a
-    torchrun world both exit non-zero before starting anything"""
+    """RCCL needs one GPU per local rank: on a box with fewer visible GPUs, a torchrun world and
+    the plain --gpus N form (whose parent makes no HIP call: its ranks check) both exit non-zero
+    without a JSON line, before any GPU work"""
     import torch
     n = max(2, torch.cuda.device_count() + 1)
-    err = _bench_fails(["--gpus", str(n)], {"DPPO_DIST_BACKEND": "nccl"})
-    assert f"--gpus {n} but only" in err
-    err = _bench_fails(["--gpus", str(n)], {"DPPO_DIST_BACKEND": "nccl", "WORLD_SIZE": str(n), "RANK": "0",
-                                            "LOCAL_RANK": "0", "LOCAL_WORLD_SIZE": str(n)})
+    err = _bench_fails(["--gpus", str(n), "--dist-backend", "nccl"], {"WORLD_SIZE": str(n), "RANK": "0",
+                                                                      "LOCAL_RANK": "0", "LOCAL_WORLD_SIZE": str(n)})
     assert "visible GPU" in err
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), *TINY], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "visible GPU" in r.stderr and f"launching {n} ranks" in r.stderr

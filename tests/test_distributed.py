@@ -244,3 +244,116 @@ def test_overlap_rollout_defers_last_step_but_applies_every_update(tmp_path):
         assert torch.equal(r0[ov][0], r1[ov][0])
     # the lagged rollouts see different weights -> a (slightly) different trajectory
     assert not torch.equal(r0[False][0], r0[True][0])
+
+
+# ---- the native communicator's watchdog and collective-safe creation (mocked extension) --------
+
+class _FakeCommExt:
+    """stands in for the HIP extension's comm_* entry points (csrc/comm.cpp)"""
+
+    def __init__(self, status_seq=(0,), fail_id=False, fail_init_rank=None, rank=0):
+        self.status_seq = list(status_seq)
+        self.fail_id, self.fail_init_rank, self.rank = fail_id, fail_init_rank, rank
+        self.aborted, self.polls = [], 0
+
+    def comm_unique_id(self):
+        if self.fail_id:
+            raise RuntimeError("RCCL ncclGetUniqueId failed: test")
+        return b"x" * 128
+
+    def comm_init(self, tok, n, rank, timeout_s):
+        if self.fail_init_rank == rank:
+            raise RuntimeError("RCCL ncclCommInitRankConfig timed out: test")
+        return 7
+
+    def comm_status(self, h):
+        self.polls += 1
+        return self.status_seq[min(self.polls - 1, len(self.status_seq) - 1)]
+
+    def comm_abort(self, h):
+        self.aborted.append(h)
+
+
+class _NeverEvent:
+    def query(self):
+        return False
+
+    def synchronize(self):
+        raise AssertionError("the watchdog must poll, not block")
+
+
+def test_watchdog_aborts_on_async_error():
+    """an asynchronous RCCL error seen while waiting on the device -> ncclCommAbort + CollectiveError"""
+    from pytorch_dppo_amd.parallel.dist import CollectiveError, DistContext, NativeComm
+    ext = _FakeCommExt(status_seq=[0, 0, 0, 5])
+    ctx = DistContext(rank=0, world_size=2, timeout_s=60.0)
+    ctx.native = NativeComm(ext, 7, 2)
+    t0 = time.time()
+    with pytest.raises(CollectiveError, match="state 5"):
+        ctx.wait_event(_NeverEvent())
+    assert ext.aborted == [7] and time.time() - t0 < 10
+
+
+def test_watchdog_aborts_after_timeout():
+    """no completion within dist_timeout_s (a peer that died silently) -> abort + CollectiveError"""
+    from pytorch_dppo_amd.parallel.dist import CollectiveError, DistContext, NativeComm
+    ext, ext_side = _FakeCommExt(), _FakeCommExt()
+    ctx = DistContext(rank=1, world_size=2, timeout_s=0.3)
+    ctx.native, ctx.native_side = NativeComm(ext, 3, 2), NativeComm(ext_side, 4, 2)
+    t0 = time.time()
+    with pytest.raises(CollectiveError, match="did not complete"):
+        ctx.wait_event(_NeverEvent())
+    el = time.time() - t0
+    assert 0.3 <= el < 5, el
+    assert ext.aborted == [3] and ext_side.aborted == [4]      # both communicators aborted
+
+
+def test_heartbeat_dead_peer_aborts_communicators_before_exit():
+    from pytorch_dppo_amd.utils.heartbeat import Heartbeat
+    calls = []
+
+    class Store:
+        def set(self, k, v):
+            pass
+
+    hb = Heartbeat(Store(), 0, 2, 0.1, 0.2, on_dead=None, abort=lambda msg: calls.append(msg))
+    import pytorch_dppo_amd.utils.heartbeat as hbm
+    real_exit = hbm.os._exit
+    hbm.os._exit = lambda code: calls.append(code)
+    try:
+        hb._default_on_dead([1])
+    finally:
+        hbm.os._exit = real_exit
+    assert len(calls) == 2 and "rank(s) [1]" in calls[0] and calls[1] == 75
+
+
+def _worker_comm_create(rank, world, port, out_dir, mode):
+    from pytorch_dppo_amd.parallel.dist import NativeComm
+    _init(rank, world, port, timeout=30.0)
+    ext = _FakeCommExt(fail_id=(mode == "id" and rank == 0), fail_init_rank=(1 if mode == "init" else None), rank=rank)
+    nat = NativeComm.create(ext, rank, world, 5.0, device=torch.device("cpu"))
+    with open(os.path.join(out_dir, f"c{rank}.txt"), "w") as f:
+        f.write("none" if nat is None else "comm")
+
+
+@pytest.mark.parametrize("mode", ["ok", "id", "init"])
+def test_native_comm_creation_is_collective_safe(tmp_path, mode):
+    """rank 0 failing to make the id, or one rank failing its init: EVERY rank falls back together
+    (no rank left waiting in a broadcast or all-reduce the others skipped)"""
+    codes = _join(_spawn(_worker_comm_create, 2, str(tmp_path), mode), 60)
+    assert codes == [0, 0], codes
+    got = [(tmp_path / f"c{r}.txt").read_text() for r in range(2)]
+    assert got == (["comm", "comm"] if mode == "ok" else ["none", "none"]), got
+
+
+def test_params_carry_the_execution_options():
+    """the former DPPO_* environment switches are Params fields / CLI flags"""
+    from pytorch_dppo_amd.config import params_from_args
+    p = params_from_args(["--update-kernels", "tile", "--grad-comm", "process_group", "--dist-backend", "gloo",
+                          "--fused-apply", "false", "--stats-stream", "on", "--wgrad-wgs", "128"])
+    assert (p.update_kernels, p.grad_comm, p.dist_backend, p.fused_apply, p.stats_stream, p.wgrad_wgs) == \
+        ("tile", "process_group", "gloo", False, "on", 128)
+    with pytest.raises(ValueError):
+        Params(update_kernels="bogus")
+    assert Params().heartbeat_interval(1) == 0.0 and Params().heartbeat_interval(8) == 5.0
+    assert Params(heartbeat_s=0).heartbeat_interval(8) == 0.0
