@@ -101,12 +101,12 @@ int64_t wimg_extent(const Layout& L) {
 }
 
 // ------------------------------------------------------------------------------------------
-void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len, torch::Tensor ep_ret,
-             torch::Tensor wimg, std::vector<int64_t> layout, std::vector<double> scales, torch::Tensor flat,
-             torch::Tensor mean, torch::Tensor inv_std, torch::Tensor shift, torch::Tensor x_out,
-             torch::Tensor actions, torch::Tensor logp, torch::Tensor rewards, torch::Tensor dones,
-             torch::Tensor mom, torch::Tensor epstat, std::vector<int64_t> ints, std::vector<int64_t> keys,
-             double reward_clip, torch::Tensor qscale, torch::Tensor xT_out, int64_t xT_rows) {
+RolloutArgs rollout_args(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len, torch::Tensor ep_ret,
+                         torch::Tensor wimg, std::vector<int64_t> layout, std::vector<double> scales, torch::Tensor flat,
+                         torch::Tensor mean, torch::Tensor inv_std, torch::Tensor shift, torch::Tensor x_out,
+                         torch::Tensor actions, torch::Tensor logp, torch::Tensor rewards, torch::Tensor dones,
+                         torch::Tensor mom, torch::Tensor epstat, std::vector<int64_t> ints, std::vector<int64_t> keys,
+                         double reward_clip, torch::Tensor qscale, torch::Tensor xT_out, int64_t xT_rows) {
   TORCH_CHECK(ints.size() == 11, "ints: kind,E,O,A,S,T,t_base,buf_E,t0,limit,std_var");
   TORCH_CHECK(keys.size() == 4, "keys: env,term,reset,action");
   TORCH_CHECK(rows == 16 || rows == 32, "rows must be 16 or 32");
@@ -175,8 +175,69 @@ void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len
     TORCH_CHECK(g_roll_tstamp_numel >= (int64_t)nblk * 8 * 8, "rollout tstamp buffer too small");
     a.tstamp = g_roll_tstamp;
   }
+  return a;
+}
+
+void rollout(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len, torch::Tensor ep_ret,
+             torch::Tensor wimg, std::vector<int64_t> layout, std::vector<double> scales, torch::Tensor flat,
+             torch::Tensor mean, torch::Tensor inv_std, torch::Tensor shift, torch::Tensor x_out,
+             torch::Tensor actions, torch::Tensor logp, torch::Tensor rewards, torch::Tensor dones,
+             torch::Tensor mom, torch::Tensor epstat, std::vector<int64_t> ints, std::vector<int64_t> keys,
+             double reward_clip, torch::Tensor qscale, torch::Tensor xT_out, int64_t xT_rows) {
+  RolloutArgs a = rollout_args(dt, rows, state, ep_len, ep_ret, wimg, layout, scales, flat, mean, inv_std, shift,
+                               x_out, actions, logp, rewards, dones, mom, epstat, ints, keys, reward_clip, qscale,
+                               xT_out, xT_rows);
   launch_rollout((int)dt, a, (int)rows, cur_stream());
   after_launch(__func__);
+}
+
+// The per-step observation-normalisation rollout (obs_norm_update = "step") as ONE cooperative
+// launch (csrc/rollout.hip sn_step): `sn` = [mean f64, m2 f64, mean_f32, inv_std] of the stats the
+// steps absorb (updated in place), g1 / g2 the granule buffers (int64, zero-initialised once; tags
+// never reused: epoch0 grows by T per launch), err an int32 timeout word.  The launch's own
+// normalisation inputs (mean / inv_std) are ignored: every step takes the freshly merged stats.
+void rollout_stepnorm(int64_t dt, int64_t rows, torch::Tensor state, torch::Tensor ep_len, torch::Tensor ep_ret,
+                      torch::Tensor wimg, std::vector<int64_t> layout, std::vector<double> scales, torch::Tensor flat,
+                      torch::Tensor shift, torch::Tensor x_out, torch::Tensor actions, torch::Tensor logp,
+                      torch::Tensor rewards, torch::Tensor dones, torch::Tensor mom, torch::Tensor epstat,
+                      std::vector<int64_t> ints, std::vector<int64_t> keys, double reward_clip, torch::Tensor qscale,
+                      std::vector<torch::Tensor> sn, torch::Tensor g1, torch::Tensor g2, torch::Tensor err,
+                      double n0, int64_t epoch0, double var_floor) {
+  TORCH_CHECK(sn.size() == 4, "sn: mean f64, m2 f64, mean_f32, inv_std");
+  RolloutArgs a = rollout_args(dt, rows, state, ep_len, ep_ret, wimg, layout, scales, flat, sn[2], sn[3], shift,
+                               x_out, actions, logp, rewards, dones, mom, epstat, ints, keys, reward_clip, qscale,
+                               torch::Tensor(), 0);
+  TORCH_CHECK(a.t_base == 0, "the per-step normalisation launch covers the whole rollout");
+  const int nblk = (a.E + (int)rows - 1) / (int)rows;
+  check(sn[0], "sn mean", at::kDouble, a.O);
+  check(sn[1], "sn m2", at::kDouble, a.O);
+  TORCH_CHECK(sn[2].data_ptr() != shift.data_ptr(), "the shift must not alias the stats being merged into");
+  check(g1, "g1", at::kLong, (int64_t)nblk * 2 * a.O);
+  check(g2, "g2", at::kLong, 2 * (int64_t)a.O);
+  check(err, "err", at::kInt, 1);
+  TORCH_CHECK(epoch0 >= 1 && epoch0 + a.T < (int64_t)UINT32_MAX, "epoch0");
+  a.sn_mean = sn[0].data_ptr<double>();
+  a.sn_m2 = sn[1].data_ptr<double>();
+  a.sn_mean_f32 = sn[2].data_ptr<float>();
+  a.sn_inv_std = sn[3].data_ptr<float>();
+  a.sn_g1 = reinterpret_cast<unsigned long long*>(g1.data_ptr<int64_t>());
+  a.sn_g2 = reinterpret_cast<unsigned long long*>(g2.data_ptr<int64_t>());
+  a.sn_err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
+  a.sn_n0 = n0;
+  a.sn_epoch0 = (unsigned)epoch0;
+  a.sn_var_floor = var_floor;
+  launch_rollout((int)dt, a, (int)rows, cur_stream());
+  after_launch(__func__);
+}
+
+// the largest env-tile grid the per-step normalisation launch can run co-resident
+int64_t rollout_stepnorm_cap_b(int64_t dt, int64_t rows, std::vector<int64_t> layout, int64_t O, int64_t A, int64_t S) {
+  Layout L = parse_layout(layout);
+  RolloutArgs a{};
+  a.O = (int)O; a.A = (int)A; a.S = (int)S;
+  a.d1 = L.d_in[0]; a.d2 = L.d_in[1]; a.d3 = L.d_in[2];
+  a.sn_g1 = reinterpret_cast<unsigned long long*>(1);   // (only selects the LDS size of the SN kernel)
+  return (int64_t)::rollout_stepnorm_cap((int)dt, a, (int)rows);
 }
 
 // idx_limit: exclusive upper bound every gathered row index must respect (rows of x_buf and of
@@ -705,6 +766,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X-native DPPO kernels (gfx950 HIP)";
   register_comm(m);
   m.def("rollout", &rollout);
+  m.def("rollout_stepnorm", &rollout_stepnorm);
+  m.def("rollout_stepnorm_cap", &rollout_stepnorm_cap_b);
   m.def("mlp_value", &mlp_value);
   m.def("mlp_train", &mlp_train);
   m.def("head_applies", &head_applies);

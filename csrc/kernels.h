@@ -42,6 +42,25 @@ struct RolloutArgs {
   float* mom;          // [nblk][2][O]  sum(x-shift), sum((x-shift)^2)
   float* epstat;       // [nblk][2]     finished-episode return sum, count
   unsigned long long* tstamp;  // DIAGNOSTIC ONLY (null in real runs): [nblk][NW][8] phase cycles
+  // Per-step observation normalisation INSIDE the launch (obs_norm_update = "step", the reference's
+  // filter that absorbs every observation before normalising it, model.py:68 / train.py:84-85);
+  // sn_g1 == null: off (mean / inv_std above are fixed for the launch).  Step t, all workgroups
+  // co-resident (cooperative launch): each publishes its batch moments about `shift` as 8-byte
+  // {tag, fp32} granules (sn_g1[blk][2O]); workgroup b sums features b, b + nblk, ... over all
+  // workgroups in a fixed order (fp64), Chan-merges them into the fp64 running stats (sn_mean,
+  // sn_m2: each feature owned by ONE workgroup for the whole launch) and publishes the new fp32
+  // (mean, 1/std) as granules (sn_g2[2O]); every workgroup gathers those and normalises.  Tags
+  // are sn_epoch0 + t (the host never reuses one: no memset), spins are bounded (sn_err).
+  double* sn_mean;           // [O] running mean (fp64, in place)
+  double* sn_m2;             // [O] running sum of squared deviations (fp64, in place)
+  float* sn_mean_f32;        // [O] fp32 images after the last step (host-visible)
+  float* sn_inv_std;         // [O]
+  unsigned long long* sn_g1; // [nblk][2O] partial-moment granules
+  unsigned long long* sn_g2; // [2O] stats granules
+  unsigned* sn_err;          // nonzero: a spin timed out (the launch gave up; the host raises)
+  double sn_n0;              // running count before step 0 (each step adds E)
+  unsigned sn_epoch0;        // tag of step 0's granules (>= 1)
+  double sn_var_floor;
 };
 
 // fp8 mode's gradient-amax ring (csrc/common.h Q8): [3 slots][4 tensors][Q8_SUB sub-slots][Q8_LINE]
@@ -175,6 +194,7 @@ int dppo_take_error(char* msg, int cap);
 void launch_debug_invalid(double* out, hipStream_t s);   // test hook: a launch the runtime refuses
 void launch_rollout(int dt, const RolloutArgs& a, int rows, hipStream_t s);
 void set_rollout_waves(int nw);                 // 4 or 8 waves per rollout workgroup (A/B)
+int rollout_stepnorm_cap(int dt, const RolloutArgs& a, int rows);   // co-resident grid of the SN launch
 void launch_mlp_value(int dt, const MlpArgs& a, hipStream_t s);
 void launch_mlp_train(int dt, const MlpArgs& a, hipStream_t s);
 size_t mlp_train_lds_bytes(int dt, const MlpArgs& a);

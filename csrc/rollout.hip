@@ -36,10 +36,103 @@ DEV float env_obs(const float* st, int S, int r, int d) {
   }
 }
 
+// ---- per-step observation normalisation inside the launch (RolloutArgs sn_*) ----
+// 8-byte {tag, fp32 bits} granules, stored and loaded relaxed at agent scope (sc1 vector accesses:
+// MI355X_MICROARCH.md "granule"): the data is its own flag, so a hand-off needs no fence and no
+// separate flag word.  Every spin is bounded: on a timeout the launch gives up (sn_err) instead of
+// leaving waves that never finish.
+typedef unsigned long long u64;
+constexpr unsigned SN_SPIN_MAX = 1u << 21;   // >= ~1 s of polling per hand-off
+constexpr int SN_MAX_BLOCKS = 1024;          // grid cap of the per-step normalisation launch
+DEV void sn_put(u64* g, unsigned tag, float v) {
+  __hip_atomic_store(g, ((u64)tag << 32) | (u64)__float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV u64 sn_get(const u64* g) {
+  return __hip_atomic_load(const_cast<u64*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV float sn_val(u64 x) { return __uint_as_float((unsigned)x); }
+
+// Wave 0 of workgroup `blk`: the step's Chan merge of the features it owns (d = blk, blk + nblk,
+// ...): the fp32 partials of all nblk workgroups summed in fp64 in a fixed order (lane l holds
+// workgroups l, l + 64, ... in that order; then an xor butterfly, which leaves the same bits in
+// every lane), merged into the running (mean, M2) — csrc/obs.hip obs_merge's formulas — and
+// published as the (mean, 1/std) granules.  Then it gathers every feature's new granules into
+// LDS.  Returns false on a timeout.
+DEV bool sn_step(const RolloutArgs& a, int blk, int nblk, int step, int lane, const float* shs, float* nm,
+                 float* ninv) {
+  const int O = a.O;
+  const unsigned tag = a.sn_epoch0 + (unsigned)step;
+  const u64* g1 = a.sn_g1;
+  unsigned spins = 0;
+  // (two passes per hand-off — poll the tags until all match, then read the values — so no
+  // register array holds a whole sweep: the kernel around this is at its register budget)
+  auto ready1 = [&](int d) {
+    bool ok = true;
+    for (int w = lane; w < nblk; w += 64)
+      ok &= (unsigned)(sn_get(g1 + (size_t)w * 2 * O + d) >> 32) == tag &&
+            (unsigned)(sn_get(g1 + (size_t)w * 2 * O + O + d) >> 32) == tag;
+    return ok;
+  };
+  for (int d = blk; d < O; d += nblk) {
+    while (!__all(ready1(d))) {
+      if (++spins > SN_SPIN_MAX) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    double p1 = 0.0, p2 = 0.0;
+    for (int w = lane; w < nblk; w += 64) {
+      p1 += (double)sn_val(sn_get(g1 + (size_t)w * 2 * O + d));
+      p2 += (double)sn_val(sn_get(g1 + (size_t)w * 2 * O + O + d));
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      p1 += __shfl_xor(p1, o, 64);
+      p2 += __shfl_xor(p2, o, 64);
+    }
+    if (lane == 0) {
+      const double count = (double)a.E, n_a = a.sn_n0 + (double)step * count;
+      const double bmean_d = p1 / count;
+      const double bmean = (double)shs[d] + bmean_d;
+      double bm2 = p2 - p1 * bmean_d;
+      if (bm2 < 0.0) bm2 = 0.0;
+      const double n = n_a + count;
+      const double mean0 = a.sn_mean[d];
+      const double delta = bmean - mean0;
+      const double mu = mean0 + delta * (count / n);
+      const double M2 = a.sn_m2[d] + bm2 + delta * delta * (n_a * count / n);
+      double var = M2 / n;
+      if (var < a.sn_var_floor) var = a.sn_var_floor;
+      const float muf = (float)mu, inv = (float)(1.0 / sqrt(var));
+      a.sn_mean[d] = mu;
+      a.sn_m2[d] = M2;
+      a.sn_mean_f32[d] = muf;
+      a.sn_inv_std[d] = inv;
+      sn_put(a.sn_g2 + d, tag, muf);
+      sn_put(a.sn_g2 + O + d, tag, inv);
+    }
+  }
+  // gather every feature's (mean, 1/std) of this step
+  auto ready2 = [&]() {
+    bool ok = true;
+    for (int i = lane; i < 2 * O; i += 64) ok &= (unsigned)(sn_get(a.sn_g2 + i) >> 32) == tag;
+    return ok;
+  };
+  while (!__all(ready2())) {
+    if (++spins > SN_SPIN_MAX) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  for (int i = lane; i < 2 * O; i += 64) {
+    const float v = sn_val(sn_get(a.sn_g2 + i));
+    if (i < O) nm[i] = v;
+    else ninv[i - O] = v;
+  }
+  return true;
+}
+
 // NW waves per workgroup: a 16-env tile is one workgroup per CU at E = 4096, so the 8-wave
 // form (2 waves per SIMD) doubles the threads of the VALU-heavy observe / sample / env phases
 // and gives the SIMDs a second wave to hide latency with; the MFMA layers use the first waves.
-template <int DT, int ROWS, int NW>
+// SN: per-step observation normalisation inside the launch (RolloutArgs sn_*; cooperative launch)
+template <int DT, int ROWS, int NW, bool SN>
 __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   using P = Prec<DT>;
   using T = typename P::T;
@@ -70,6 +163,11 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   float* wdrv = cv.take<float>(S);                // synthetic dynamics: drive weight of state dim d
   int* jdx = cv.take<int>(S);                     //                     action index driving dim d
   float* lsg = cv.take<float>(2 * A);             // per action dim: log sigma [0, A), sigma [A, 2A)
+  // SN: the iteration shift and this step's (mean, 1/std) of every feature; the timeout flag
+  float* shs = SN ? cv.take<float>(O) : nullptr;
+  float* nm = SN ? cv.take<float>(O) : nullptr;
+  float* ninv = SN ? cv.take<float>(O) : nullptr;
+  int* sn_fail = SN ? cv.take<int>(1) : nullptr;
   // fp8: the MFMA tile is e4m3 but the buffer rows are bf16 — a bf16 staging tile lets them
   // leave as 16-byte row chunks (element stores strided by the row length were 2.6x the bf16
   // kernel's time)
@@ -96,6 +194,10 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   preset_pad<DT>(h1, ld2, ROWS, a.n1, tid, NTHR);   // the layers' epilogues write columns < n
   preset_pad<DT>(h2, ld3, ROWS, a.n2, tid, NTHR);
   for (int d = tid; d < O; d += NTHR) { s1[d] = 0.f; s2[d] = 0.f; }
+  if constexpr (SN) {
+    for (int d = tid; d < O; d += NTHR) shs[d] = a.shift[d];
+    if (tid == 0) *sn_fail = 0;
+  }
   for (int d = tid; d < S; d += NTHR) {   // per-dim constants once per launch (no per-step modulo)
     wdrv[d] = 0.5f + (float)(d % 7) / 7.0f;
     jdx[d] = d % A;
@@ -149,7 +251,11 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
       constexpr int KIND = decltype(kind_tag)::value;
       for (int d = tid; d < a.d1; d += NTHR) {
         float m = hm, is = his, sh = hsh;
-        if (d != tid && d < O) { m = a.mean[d]; is = a.inv_std[d]; sh = a.shift[d]; }
+        if constexpr (SN) {
+          if (d < O) { m = nm[d]; is = ninv[d]; }
+        } else {
+          if (d != tid && d < O) { m = a.mean[d]; is = a.inv_std[d]; sh = a.shift[d]; }
+        }
         float ls1 = 0.f, ls2 = 0.f;
         GT grp[ROWS];   // this feature's ROWS consecutive buffer rows (xT groups of 8)
 #pragma unroll
@@ -157,7 +263,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
           float xv;
           if (d < O) {
             float o = env_obs<KIND>(st, S, r, d);
-            if (!last && r < nvalid) { float dd = o - sh; ls1 += dd; ls2 += dd * dd; }
+            if (!SN && !last && r < nvalid) { float dd = o - sh; ls1 += dd; ls2 += dd * dd; }
             xv = fminf(fmaxf((o - m) * is, -5.f), 5.f);
           } else {
             xv = (d == O) ? 1.f : 0.f;
@@ -167,7 +273,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
           else grp[r] = PX::cvt(xv);
           if constexpr (STAGE) xsb[r * a.d1 + d] = grp[r];
         }
-        if (d < O) { s1[d] += ls1; s2[d] += ls2; }
+        if (!SN && d < O) { s1[d] += ls1; s2[d] += ls2; }
         // full-batch update operand: rows m = tb*E + e0 + r are contiguous 8-groups of the FM
         // layout (host guarantees E % 16 == 0), written once per rollout instead of per epoch
         if (a.xT_out != nullptr && !last) {
@@ -198,6 +304,43 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
         }
       }
     };
+    if constexpr (SN) {
+      if (!last) {
+        // this step's batch moments about the iteration shift -> the iteration's moments (as in
+        // rollout mode) and this workgroup's granules; wave 0 merges its features and gathers
+        // the new stats of every feature (sn_step); the others wait at the barrier
+        const unsigned tag = a.sn_epoch0 + (unsigned)step;
+        auto moments = [&](auto kind_tag) {
+          constexpr int KIND = decltype(kind_tag)::value;
+          for (int d = tid; d < O; d += NTHR) {
+            const float sh = shs[d];
+            float ls1 = 0.f, ls2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r)
+              if (r < nvalid) {
+                const float dd = env_obs<KIND>(st, S, r, d) - sh;
+                ls1 += dd;
+                ls2 += dd * dd;
+              }
+            s1[d] += ls1;
+            s2[d] += ls2;
+            u64* g = a.sn_g1 + (size_t)blockIdx.x * 2 * O;
+            sn_put(g + d, tag, ls1);
+            sn_put(g + O + d, tag, ls2);
+          }
+        };
+        if (a.kind == 1) moments(std::integral_constant<int, 1>{});
+        else moments(std::integral_constant<int, 0>{});
+        if (wave == 0 && !sn_step(a, (int)blockIdx.x, (int)gridDim.x, step, lane, shs, nm, ninv)) {
+          if (lane == 0) {
+            *sn_fail = 1;
+            __hip_atomic_store(a.sn_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        __syncthreads();
+        if (*sn_fail) return;   // a peer never published: give up (the host raises)
+      }
+    }
     if (a.kind == 1) observe(std::integral_constant<int, 1>{});
     else observe(std::integral_constant<int, 0>{});
     if (!last) layer_prefetch<DT, ROWS, NW>(pf, W1, a.d1, a.n1, wave, lane);
@@ -439,6 +582,7 @@ size_t rollout_lds(const RolloutArgs& a) {
   b += al(sizeof(uint32_t) * 3 * ROWS);
   b += al(sizeof(float) * a.S) + al(sizeof(int) * a.S);
   b += al(sizeof(float) * 2 * a.A);
+  if (a.sn_g1 != nullptr) b += 3 * al(sizeof(float) * a.O) + al(sizeof(int));
   if (DT == DT_FP8) b += al(sizeof(__bf16) * ROWS * a.d1);   // bf16 staging tile of the buffer rows
   return b;
 }
@@ -449,10 +593,51 @@ template <int DT, int ROWS, int NW>
 void launch_nw(const RolloutArgs& a, hipStream_t s) {
   const size_t lds = rollout_lds<DT, ROWS>(a);
   const int nblk = (a.E + ROWS - 1) / ROWS;
-  if (lds > 65536)
-    set_max_lds_once<rollout_kernel<DT, ROWS, NW>>(lds);
-  hipLaunchKernelGGL((rollout_kernel<DT, ROWS, NW>), dim3(nblk), dim3(NW * 64), lds, s, a);
-  HIP_CHECK_LAUNCH();
+  if (a.sn_g1 == nullptr) {
+    if (lds > 65536) set_max_lds_once<rollout_kernel<DT, ROWS, NW, false>>(lds);
+    hipLaunchKernelGGL((rollout_kernel<DT, ROWS, NW, false>), dim3(nblk), dim3(NW * 64), lds, s, a);
+    HIP_CHECK_LAUNCH();
+    return;
+  }
+  // per-step normalisation: every workgroup must be resident at once (the hand-offs wait on all
+  // of them).  Cooperative launch: the runtime refuses a grid that cannot be co-resident; the
+  // grid is also kept one workgroup per CU below the occupancy answer (MI355X_MICROARCH.md:
+  // the API can overstate residency by one per CU)
+  auto kfn = rollout_kernel<DT, ROWS, NW, true>;
+  if (lds > 65536) set_max_lds_once<rollout_kernel<DT, ROWS, NW, true>>(lds);
+  int per_cu = 0, dev = 0, ncu = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kfn), NW * 64, lds);
+  if (e == hipSuccess) e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) {
+    dppo_note_error(e, __FILE__, __LINE__);
+    return;
+  }
+  const int cap = ncu * (per_cu > 1 ? per_cu - 1 : per_cu);
+  if (nblk > cap || nblk > SN_MAX_BLOCKS) {
+    dppo_note_error(hipErrorCooperativeLaunchTooLarge, __FILE__, __LINE__);
+    return;
+  }
+  RolloutArgs aa = a;
+  void* args[] = {&aa};
+  e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kfn), dim3(nblk), dim3(NW * 64), args, (unsigned)lds, s);
+  if (e != hipSuccess) dppo_note_error(e, __FILE__, __LINE__);
+}
+
+// the largest grid the per-step normalisation launch accepts (0: none)
+template <int DT, int ROWS, int NW>
+int stepnorm_cap(const RolloutArgs& a) {
+  const size_t lds = rollout_lds<DT, ROWS>(a);
+  auto kfn = rollout_kernel<DT, ROWS, NW, true>;
+  if (lds > 65536) set_max_lds_once<rollout_kernel<DT, ROWS, NW, true>>(lds);
+  int per_cu = 0, dev = 0, ncu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kfn), NW * 64, lds) !=
+          hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const int cap = ncu * (per_cu > 1 ? per_cu - 1 : per_cu);
+  return cap < SN_MAX_BLOCKS ? cap : SN_MAX_BLOCKS;
 }
 
 template <int DT, int ROWS>
@@ -461,10 +646,29 @@ void launch_t(const RolloutArgs& a, hipStream_t s) {
   if (g_rollout_waves == 4 || DT == DT_F32 || ROWS > 16) launch_nw<DT, ROWS, 4>(a, s);
   else launch_nw<DT, ROWS, 8>(a, s);
 }
+template <int DT, int ROWS>
+int cap_t(const RolloutArgs& a) {
+  if (g_rollout_waves == 4 || DT == DT_F32 || ROWS > 16) return stepnorm_cap<DT, ROWS, 4>(a);
+  return stepnorm_cap<DT, ROWS, 8>(a);
+}
 
 }  // namespace
 
 extern "C" void set_rollout_waves(int nw) { g_rollout_waves = nw; }
+
+// workgroups the per-step normalisation launch can hold co-resident (its grid must not exceed it)
+extern "C" int rollout_stepnorm_cap(int dt, const RolloutArgs& a, int rows) {
+  if (rows == 32) {
+    if (dt == DT_F32) return cap_t<DT_F32, 32>(a);
+    if (dt == DT_BF16) return cap_t<DT_BF16, 32>(a);
+    if (dt == DT_S3) return cap_t<DT_S3, 32>(a);
+    return cap_t<DT_FP8, 32>(a);
+  }
+  if (dt == DT_F32) return cap_t<DT_F32, 16>(a);
+  if (dt == DT_BF16) return cap_t<DT_BF16, 16>(a);
+  if (dt == DT_S3) return cap_t<DT_S3, 16>(a);
+  return cap_t<DT_FP8, 16>(a);
+}
 
 extern "C" void launch_rollout(int dt, const RolloutArgs& a, int rows, hipStream_t s) {
   if (rows == 32) {

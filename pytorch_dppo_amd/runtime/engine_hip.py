@@ -139,6 +139,9 @@ class HipEngine:
         self.epstat = torch.zeros(nroll, 2, **f32)
         self.ep_sum = torch.zeros(2, dtype=torch.float64, device=device)
         self._step_bufs = None     # per-step obs-norm mode: the steps' rollout moments / episode stats
+        self._sn_cap = None        # per-step obs-norm launch: co-resident grid cap of this device
+        self._sn_bufs = None       # its granule buffers, timeout word (+ pinned copy)
+        self._sn_epoch = 1         # its next granule tag (never reused)
         self._obs_scratch = None   # obs_observe partials + fp64 sums
         # ---- update geometry ----
         self.mb = params.minibatch_rows()
@@ -565,6 +568,41 @@ class HipEngine:
                          self.mom if mom is None else mom, self.epstat if epstat is None else epstat, ints, keys,
                          float(self.p.reward_clip), self.qscale, xt, self.x_rows[0])
 
+    def _stepnorm_fits(self) -> bool:
+        """the per-step normalisation launch holds every env tile co-resident on this device"""
+        if self._sn_cap is None:
+            e = self.env
+            self._sn_cap = int(self.ext.rollout_stepnorm_cap(self.dt_fwd, ROLL_ROWS, self.layout, self.O, self.A,
+                                                              e.state_dim))
+        return self.mom.shape[0] <= self._sn_cap
+
+    def _launch_stepnorm(self, ls: RunningObsStats, shift: torch.Tensor) -> None:
+        """obs_norm_update='step' as one cooperative rollout launch: every step merges its batch
+        into ``ls`` (in place, fp64) before normalising it (csrc/rollout.hip sn_step)."""
+        if self._sn_bufs is None:
+            nroll = self.mom.shape[0]
+            self._sn_bufs = (torch.zeros(nroll * 2 * self.O, dtype=torch.int64, device=self.device),
+                             torch.zeros(2 * self.O, dtype=torch.int64, device=self.device),
+                             torch.zeros(1, dtype=torch.int32, device=self.device),
+                             torch.zeros(1, dtype=torch.int32, pin_memory=True))
+        g1, g2, err, err_host = self._sn_bufs
+        if int(err_host[0]) != 0:   # (staged after an earlier launch: no sync here)
+            raise RuntimeError("per-step observation normalisation launch timed out waiting for a workgroup")
+        e = self.env
+        kp = e.kernel_params()
+        ints = [kp["kind"], self.E, self.O, self.A, e.state_dim, self.T, 0, self.E, e.t & 0xFFFFFFFF,
+                kp["limit"], 1 if self.p.std_convention == "var" else 0]
+        keys = [kp["key_env"], kp["key_term"], kp["key_reset"], self.key_action]
+        self.ext.rollout_stepnorm(self.dt_fwd, ROLL_ROWS, e.state, e.ep_len, e.ep_ret, self.wimg_fwd, self.layout,
+                                  self.scales, self.model.flat.data, shift, self.x_buf, self.actions, self.logp,
+                                  self.rewards, self.dones, self.mom, self.epstat, ints, keys,
+                                  float(self.p.reward_clip), self.qscale,
+                                  [ls.mean, ls.mean_diff, ls.mean_f32, ls.inv_std_f32], g1, g2, err, float(ls.n),
+                                  self._sn_epoch, 1e-2)
+        self._sn_epoch += self.T
+        ls.n += float(self.N)
+        err_host.copy_(err, non_blocking=True)
+
     def _observe_step(self, norm: RunningObsStats, obs: torch.Tensor, shift: torch.Tensor) -> None:
         """norm.observes(obs) as three device launches (csrc/obs.hip obs_observe), moments about
         the iteration's shift snapshot."""
@@ -684,14 +722,22 @@ class HipEngine:
         else:
             # per-step obs-norm mode (the reference's filter updates with every observation before
             # normalising it, model.py:68 / train.py:84): step t's normalisation needs the stats of
-            # step t's batch, a grid-wide dependency, so each step is one observe (csrc/obs.hip:
-            # moments -> reduce -> merge into the worker-local stats) + a one-step rollout launch.
-            # The steps' rollout moments / episode stats land in per-step slices and ONE reduce
-            # after the loop gives the iteration's totals.  No host sync.
+            # step t's batch, a grid-wide dependency.  Default: ONE cooperative launch whose
+            # workgroups exchange each step's moments and merged stats in-kernel
+            # (csrc/rollout.hip sn_step), into the worker-local stats.  Fallback (the env tiles do
+            # not fit co-resident): per step one observe (csrc/obs.hip: moments -> reduce -> merge)
+            # + a one-step rollout launch, the steps' moments / episode stats in per-step slices
+            # and ONE reduce after the loop.  No host sync either way.
             self._flush_value()
             shift = self.stats.shift().clone()
             ls = self.local_stats = RunningObsStats(self.O, self.device)
             ls.copy_from(self.stats)
+            if self._stepnorm_fits():
+                self._launch_stepnorm(ls, shift)
+                self.env.t += self.T
+                self.ext.obs_reduce(self.mom, self.mom.shape[0], self.O, self.s12, self.epstat, self.ep_sum)
+                return {"count": float(self.N), "s1": self.s12[0], "s2": self.s12[1], "shift": shift,
+                        "ep_return_sum": self.ep_sum[0], "ep_count": self.ep_sum[1], "ep2": self.ep_sum}
             T, nroll = self.T, self.mom.shape[0]
             if self._step_bufs is None or self._step_bufs[0].shape[0] != T:
                 f32 = dict(dtype=torch.float32, device=self.device)
