@@ -414,7 +414,12 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   float* mus = tpb;                        // (loss) mu [32][32] | v [32]
 
   auto src_of = [&](int r) __attribute__((always_inline)) {
+#ifdef DPPO_ABL_XL2
+    // ABLATION (timing only, wrong numerics): every workgroup reads the same 1,024 rows (L2-resident)
+    const int rr = (int)(blockIdx.x & 7) * ROWS + r;
+#else
     const int rr = (m0 + r < a.M) ? m0 + r : m0;   // rows past M re-read row m0 (zero gradient)
+#endif
     return a.idx ? a.idx[rr] : a.row0 + rr;
   };
   const int mw = m0 + WROWS * wave;
@@ -472,6 +477,10 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   __amdgpu_buffer_rsrc_t rw8 = rw;
   if constexpr (F8) rw8 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W8), (short)0, 0x7fffffff, 0x00020000);
   auto issue = [&](int st, int stage) __attribute__((always_inline)) {
+#ifdef DPPO_ABL_NOWDMA
+    // ABLATION (timing only, wrong numerics): the ring keeps its primed fragments
+    if (st >= S - 1) return;
+#endif
     const int l = min(st, MAX_STEPS - 1);
     const uint32_t w01 = __builtin_amdgcn_readlane(cw0, l);
     const uint32_t w23 = SPW > 2 ? __builtin_amdgcn_readlane(cw1, l) : 0u;
@@ -547,6 +556,10 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     return stg;
   };
 
+#ifdef DPPO_HD_PRIO
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+  if (__builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   HD_STAMP(0);
   // Q8: wave 0 DMAs the previous step's sub-slot maxima of the head's two gradient tensors into
   // LDS — the oldest vector-memory ops of the wave (never behind a counted wait), read after many
@@ -1182,7 +1195,18 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     if (blockIdx.x == 0 && tid < 2 * Q8_SUB) a.q8_clr[(2 * HEAD * Q8_SUB + tid) * Q8_LINE] = 0u;
   }
   // ---------------- per-workgroup partials (deterministic fixed order) ----------------
+#ifdef DPPO_HD_NODRAIN
+  // no DMA may outlive the workgroup's LDS (or overlap its reuse below): wait for the last ring
+  // refill, not for the g1^T stores of the last two dgrad stages issued after it (vector-memory
+  // operations retire in issue order; the stamps / Q8 atomics after them are not counted, so the
+  // wait is at least this long)
+  {
+    constexpr int tiles_last2 = (C::N1R < 4 * C::NS4 ? C::N1R : 4 * C::NS4) - 4 * (C::NS4 - 2);
+    WAIT_VMCNT((tiles_last2 * H::SPS * RB) & 63);
+  }
+#else
   WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
+#endif
   __syncthreads();
   if constexpr (HEAD == 0) {
     // the 8 waves' dW_mu tiles [32][128] through the (now idle) 64 KiB ring in two rounds:

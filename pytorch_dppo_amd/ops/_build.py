@@ -58,7 +58,7 @@ def _digest(paths, extra: str) -> str:
     return h.hexdigest()[:16]
 
 
-def _compile(src: str, cflags, verbose: bool, csrc: str = CSRC) -> str:
+def _compile(src: str, cflags, verbose: bool, csrc: str = CSRC, extra=()) -> str:
     srcp = os.path.join(csrc, src)
     deps = [srcp] + [os.path.join(csrc, h) for h in HEADERS]
     # -amdgpu-mfma-vgpr-form: MFMA accumulators in ordinary VGPRs (gfx90a+ unified register
@@ -68,7 +68,7 @@ def _compile(src: str, cflags, verbose: bool, csrc: str = CSRC) -> str:
             "-mllvm", "-amdgpu-mfma-vgpr-form"]
     # A/B builds of compile-time variants (e.g. DPPO_EXTRA_CFLAGS="-DDPPO_X_CACHED"); the
     # flags enter the object cache key, so switching back rebuilds nothing stale
-    base += os.environ.get("DPPO_EXTRA_CFLAGS", "").split()
+    base += os.environ.get("DPPO_EXTRA_CFLAGS", "").split() + list(extra)
     flags = base + cflags
     key = _digest(deps, " ".join(flags))
     obj = os.path.join(BUILD, f"{os.path.splitext(src)[0]}-{key}.o")
@@ -83,16 +83,17 @@ def _compile(src: str, cflags, verbose: bool, csrc: str = CSRC) -> str:
     return obj
 
 
-def build(verbose: bool = False, force: bool = False, variant: str = "", csrc: str = CSRC) -> str:
-    """Build the extension.  ``variant`` + ``csrc`` (A/B diagnostics): the same bindings built
-    from another source tree (e.g. an earlier commit's csrc/) as module ``_dppo_hip_<variant>``,
-    loadable next to the default one (ops/native.py load_variant) so two kernel versions can be
-    timed interleaved in one process on one box."""
+def build(verbose: bool = False, force: bool = False, variant: str = "", csrc: str = CSRC, defines=()) -> str:
+    """Build the extension.  ``variant`` + ``csrc`` / ``defines`` (A/B diagnostics): the same
+    bindings built from another source tree (e.g. an earlier commit's csrc/) or with extra -D
+    macros as module ``_dppo_hip_<variant>``, loadable next to the default one (ops/native.py
+    load_variant) so kernel versions can be timed interleaved in one process on one box."""
     os.makedirs(BUILD, exist_ok=True)
     tcflags, ldflags = _torch_flags(EXT_NAME + (f"_{variant}" if variant else ""))
     jobs = [(s, []) for s in DEVICE_SRCS] + [(s, tcflags) for s in HOST_SRCS]
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
-        objs = list(ex.map(lambda j: _compile(j[0], j[1], verbose, csrc), jobs))
+        extra = [f"-D{d}" for d in defines]
+        objs = list(ex.map(lambda j: _compile(j[0], j[1], verbose, csrc, extra), jobs))
     out = ext_path(variant)
     # the object names carry their source digests (hipcc's object bytes are not reproducible
     # across machines), so the stamp names the sources + flags the .so was built from
@@ -118,5 +119,6 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     var = args[args.index("--variant") + 1] if "--variant" in args else ""
     src = args[args.index("--src") + 1] if "--src" in args else CSRC
-    p = build(verbose="-v" in args, force="--force" in args, variant=var, csrc=src)
+    defs = args[args.index("--define") + 1].split(",") if "--define" in args else []
+    p = build(verbose="-v" in args, force="--force" in args, variant=var, csrc=src, defines=defs)
     print(p)

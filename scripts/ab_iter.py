@@ -3,7 +3,12 @@
 Arms run interleaved in ONE process on ONE worker (same box, same clocks): each round runs K
 deferred iterations per arm (the bench's production loop) and reports ms per iteration.
 
-    python scripts/ab_iter.py bf16x3 x_cached,x_stream [rounds] [iters]
+    python scripts/ab_iter.py bf16x3 A,b,c [rounds] [iters]
+
+Arm names: "A" = the default build; a name of the table below = a runtime knob; any other name =
+the variant module _dppo_hip_<name> (ops/_build.py --variant <name> --define ...).  The engine
+state (parameters, Adam moments and step) is restored before every timed block, so an ablation
+variant (wrong numerics by design) cannot leave the next arm different weights.
 """
 import json
 import os
@@ -53,10 +58,25 @@ def main():
     }
     for _ in range(2):
         w.iteration_step()
+    eng = w.engine
+    snap = (w.model.flat.data.clone(), eng.adam_m.clone(), eng.adam_v.clone(), eng.adam_step,
+            w.stats.mean.clone(), w.stats.mean_diff.clone(), w.stats.n)
+
+    def restore():
+        w.model.flat.data.copy_(snap[0])
+        eng.adam_m.copy_(snap[1])
+        eng.adam_v.copy_(snap[2])
+        eng.adam_step = snap[3]
+        w.stats.mean.copy_(snap[4])
+        w.stats.mean_diff.copy_(snap[5])
+        w.stats.n = snap[6]
+        w.stats._refresh()
+        eng.params_changed()
     res = {k: [] for k in want}
     for _ in range(rounds):
         for k in want:
-            arms[k]()
+            (arms[k] if k in arms else (lambda k=k: use_ext(k)))()
+            restore()
             w.iteration_step()                     # settle on the arm
             torch.cuda.synchronize()
             t0 = time.perf_counter()

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Cost of the per-step obs-norm mode (obs_norm_update='step', the reference's per-observation
 filter update, model.py:68) at the bench geometry (Humanoid dims, 4096 envs x 16 steps, bf16x3):
-rollout() and a whole iteration in 'rollout' mode (one fused T-step launch) vs 'step' mode
-(T x [obs_observe + one-step rollout] + one reduce), and 'step' mode with the observe done by
-torch ops (RunningObsStats.observes, the round-2 path) for comparison.  Diagnostics.
+rollout() and a whole iteration in 'rollout' mode (one fused T-step launch) vs 'step' mode as ONE
+cooperative launch (round 4: in-kernel granule hand-offs, csrc/rollout.hip sn_step), 'step_launches'
+(round 3: T x [obs_observe + one-step rollout] + one reduce), and 'step_torch_observe' (round 2:
+the observe by torch ops) for comparison.  Diagnostics.
 
     python scripts/probe_obs_norm_step.py [reps]
 """
@@ -37,12 +38,14 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     out = {}
-    for mode in ("rollout", "step", "step_torch_observe"):
+    for mode in ("rollout", "step", "step_launches", "step_torch_observe"):
         p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536,
                         batch_size=65536, dtype="bf16x3", seed=1,
                         obs_norm_update="rollout" if mode == "rollout" else "step")
         w = DPPOWorker(p, DistContext(device=dev))
         eng = w.engine
+        if mode != "step":
+            eng._sn_cap = 0          # the per-step launch sequence
         if mode == "step_torch_observe":
             eng._observe_step = lambda norm, obs, shift: norm.observes(obs.to(eng.device, torch.float32))
         w.iteration_step()
