@@ -556,10 +556,6 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     return stg;
   };
 
-#ifdef DPPO_HD_PRIO
-  // static priority for the second-dispatched half (MI355X_MICROARCH.md "Two waves per SIMD" item 4)
-  if (__builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
-#endif
   HD_STAMP(0);
   // Q8: wave 0 DMAs the previous step's sub-slot maxima of the head's two gradient tensors into
   // LDS — the oldest vector-memory ops of the wave (never behind a counted wait), read after many
@@ -1195,18 +1191,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     if (blockIdx.x == 0 && tid < 2 * Q8_SUB) a.q8_clr[(2 * HEAD * Q8_SUB + tid) * Q8_LINE] = 0u;
   }
   // ---------------- per-workgroup partials (deterministic fixed order) ----------------
-#ifdef DPPO_HD_NODRAIN
-  // no DMA may outlive the workgroup's LDS (or overlap its reuse below): wait for the last ring
-  // refill, not for the g1^T stores of the last two dgrad stages issued after it (vector-memory
-  // operations retire in issue order; the stamps / Q8 atomics after them are not counted, so the
-  // wait is at least this long)
-  {
-    constexpr int tiles_last2 = (C::N1R < 4 * C::NS4 ? C::N1R : 4 * C::NS4) - 4 * (C::NS4 - 2);
-    WAIT_VMCNT((tiles_last2 * H::SPS * RB) & 63);
-  }
-#else
   WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
-#endif
   __syncthreads();
   if constexpr (HEAD == 0) {
     // the 8 waves' dW_mu tiles [32][128] through the (now idle) 64 KiB ring in two rounds:

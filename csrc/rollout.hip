@@ -43,7 +43,7 @@ DEV float env_obs(const float* st, int S, int r, int d) {
 // leaving waves that never finish.
 typedef unsigned long long u64;
 constexpr unsigned SN_SPIN_MAX = 1u << 21;   // >= ~1 s of polling per hand-off
-constexpr int SN_MAX_BLOCKS = 1024;          // grid cap of the per-step normalisation launch
+constexpr int SN_MAX_BLOCKS = 256;           // grid cap of the per-step normalisation launch (SN_CHUNKS lanes' worth)
 DEV void sn_put(u64* g, unsigned tag, float v) {
   __hip_atomic_store(g, ((u64)tag << 32) | (u64)__float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -52,78 +52,99 @@ DEV u64 sn_get(const u64* g) {
 }
 DEV float sn_val(u64 x) { return __uint_as_float((unsigned)x); }
 
-// Wave 0 of workgroup `blk`: the step's Chan merge of the features it owns (d = blk, blk + nblk,
-// ...): the fp32 partials of all nblk workgroups summed in fp64 in a fixed order (lane l holds
-// workgroups l, l + 64, ... in that order; then an xor butterfly, which leaves the same bits in
-// every lane), merged into the running (mean, M2) — csrc/obs.hip obs_merge's formulas — and
-// published as the (mean, 1/std) granules.  Then it gathers every feature's new granules into
-// LDS.  Returns false on a timeout.
-DEV bool sn_step(const RolloutArgs& a, int blk, int nblk, int step, int lane, const float* shs, float* nm,
-                 float* ninv) {
+// Waves 0 .. NW-1 of workgroup `blk`: the step's Chan merge of the features it owns (feature
+// blk + nblk * w on wave w): the fp32 partials of all nblk workgroups summed in fp64 in a fixed
+// order (lane l holds workgroups l, l + 64, ... in that order; then an xor butterfly, which leaves
+// the same bits in every lane), merged into the running (mean, M2) — csrc/obs.hip obs_merge's
+// formulas — and published as the (mean, 1/std) granules.  The values of a poll pass whose tags
+// all match are the values (no second read).  Returns false on a timeout.
+constexpr int SN_CHUNKS = 4;                 // workgroups per reducer lane: the grid is <= 256
+DEV bool sn_reduce(const RolloutArgs& a, int d, int nblk, int step, int lane, const float* shs) {
   const int O = a.O;
   const unsigned tag = a.sn_epoch0 + (unsigned)step;
   const u64* g1 = a.sn_g1;
-  unsigned spins = 0;
-  // (two passes per hand-off — poll the tags until all match, then read the values — so no
-  // register array holds a whole sweep: the kernel around this is at its register budget)
-  auto ready1 = [&](int d) {
+  float v1[SN_CHUNKS], v2[SN_CHUNKS];
+  for (unsigned spins = 0;; ++spins) {
     bool ok = true;
-    for (int w = lane; w < nblk; w += 64)
-      ok &= (unsigned)(sn_get(g1 + (size_t)w * 2 * O + d) >> 32) == tag &&
-            (unsigned)(sn_get(g1 + (size_t)w * 2 * O + O + d) >> 32) == tag;
-    return ok;
-  };
-  for (int d = blk; d < O; d += nblk) {
-    while (!__all(ready1(d))) {
-      if (++spins > SN_SPIN_MAX) return false;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    double p1 = 0.0, p2 = 0.0;
-    for (int w = lane; w < nblk; w += 64) {
-      p1 += (double)sn_val(sn_get(g1 + (size_t)w * 2 * O + d));
-      p2 += (double)sn_val(sn_get(g1 + (size_t)w * 2 * O + O + d));
-    }
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      p1 += __shfl_xor(p1, o, 64);
-      p2 += __shfl_xor(p2, o, 64);
+    for (int c = 0; c < SN_CHUNKS; ++c) {
+      const int w = 64 * c + lane;
+      v1[c] = v2[c] = 0.f;
+      if (w < nblk) {
+        const u64 x1 = sn_get(g1 + (size_t)w * 2 * O + d), x2 = sn_get(g1 + (size_t)w * 2 * O + O + d);
+        ok &= (unsigned)(x1 >> 32) == tag && (unsigned)(x2 >> 32) == tag;
+        v1[c] = sn_val(x1);
+        v2[c] = sn_val(x2);
+      }
     }
-    if (lane == 0) {
-      const double count = (double)a.E, n_a = a.sn_n0 + (double)step * count;
-      const double bmean_d = p1 / count;
-      const double bmean = (double)shs[d] + bmean_d;
-      double bm2 = p2 - p1 * bmean_d;
-      if (bm2 < 0.0) bm2 = 0.0;
-      const double n = n_a + count;
-      const double mean0 = a.sn_mean[d];
-      const double delta = bmean - mean0;
-      const double mu = mean0 + delta * (count / n);
-      const double M2 = a.sn_m2[d] + bm2 + delta * delta * (n_a * count / n);
-      double var = M2 / n;
-      if (var < a.sn_var_floor) var = a.sn_var_floor;
-      const float muf = (float)mu, inv = (float)(1.0 / sqrt(var));
-      a.sn_mean[d] = mu;
-      a.sn_m2[d] = M2;
-      a.sn_mean_f32[d] = muf;
-      a.sn_inv_std[d] = inv;
-      sn_put(a.sn_g2 + d, tag, muf);
-      sn_put(a.sn_g2 + O + d, tag, inv);
-    }
+    if (__all(ok)) break;
+    if (spins > SN_SPIN_MAX) return false;
+    if (spins > 8) __builtin_amdgcn_s_sleep(1);
   }
-  // gather every feature's (mean, 1/std) of this step
-  auto ready2 = [&]() {
+  double p1 = 0.0, p2 = 0.0;
+#pragma unroll
+  for (int c = 0; c < SN_CHUNKS; ++c) {
+    p1 += (double)v1[c];
+    p2 += (double)v2[c];
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    p1 += __shfl_xor(p1, o, 64);
+    p2 += __shfl_xor(p2, o, 64);
+  }
+  if (lane == 0) {
+    const double count = (double)a.E, n_a = a.sn_n0 + (double)step * count;
+    const double bmean_d = p1 / count;
+    const double bmean = (double)shs[d] + bmean_d;
+    double bm2 = p2 - p1 * bmean_d;
+    if (bm2 < 0.0) bm2 = 0.0;
+    const double n = n_a + count;
+    const double mean0 = a.sn_mean[d];
+    const double delta = bmean - mean0;
+    const double mu = mean0 + delta * (count / n);
+    const double M2 = a.sn_m2[d] + bm2 + delta * delta * (n_a * count / n);
+    double var = M2 / n;
+    if (var < a.sn_var_floor) var = a.sn_var_floor;
+    const float muf = (float)mu, inv = (float)(1.0 / sqrt(var));
+    a.sn_mean[d] = mu;
+    a.sn_m2[d] = M2;
+    a.sn_mean_f32[d] = muf;
+    a.sn_inv_std[d] = inv;
+    sn_put(a.sn_g2 + d, tag, muf);
+    sn_put(a.sn_g2 + O + d, tag, inv);
+  }
+  return true;
+}
+
+// Wave 0: gather every feature's (mean, 1/std) of this step into LDS (the values of the poll pass
+// whose tags all match; O <= 384 features (Humanoid: 376): 2 O granules in 12 registers per lane)
+constexpr int SN_GATHER = 12;
+DEV bool sn_gather(const RolloutArgs& a, int step, int lane, float* nm, float* ninv) {
+  const int O = a.O;
+  const unsigned tag = a.sn_epoch0 + (unsigned)step;
+  float v[SN_GATHER];
+  for (unsigned spins = 0;; ++spins) {
     bool ok = true;
-    for (int i = lane; i < 2 * O; i += 64) ok &= (unsigned)(sn_get(a.sn_g2 + i) >> 32) == tag;
-    return ok;
-  };
-  while (!__all(ready2())) {
-    if (++spins > SN_SPIN_MAX) return false;
-    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int u = 0; u < SN_GATHER; ++u) {
+      const int i = 64 * u + lane;
+      if (64 * u < 2 * O && i < 2 * O) {
+        const u64 x = sn_get(a.sn_g2 + i);
+        ok &= (unsigned)(x >> 32) == tag;
+        v[u] = sn_val(x);
+      }
+    }
+    if (__all(ok)) break;
+    if (spins > SN_SPIN_MAX) return false;
+    if (spins > 8) __builtin_amdgcn_s_sleep(1);
   }
-  for (int i = lane; i < 2 * O; i += 64) {
-    const float v = sn_val(sn_get(a.sn_g2 + i));
-    if (i < O) nm[i] = v;
-    else ninv[i - O] = v;
+#pragma unroll
+  for (int u = 0; u < SN_GATHER; ++u) {
+    const int i = 64 * u + lane;
+    if (64 * u < 2 * O && i < 2 * O) {
+      if (i < O) nm[i] = v[u];
+      else ninv[i - O] = v[u];
+    }
   }
   return true;
 }
@@ -307,8 +328,8 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
     if constexpr (SN) {
       if (!last) {
         // this step's batch moments about the iteration shift -> the iteration's moments (as in
-        // rollout mode) and this workgroup's granules; wave 0 merges its features and gathers
-        // the new stats of every feature (sn_step); the others wait at the barrier
+        // rollout mode) and this workgroup's granules; its waves merge the features it owns
+        // (sn_reduce), wave 0 gathers the new stats of every feature (sn_gather)
         const unsigned tag = a.sn_epoch0 + (unsigned)step;
         auto moments = [&](auto kind_tag) {
           constexpr int KIND = decltype(kind_tag)::value;
@@ -331,14 +352,18 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
         };
         if (a.kind == 1) moments(std::integral_constant<int, 1>{});
         else moments(std::integral_constant<int, 0>{});
-        if (wave == 0 && !sn_step(a, (int)blockIdx.x, (int)gridDim.x, step, lane, shs, nm, ninv)) {
-          if (lane == 0) {
-            *sn_fail = 1;
-            __hip_atomic_store(a.sn_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
+        // features blk + nblk * (w + NW j) on wave w: the features of this workgroup are merged
+        // by its waves concurrently
+        bool okr = true;
+        for (int dfeat = (int)blockIdx.x + (int)gridDim.x * wave; okr && dfeat < O; dfeat += (int)gridDim.x * NW)
+          okr = sn_reduce(a, dfeat, (int)gridDim.x, step, lane, shs);
+        if (!okr && lane == 0) *sn_fail = 1;
+        if (wave == 0 && !sn_gather(a, step, lane, nm, ninv) && lane == 0) *sn_fail = 1;
         __syncthreads();
-        if (*sn_fail) return;   // a peer never published: give up (the host raises)
+        if (*sn_fail) {   // a peer never published: give up (the host raises)
+          if (tid == 0) __hip_atomic_store(a.sn_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return;
+        }
       }
     }
     if (a.kind == 1) observe(std::integral_constant<int, 1>{});
@@ -614,7 +639,7 @@ void launch_nw(const RolloutArgs& a, hipStream_t s) {
     return;
   }
   const int cap = ncu * (per_cu > 1 ? per_cu - 1 : per_cu);
-  if (nblk > cap || nblk > SN_MAX_BLOCKS) {
+  if (nblk > cap || nblk > SN_MAX_BLOCKS || a.O > 64 * SN_GATHER / 2) {
     dppo_note_error(hipErrorCooperativeLaunchTooLarge, __FILE__, __LINE__);
     return;
   }
@@ -636,6 +661,7 @@ int stepnorm_cap(const RolloutArgs& a) {
       hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
+  if (a.O > 64 * SN_GATHER / 2) return 0;   // the gather holds 2 O granules in registers
   const int cap = ncu * (per_cu > 1 ? per_cu - 1 : per_cu);
   return cap < SN_MAX_BLOCKS ? cap : SN_MAX_BLOCKS;
 }

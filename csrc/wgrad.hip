@@ -85,9 +85,6 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   // oldest vector-memory op: it never holds up a counted wait), folded in the epilogue
   uint32_t q8v = 0;
   if constexpr (DT == DT_FP8) q8v = a.q8_rd[(a.q8_t[tk.layer] * Q8_SUB + lane) * Q8_LINE];
-#ifdef DPPO_WG_PRIO
-  if (wave >= WG_WAVES / 2) __builtin_amdgcn_s_setprio(1);   // (MI355X_MICROARCH.md two-waves item 4)
-#endif
   const bool active = wave < tk.nq * tk.kq;
   const int wn = wave / tk.kq, wk = wave - (wave / tk.kq) * tk.kq;
   f32x4 acc[4][4];
