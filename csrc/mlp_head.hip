@@ -43,6 +43,9 @@ constexpr int ROWS = 128;                   // rows per workgroup (both heads)
 constexpr int NSLOT = 16;                   // fragments per ring stage
 constexpr int SST = 36, TILE_F = 16 * SST;  // [16][SST] fp32 transpose tile (conflict-free)
 constexpr int MAX_STEPS = 64;
+#ifndef HD_G1
+#define HD_G1 4   // value fc1: fragments per LDS read group (A/B: -DHD_G1=2 / 8)
+#endif
 
 typedef __attribute__((ext_vector_type(8))) float f32x8;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4h;
@@ -301,8 +304,13 @@ DEV void static_for(F&& f) {
 
 // Fragments q in [Q0, Q1) of a stage with bit q of MASK set, read in groups of G: group g + 1's
 // LDS reads are in flight while group g's MFMAs run.  f(integral_constant<q>, fragment).
-template <int DT, unsigned MASK, int Q0, int Q1, int G, typename F>
-DEV void for_slots(const char* stg, int lane, F&& f) {
+struct NoHook {
+  DEV void operator()() const {}
+};
+// (pre(): called once the first group's LDS reads are issued — the stage's ring refill goes there,
+// so its issue cost overlaps their latency instead of delaying them)
+template <int DT, unsigned MASK, int Q0, int Q1, int G, typename F, typename PRE = NoHook>
+DEV void for_slots(const char* stg, int lane, F&& f, PRE&& pre = PRE{}) {
   using H = HT<DT>;
   constexpr int NG = (Q1 - Q0 + G - 1) / G;
   typename H::Frag b[2][G];
@@ -316,10 +324,13 @@ DEV void for_slots(const char* stg, int lane, F&& f) {
     });
   };
   rd(std::integral_constant<int, 0>{});
+  pre();
   static_for<0, NG>([&](auto gc) __attribute__((always_inline)) {
     constexpr int g = decltype(gc)::value;
     if constexpr (g + 1 < NG) rd(std::integral_constant<int, g + 1>{});
+#ifndef DPPO_HD_NOSCHED
     __builtin_amdgcn_sched_barrier(0);
+#endif
     static_for<0, G>([&](auto ic) __attribute__((always_inline)) {
       constexpr int q = Q0 + g * G + decltype(ic)::value;
       if constexpr (q < Q1 && ((MASK >> q) & 1u)) f(std::integral_constant<int, q>{}, b[g & 1][decltype(ic)::value]);
@@ -334,8 +345,8 @@ DEV void for_slots(const char* stg, int lane, F&& f) {
 // NM times, so the VALU issues in the MFMAs' shadow instead of after them (at one wave per SIMD
 // an in-order wave otherwise runs the MFMA block and the VALU block back to back).  v() must not
 // contain inline asm (a scheduling boundary).
-template <int DT, unsigned MASK, int Q0, int Q1, int NM, int VPM, typename F, typename V>
-DEV void mma_mix(const char* stg, int lane, F&& f, V&& v) {
+template <int DT, unsigned MASK, int Q0, int Q1, int NM, int VPM, typename F, typename V, typename PRE = NoHook>
+DEV void mma_mix(const char* stg, int lane, F&& f, V&& v, PRE&& pre = PRE{}) {
   using H = HT<DT>;
   constexpr int N = Q1 - Q0;
   typename H::Frag b[N];
@@ -344,6 +355,7 @@ DEV void mma_mix(const char* stg, int lane, F&& f, V&& v) {
     constexpr int q = Q0 + decltype(ic)::value;
     if constexpr ((MASK >> q) & 1u) b[decltype(ic)::value] = H::lds(base + q * H::FB);
   });
+  pre();
   __builtin_amdgcn_sched_barrier(0);
   static_for<0, N>([&](auto ic) __attribute__((always_inline)) {
     constexpr int q = Q0 + decltype(ic)::value;
@@ -405,6 +417,8 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   const int A = a.A;
   const int ks1 = a.d_in[0] >> 5;
   const int ns1 = fc1_stages<HEAD, F8>(ks1);
+  // stream steps of this kernel (step_src's s_end)
+  const int n_steps = ns1 + C::K2 / 2 + 1 + (FWD ? 0 : 1 + C::NS4);
   char* ring = smem;
   float* scr = reinterpret_cast<float*>(smem + (size_t)S * SB) + wave * WS_F;
   char* xring = reinterpret_cast<char*>(scr);
@@ -477,6 +491,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   __amdgpu_buffer_rsrc_t rw8 = rw;
   if constexpr (F8) rw8 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W8), (short)0, 0x7fffffff, 0x00020000);
   auto issue = [&](int st, int stage) __attribute__((always_inline)) {
+#ifdef DPPO_HD_NOTAIL
+    if (st >= n_steps) return;   // past the end: nothing to refill (the waits count what was issued)
+#endif
 #ifdef DPPO_ABL_NOWDMA
     // ABLATION (timing only, wrong numerics): the ring keeps its primed fragments
     if (st >= S - 1) return;
@@ -537,7 +554,23 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   int hist[NH];
 #pragma unroll
   for (int i = 0; i < NH; ++i) hist[i] = 0;
+#ifdef DPPO_HD_LATE_ISSUE
+  // the stage's refill is issued by the stage's first for_slots / mma_mix after its first LDS
+  // reads (flush); a stage that has not issued it by its end issues it before the next wait
+  int pend_st = -1, pend_stage = 0;
+  auto flush = [&]() __attribute__((always_inline)) {
+    if (pend_st >= 0) {
+      issue(pend_st, pend_stage);
+      pend_st = -1;
+    }
+  };
+#else
+  auto flush = NoHook{};
+#endif
   auto wait_step = [&](int younger) __attribute__((always_inline)) -> const char* {
+#ifdef DPPO_HD_LATE_ISSUE
+    flush();
+#endif
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = NH - 1; i > 0; --i) hist[i] = hist[i - 1];
@@ -545,12 +578,26 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     int extra = 0;
 #pragma unroll
     for (int i = 0; i < NH; ++i) extra += hist[i];
+#ifdef DPPO_HD_NOTAIL
+    // no refill is issued past the stream's end: the batches younger than this step's are the
+    // min(S - 2, n_steps - 1 - cur) refills actually issued after it
+    {
+      const int nb = min(S - 2, n_steps - 1 - cur);
+      wait_vm<0>(GL * (nb > 0 ? nb : 0) + extra);
+    }
+#else
     wait_vm<GL * (S - 2)>(extra);
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const char* stg = ring + cst * SB;
+#ifdef DPPO_HD_LATE_ISSUE
+    pend_st = cur + S - 1;
+    pend_stage = cst == 0 ? S - 1 : cst - 1;
+#else
     issue(cur + S - 1, cst == 0 ? S - 1 : cst - 1);
+#endif
     cst = cst + 1 == S ? 0 : cst + 1;
     ++cur;
     return stg;
@@ -645,6 +692,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       static_for<0, 2>([&](auto sc) __attribute__((always_inline)) {
         constexpr int sub = decltype(sc)::value;
         stg = wait_step(sub == 1 ? 2 * XDMA : 0);
+        flush();
         if constexpr (sub == 0) {
           xq0 = to_f8(read_x(2 * j, 0));
           xq1 = to_f8(read_x(2 * j + 1, 0));
@@ -676,11 +724,11 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb) xa[rb] = read_x(ks, rb);
         }
-        for_slots<DT, 0xffffu, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+        for_slots<DT, 0xffffu, 0, 16, HD_G1>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
             constexpr int t = 16 * sub + decltype(qc)::value;
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) acc1[rb][t] = P::mma(acc1[rb][t], xa[rb], b);
-          });
+          }, flush);
         if constexpr (sub == 0) issue_x(ks + XS);   // into the slot X[ks] just left
       });
       if (ks == 1) HD_STAMP(8);
@@ -708,7 +756,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
             for (int rb = 0; rb < RB; ++rb) acc1[rb][q - 8] = P::mma(acc1[rb][q - 8], xb[rb], b);
           }
         }
-      });
+      }, flush);
       if (want_xT) {
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
@@ -781,7 +829,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       constexpr int t = decltype(qc)::value;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a0[rb], b);
-    }, [&]() __attribute__((always_inline)) { prep_a(std::integral_constant<int, 2 * j + 1>{}); });
+    }, [&]() __attribute__((always_inline)) { prep_a(std::integral_constant<int, 2 * j + 1>{}); }, flush);
     prep_b(a1);
     nst = NSTA;
     if constexpr (2 * j + 2 < C::K2) {
@@ -789,7 +837,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a1[rb], b);
-      }, [&]() __attribute__((always_inline)) { prep_a(std::integral_constant<int, 2 * j + 2>{}); });
+      }, [&]() __attribute__((always_inline)) { prep_a(std::integral_constant<int, 2 * j + 2>{}); }, flush);
       prep_b(a0);
       nst += NSTA;
     } else {
@@ -797,7 +845,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a1[rb], b);
-      });
+      }, flush);
       // h2 = tanh(fc2), kept in registers for fc3, dgrad fc3 and the fused narrow-layer wgrad
 #pragma unroll
       for (int t = 0; t < 8; ++t)
@@ -831,7 +879,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       constexpr int t = decltype(qc)::value >> 2;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) a3[rb][t] = P::mma(a3[rb][t], am[rb], b);
-    });
+    }, flush);
   });
   if constexpr (FWD) {
     // V of the wave's rows: column 0 of the fc3 tile (lanes lr == 0 hold rows 4 lg .. 4 lg + 3)
@@ -844,7 +892,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
           if (m < a.M) a.v_out[m] = a3[rb][0][i];
         }
     }
+#ifndef DPPO_HD_NOTAIL
     WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
+#endif
     return;
   } else {
   // (the transpose tiles hold mu / v from here: every wave's own)
@@ -1053,7 +1103,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) d2[rb][t] = P::mma(d2[rb][t], ad[rb], b);
-  });
+  }, flush);
   nst = 0;
   // Q8: this step's store scales of the head's two gradient tensors (g1: 2 HEAD, g2: 2 HEAD + 1)
   // from the previous step's maxima (scalar loads); the running |g| maxima of this wave
@@ -1120,7 +1170,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       constexpr int q = decltype(qc)::value;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) g[q >> 2][rb] = P::mma(g[q >> 2][rb], a2[q & 3][rb], b);
-    });
+    }, flush);
     if constexpr (s > 0) nst = epi(std::integral_constant<int, s - 1>{});
     else nst = 0;
 #pragma unroll
@@ -1191,7 +1241,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     if (blockIdx.x == 0 && tid < 2 * Q8_SUB) a.q8_clr[(2 * HEAD * Q8_SUB + tid) * Q8_LINE] = 0u;
   }
   // ---------------- per-workgroup partials (deterministic fixed order) ----------------
+#ifndef DPPO_HD_NOTAIL
   WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
+#endif
   __syncthreads();
   if constexpr (HEAD == 0) {
     // the 8 waves' dW_mu tiles [32][128] through the (now idle) 64 KiB ring in two rounds:

@@ -97,7 +97,11 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   for (int k = 0; k < nk; ++k) {
     WAIT_VMCNT(C * NI * (S - 2));             // this wave's part of stage k has landed
     __builtin_amdgcn_s_barrier();              // ... everyone's; and stage k-1 is no longer read
+#ifndef DPPO_WG_LATE_ISSUE
     issue(k + S - 1);                          // refill the slot stage k-1 used
+#else
+    if (!active) issue(k + S - 1);
+#endif
     if (active) {
       const char* st = smem + (k % S) * SB;
       Frag af[4], bf[4];
@@ -119,6 +123,9 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
           a8[i] = rd(wn * 4 + i);
           b8[i] = rd(NF + wk * 4 + i);
         }
+#ifdef DPPO_WG_LATE_ISSUE
+        issue(k + S - 1);
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -139,6 +146,9 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
         af[i] = lds_frag(wn * 4 + i);
         bf[i] = lds_frag(NF + wk * 4 + i);
       }
+#ifdef DPPO_WG_LATE_ISSUE
+      issue(k + S - 1);   // (after the fragment reads: its issue cost overlaps their latency)
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
