@@ -328,9 +328,7 @@ DEV void for_slots(const char* stg, int lane, F&& f, PRE&& pre = PRE{}) {
   static_for<0, NG>([&](auto gc) __attribute__((always_inline)) {
     constexpr int g = decltype(gc)::value;
     if constexpr (g + 1 < NG) rd(std::integral_constant<int, g + 1>{});
-#ifndef DPPO_HD_NOSCHED
     __builtin_amdgcn_sched_barrier(0);
-#endif
     static_for<0, G>([&](auto ic) __attribute__((always_inline)) {
       constexpr int q = Q0 + g * G + decltype(ic)::value;
       if constexpr (q < Q1 && ((MASK >> q) & 1u)) f(std::integral_constant<int, q>{}, b[g & 1][decltype(ic)::value]);
@@ -417,8 +415,6 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   const int A = a.A;
   const int ks1 = a.d_in[0] >> 5;
   const int ns1 = fc1_stages<HEAD, F8>(ks1);
-  // stream steps of this kernel (step_src's s_end)
-  const int n_steps = ns1 + C::K2 / 2 + 1 + (FWD ? 0 : 1 + C::NS4);
   char* ring = smem;
   float* scr = reinterpret_cast<float*>(smem + (size_t)S * SB) + wave * WS_F;
   char* xring = reinterpret_cast<char*>(scr);
@@ -491,9 +487,6 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   __amdgpu_buffer_rsrc_t rw8 = rw;
   if constexpr (F8) rw8 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W8), (short)0, 0x7fffffff, 0x00020000);
   auto issue = [&](int st, int stage) __attribute__((always_inline)) {
-#ifdef DPPO_HD_NOTAIL
-    if (st >= n_steps) return;   // past the end: nothing to refill (the waits count what was issued)
-#endif
 #ifdef DPPO_ABL_NOWDMA
     // ABLATION (timing only, wrong numerics): the ring keeps its primed fragments
     if (st >= S - 1) return;
@@ -554,23 +547,8 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   int hist[NH];
 #pragma unroll
   for (int i = 0; i < NH; ++i) hist[i] = 0;
-#ifdef DPPO_HD_LATE_ISSUE
-  // the stage's refill is issued by the stage's first for_slots / mma_mix after its first LDS
-  // reads (flush); a stage that has not issued it by its end issues it before the next wait
-  int pend_st = -1, pend_stage = 0;
-  auto flush = [&]() __attribute__((always_inline)) {
-    if (pend_st >= 0) {
-      issue(pend_st, pend_stage);
-      pend_st = -1;
-    }
-  };
-#else
-  auto flush = NoHook{};
-#endif
+  auto flush = NoHook{};   // (A/B in round 4: the refill issued after the first fragment reads: no gain)
   auto wait_step = [&](int younger) __attribute__((always_inline)) -> const char* {
-#ifdef DPPO_HD_LATE_ISSUE
-    flush();
-#endif
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = NH - 1; i > 0; --i) hist[i] = hist[i - 1];
@@ -578,26 +556,12 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     int extra = 0;
 #pragma unroll
     for (int i = 0; i < NH; ++i) extra += hist[i];
-#ifdef DPPO_HD_NOTAIL
-    // no refill is issued past the stream's end: the batches younger than this step's are the
-    // min(S - 2, n_steps - 1 - cur) refills actually issued after it
-    {
-      const int nb = min(S - 2, n_steps - 1 - cur);
-      wait_vm<0>(GL * (nb > 0 ? nb : 0) + extra);
-    }
-#else
     wait_vm<GL * (S - 2)>(extra);
-#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const char* stg = ring + cst * SB;
-#ifdef DPPO_HD_LATE_ISSUE
-    pend_st = cur + S - 1;
-    pend_stage = cst == 0 ? S - 1 : cst - 1;
-#else
     issue(cur + S - 1, cst == 0 ? S - 1 : cst - 1);
-#endif
     cst = cst + 1 == S ? 0 : cst + 1;
     ++cur;
     return stg;
@@ -892,9 +856,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
           if (m < a.M) a.v_out[m] = a3[rb][0][i];
         }
     }
-#ifndef DPPO_HD_NOTAIL
     WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
-#endif
     return;
   } else {
   // (the transpose tiles hold mu / v from here: every wave's own)
@@ -1241,9 +1203,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     if (blockIdx.x == 0 && tid < 2 * Q8_SUB) a.q8_clr[(2 * HEAD * Q8_SUB + tid) * Q8_LINE] = 0u;
   }
   // ---------------- per-workgroup partials (deterministic fixed order) ----------------
-#ifndef DPPO_HD_NOTAIL
   WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
-#endif
   __syncthreads();
   if constexpr (HEAD == 0) {
     // the 8 waves' dW_mu tiles [32][128] through the (now idle) 64 KiB ring in two rounds:

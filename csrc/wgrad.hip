@@ -97,11 +97,11 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   for (int k = 0; k < nk; ++k) {
     WAIT_VMCNT(C * NI * (S - 2));             // this wave's part of stage k has landed
     __builtin_amdgcn_s_barrier();              // ... everyone's; and stage k-1 is no longer read
-#ifndef DPPO_WG_LATE_ISSUE
-    issue(k + S - 1);                          // refill the slot stage k-1 used
-#else
-    if (!active) issue(k + S - 1);
-#endif
+    // refill the slot stage k-1 used: split-bf16 / bf16 after this step's fragment reads (the DMA
+    // issue cost then overlaps their latency: 4.16 vs 4.22 ms per bf16x3 iteration, 2.30 vs 2.32
+    // bf16, same box); e4m3 right here (2.01 vs 1.99 the other way; profiles/r4/ab_late_issue_*.json)
+    constexpr bool LATE = DT != DT_FP8;
+    if (!LATE || !active) issue(k + S - 1);
     if (active) {
       const char* st = smem + (k % S) * SB;
       Frag af[4], bf[4];
@@ -123,9 +123,7 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
           a8[i] = rd(wn * 4 + i);
           b8[i] = rd(NF + wk * 4 + i);
         }
-#ifdef DPPO_WG_LATE_ISSUE
-        issue(k + S - 1);
-#endif
+
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -146,9 +144,7 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
         af[i] = lds_frag(wn * 4 + i);
         bf[i] = lds_frag(NF + wk * 4 + i);
       }
-#ifdef DPPO_WG_LATE_ISSUE
-      issue(k + S - 1);   // (after the fragment reads: its issue cost overlaps their latency)
-#endif
+      if constexpr (LATE) issue(k + S - 1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
