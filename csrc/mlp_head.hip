@@ -238,6 +238,16 @@ DEV int step_src(const MlpArgs& a, int st, int q, int rot, int ks1) {
   return a.off_wt[C::L2] + (int)fm_frag(t, ks, a.d_out[C::L2], 0);
 }
 
+// the head kernels' fragment product (ABLATION DPPO_ABL_MFMA1, timing only: split-bf16 products
+// as ONE MFMA, hi x hi — the operands are still read, a third of the matrix work is issued)
+template <int DT>
+DEV f32x4 hmma(f32x4 c, const typename HT<DT>::Frag& a, const typename HT<DT>::Frag& b) {
+#ifdef DPPO_ABL_MFMA1
+  if constexpr (DT == DT_S3) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
+#endif
+  return HT<DT>::P::mma(c, a, b);
+}
+
 // C-layout tiles of features c0..c0+15 (v0) and c0+16..c0+31 (v1) -> [16][SST] fp32
 DEV void tp_put(float* tp, const f32x4& v0, const f32x4& v1, int lane) {
   const int lr = lane & 15, lg = lane >> 4;
@@ -558,7 +568,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     for (int i = 0; i < NH; ++i) extra += hist[i];
     wait_vm<GL * (S - 2)>(extra);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef DPPO_ABL_NOBAR
     __builtin_amdgcn_s_barrier();
+#endif
     asm volatile("" ::: "memory");
     const char* stg = ring + cst * SB;
     issue(cur + S - 1, cst == 0 ? S - 1 : cst - 1);
@@ -691,7 +703,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         for_slots<DT, 0xffffu, 0, 16, HD_G1>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
             constexpr int t = 16 * sub + decltype(qc)::value;
 #pragma unroll
-            for (int rb = 0; rb < RB; ++rb) acc1[rb][t] = P::mma(acc1[rb][t], xa[rb], b);
+            for (int rb = 0; rb < RB; ++rb) acc1[rb][t] = hmma<DT>(acc1[rb][t], xa[rb], b);
           }, flush);
         if constexpr (sub == 0) issue_x(ks + XS);   // into the slot X[ks] just left
       });
@@ -713,11 +725,11 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         constexpr int q = decltype(qc)::value;
         if constexpr (q < 8) {
 #pragma unroll
-          for (int rb = 0; rb < RB; ++rb) acc1[rb][q] = P::mma(acc1[rb][q], xa[rb], b);
+          for (int rb = 0; rb < RB; ++rb) acc1[rb][q] = hmma<DT>(acc1[rb][q], xa[rb], b);
         } else {
           if (two) {
 #pragma unroll
-            for (int rb = 0; rb < RB; ++rb) acc1[rb][q - 8] = P::mma(acc1[rb][q - 8], xb[rb], b);
+            for (int rb = 0; rb < RB; ++rb) acc1[rb][q - 8] = hmma<DT>(acc1[rb][q - 8], xb[rb], b);
           }
         }
       }, flush);
@@ -792,7 +804,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     mma_mix<DT, 0x7fu, 0, 8, 7 * RB * MPP, 3>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int t = decltype(qc)::value;
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a0[rb], b);
+      for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = hmma<DT>(acc2[rb][t], a0[rb], b);
     }, [&]() __attribute__((always_inline)) { prep_a(std::integral_constant<int, 2 * j + 1>{}); }, flush);
     prep_b(a1);
     nst = NSTA;
@@ -800,7 +812,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       mma_mix<DT, 0x7f00u, 8, 16, 7 * RB * MPP, 3>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
         constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a1[rb], b);
+        for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = hmma<DT>(acc2[rb][t], a1[rb], b);
       }, [&]() __attribute__((always_inline)) { prep_a(std::integral_constant<int, 2 * j + 2>{}); }, flush);
       prep_b(a0);
       nst += NSTA;
@@ -808,7 +820,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       for_slots<DT, 0x7f00u, 8, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
         constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = P::mma(acc2[rb][t], a1[rb], b);
+        for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = hmma<DT>(acc2[rb][t], a1[rb], b);
       }, flush);
       // h2 = tanh(fc2), kept in registers for fc3, dgrad fc3 and the fused narrow-layer wgrad
 #pragma unroll
@@ -842,7 +854,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     for_slots<DT, M3, 0, 8, 8>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int t = decltype(qc)::value >> 2;
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) a3[rb][t] = P::mma(a3[rb][t], am[rb], b);
+      for (int rb = 0; rb < RB; ++rb) a3[rb][t] = hmma<DT>(a3[rb][t], am[rb], b);
     }, flush);
   });
   if constexpr (FWD) {
@@ -1064,7 +1076,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   for_slots<DT, 0x7f00u, 8, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
     constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) d2[rb][t] = P::mma(d2[rb][t], ad[rb], b);
+    for (int rb = 0; rb < RB; ++rb) d2[rb][t] = hmma<DT>(d2[rb][t], ad[rb], b);
   }, flush);
   nst = 0;
   // Q8: this step's store scales of the head's two gradient tensors (g1: 2 HEAD, g2: 2 HEAD + 1)
@@ -1131,7 +1143,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     for_slots<DT, M4, 0, 16, G4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) g[q >> 2][rb] = P::mma(g[q >> 2][rb], a2[q & 3][rb], b);
+      for (int rb = 0; rb < RB; ++rb) g[q >> 2][rb] = hmma<DT>(g[q >> 2][rb], a2[q & 3][rb], b);
     }, flush);
     if constexpr (s > 0) nst = epi(std::integral_constant<int, s - 1>{});
     else nst = 0;
@@ -1183,7 +1195,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         if (lg >= 2) x0 = x1 = float4{0.f, 0.f, 0.f, 0.f};
         const Frag bh = H::from8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
 #pragma unroll
-        for (int m = 0; m < 2; ++m) dwm[m][4 * hh + tt] = P::mma(dwm[m][4 * hh + tt], am2[m], bh);
+        for (int m = 0; m < 2; ++m) dwm[m][4 * hh + tt] = hmma<DT>(dwm[m][4 * hh + tt], am2[m], bh);
       }
     });
   }

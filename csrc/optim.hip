@@ -428,9 +428,20 @@ __global__ __launch_bounds__(256) void pack_fp8_kernel(const float* __restrict__
                                                         int npart, float* __restrict__ qscale) {
   using P = Prec<DT_FP8>;
   __shared__ float sc[6];
+  __shared__ float red[6][32];
+  // fold the npart x 6 block maxima: 32 lanes per layer stride the blocks (independent loads in
+  // flight), then one lane per layer folds its 32 (max: order-independent)
+  if (threadIdx.x < 6 * 32) {
+    const int l = threadIdx.x >> 5, k = threadIdx.x & 31;
+    float v = 0.f;
+    for (int b = k; b < npart; b += 32) v = fmaxf(v, part[b * 6 + l]);
+    red[l][k] = v;
+  }
+  __syncthreads();
   if (threadIdx.x < 6) {
     float v = 0.f;
-    for (int b = 0; b < npart; ++b) v = fmaxf(v, part[b * 6 + threadIdx.x]);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v = fmaxf(v, red[threadIdx.x][k]);
     sc[threadIdx.x] = fmaxf(__fdiv_rn(v, 416.f), 1e-12f);
     if (blockIdx.x == 0) qscale[threadIdx.x] = sc[threadIdx.x];
   }
