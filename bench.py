@@ -130,6 +130,8 @@ def main():
     ap.add_argument("--dist-timeout-s", type=float, default=300.0,
                     help="bound of every wait on peers (collective watchdog; abort + non-zero exit)")
     ap.add_argument("--heartbeat-timeout-s", type=float, default=60.0)
+    ap.add_argument("--wgrad-gather", default="auto", choices=["auto", "fused", "separate"],
+                    help="the split-K slab reduction + Adam in the wgrad launch's tail (fused) or a launch after it")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -159,7 +161,7 @@ def main():
                         batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=dtype,
                         num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
                         dist_backend=args.dist_backend, grad_comm=args.grad_comm,
-                        dist_timeout_s=args.dist_timeout_s,
+                        dist_timeout_s=args.dist_timeout_s, wgrad_gather=args.wgrad_gather,
                         phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
         w = DPPOWorker(p, ctx)
         m = {}
@@ -199,6 +201,7 @@ def main():
     total_steps = rows * ctx.world_size * args.steps
     value = total_steps / elapsed
     heads = bool(getattr(w.engine, "heads", False))
+    wgrad_gather = "fused" if getattr(w.engine, "wgrad_fused", False) else "separate"
     # the gradient all-reduce in use: native RCCL on the compute stream (csrc/comm.cpp), the gloo
     # adapter of the same in-stream engine branch, the process group's (per-head chains), or none
     # (world size 1, not forced)
@@ -228,7 +231,7 @@ def main():
                                               and ctx.backend == "nccl" else 0),
                           "rollout_len": T, "num_epoch": args.num_epoch,
                           "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout,
-                          "per_head_kernels": heads, "grad_allreduce": grad_ar,
+                          "per_head_kernels": heads, "grad_allreduce": grad_ar, "wgrad_gather": wgrad_gather,
                           # --overlap-rollout on the in-stream path: the last value-head all-reduce +
                           # Adam run on a side stream (second communicator) beside the next rollout
                           "overlap_value_step": ("side_stream" if args.overlap_rollout and ctx.native_side is not None

@@ -320,7 +320,7 @@ __device__ __forceinline__ bool item_reduce(const float* __restrict__ part, int 
   const int tid = threadIdx.x, c = tid % ITEM_IPB, rg = tid / ITEM_IPB;
   j = ITEM_IPB * b + c;
   float s = 0.f;
-  if (j < nitems) {
+  if (j < nitems && tid < 256) {   // (a 512-thread block: threads 256+ add zeros; red holds blockDim floats)
     const float* p = part + red_col[j];
     for (int r0 = rg; r0 < nprow; r0 += 16 * RG) {
       float x[16];

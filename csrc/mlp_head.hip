@@ -857,6 +857,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       for (int rb = 0; rb < RB; ++rb) a3[rb][t] = hmma<DT>(a3[rb][t], am[rb], b);
     }, flush);
   });
+  HD_STAMP(12);
   if constexpr (FWD) {
     // V of the wave's rows: column 0 of the fc3 tile (lanes lr == 0 hold rows 4 lg .. 4 lg + 3)
     if (lr == 0) {
@@ -1200,6 +1201,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     });
   }
 
+  HD_STAMP(10);
   if constexpr (Q8) {
     // this step's gradient maxima (max is order-independent: the atomics keep it deterministic)
 #pragma unroll
@@ -1216,6 +1218,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   }
   // ---------------- per-workgroup partials (deterministic fixed order) ----------------
   WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
+  HD_STAMP(11);
   __syncthreads();
   if constexpr (HEAD == 0) {
     // the 8 waves' dW_mu tiles [32][128] through the (now idle) 64 KiB ring in two rounds:

@@ -1,6 +1,7 @@
 // GAE scan and fused Adam + global-norm clip + weight-image refresh (K12, K16).
 #include <stdio.h>
 
+#include "adam_core.h"
 #include "kernels.h"
 #include "mlp_core.h"
 
@@ -160,27 +161,6 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
   }
 }
 
-// One Adam element update, shared by both Adam kernels so that they round identically (explicit
-// fmaf: no contraction choice is left to the compiler).  Returns the new parameter.
-DEV float adam_elem(float& m, float& v, float p, float gi, float b1, float b2, float step_size, float rbc2,
-                    float eps) {
-  const float mi = fmaf(b1, m, (1.f - b1) * gi);
-  const float vi = fmaf(b2, v, (1.f - b2) * (gi * gi));
-  m = mi;
-  v = vi;
-  return p - step_size * mi / fmaf(sqrtf(vi), rbc2, eps);
-}
-
-// fp8 mode: the e4m3 image the update's fc1 reads, refreshed with every Adam step (scale: the
-// iteration's per-layer qscale, as pack_fp8_kernel; e4m3 conversion saturates)
-DEV void f8_put(const F8Shadow& f8, int i, int wi, int wti, float pi) {
-  if (f8.img != nullptr) {
-    const uint8_t q = Prec<DT_FP8>::cvt(__fdiv_rn(pi, f8.qs[f8.lid[i]]));
-    f8.img[wi] = q;
-    if (wti >= 0) f8.img[wti] = q;
-  }
-}
-
 template <int DT>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int n, float lr,
@@ -309,17 +289,7 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
   // the optimizer-state loads are issued before the gradient is formed (they do not depend on
   // it), so their latency overlaps the slab loads'
   auto update = [&](int i, float gi, float mi, float vi, float pv, int wi, int wti) {
-    g[i] = gi;
-    const float pi = adam_elem(mi, vi, pv, gi, b1, b2, step_size, rbc2, eps);
-    m[i] = mi;
-    v[i] = vi;
-    p[i] = pi;
-    if (wi >= 0) {   // (wti -1: no transposed image, the first layer of a head)
-      const float q = qmul ? pi * qmul[i] : pi;
-      P::put(wimg, wi, q);
-      if (wti >= 0) P::put(wimg, wti, q);
-      f8_put(f8, i, wi, wti, pi);
-    }
+    adam_apply<DT>(i, gi, mi, vi, pv, wi, wti, g, p, m, v, b1, b2, step_size, rbc2, eps, wimg, qmul, f8);
   };
   if ((int)blockIdx.x < nrb) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {

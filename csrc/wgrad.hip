@@ -11,6 +11,7 @@
 // 384 rows per step for 2x the outputs of a 128x128 tile's 256 (v_fc1: 2304 instead of 3072
 // rows per step).  Results go to per-chunk fp32 slabs ([nq*64][kq*64] per task) that
 // grad_gather sums in a fixed order — deterministic, no float atomics (SURVEY §7.4 part 2).
+#include "adam_core.h"
 #include "kernels.h"
 #include "mlp_core.h"
 
@@ -172,12 +173,155 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
       for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * KE + col + 16 * j] = acc[i][j][q];
 }
 
-template <int DT, int S>
+// ---- the fused split-K reduction (WgradFix, a.fx.mode != 0) ----
+// A stream-K style fix-up in the launch's tail instead of a grad_gather / gather_adam launch after
+// it: the task publishes its chunk (release: the XCD's L2 written back, then an agent-scope
+// arrival count on its tile), reduces grad_gather's reduce items if it has some (tasks [0, nrb)),
+// waits for the tile's other chunks, and reduces its share of the tile's elements over all nch
+// chunks in grad_gather's order (slab_sum) — the same sums, so the same bits; no float atomics.
+// The chunks of other workgroups are read with agent-scope loads (coherent across the XCDs' L2s).
+// Every wait is bounded: a timeout sets fx.err and skips the share (the host raises).
+constexpr unsigned FIX_SPIN_MAX = 1u << 22;
+
+DEV float ld_agent(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// slab_sum (csrc/common.h) with agent-scope loads: the same adds in the same order
+DEV float slab_sum_agent(const float* p, int nch, size_t st) {
+  float s = 0.f;
+  for (int c0 = 0; c0 < nch; c0 += 16) {
+    float x[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[c] = (c0 + c < nch) ? ld_agent(p + (size_t)(c0 + c) * st) : 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (c0 + c < nch) s += x[c];
+  }
+  return s;
+}
+
+template <int IDT>
+DEV void wgrad_fixup(const WgradArgs& a, char* smem) {
+  using PI = Prec<IDT>;
+  constexpr int NT = WG_WAVES * 64;
+  const WgradFix& f = a.fx;
+  const int tid = threadIdx.x;
+  const int* ft = f.ftask + 4 * blockIdx.x;
+  const int tile = ft[0], nch = ft[1], e_lo = ft[2], e_hi = ft[3];
+  float* red = reinterpret_cast<float*>(smem);          // [NT] (the ring is free: every DMA has landed)
+  int* okf = reinterpret_cast<int*>(smem + NT * sizeof(float));
+  typename PI::T* wimg = reinterpret_cast<typename PI::T*>(f.wimg);
+  const bool adam = f.mode == 2;
+  const float bc1 = 1.f - powf(f.b1, f.step);
+  const float bc2 = 1.f - powf(f.b2, f.step);
+  const float step_size = f.lr / bc1;
+  const float rbc2 = 1.f / sqrtf(bc2);
+  WAIT_VMCNT(0);      // this wave's slab stores are done
+  __syncthreads();    // ... every wave's, and every LDS read of the ring
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the chunk leaves this XCD's L2
+    __hip_atomic_fetch_add(f.sync + 2 * tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // the reduce items while the tile's other chunks finish (grad_gather / gather_adam's blocks
+  // [0, nrb): same sums, same order)
+  const int nrb = item_blocks(f.nitems);
+  if ((int)blockIdx.x < nrb) {
+    if (adam && blockIdx.x == 0 && tid == 0) {
+      f.state[0] = f.step;
+      f.state[1] = f.step;
+    }
+    float tot = 0.f, ss = 0.f;
+    int j;
+    if (item_reduce(f.part, f.npblk, f.npart, f.red_col, f.nitems, blockIdx.x, red, tot, j)) {
+      const int d = f.red_dst[j];
+      if (d >= 0) {
+        const float gi = tot * f.scale;
+        if (adam)
+          adam_apply<IDT>(d, gi, f.m[d], f.v[d], f.p[d], f.w_map[d], f.wt_map[d], f.g, f.p, f.m, f.v, f.b1, f.b2,
+                          step_size, rbc2, f.eps, wimg, f.qmul, f.f8);
+        else
+          f.g[d] = gi;
+        ss = gi * gi;
+      } else {
+        f.loss_out[-1 - d] = tot;
+      }
+    }
+    __syncthreads();
+    red[tid] = tid < ITEM_IPB ? ss : 0.f;
+    __syncthreads();
+    for (int w = 32; w > 0; w >>= 1) {
+      if (tid < w) red[tid] += red[tid + w];
+      __syncthreads();
+    }
+    if (adam && tid == 0) f.norm_part[blockIdx.x] = red[0];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int ok = 1;
+    for (unsigned spins = 0; __hip_atomic_load(f.sync + 2 * tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch;
+         ++spins) {
+      if (spins > FIX_SPIN_MAX) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    *okf = ok;
+  }
+  __syncthreads();
+  if (!*okf) {
+    if (tid == 0) __hip_atomic_store(f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  float ss = 0.f;
+  for (int j = e_lo + tid; j < e_hi; j += NT) {
+    // (no data-dependent branch before the slab loads: the per-element loads issue together)
+    const int i = f.elems[j];
+    const int mt = f.src_meta[i];
+    const int o = f.src_off[i];
+    float mi = 0.f, vi = 0.f, pv = 0.f;
+    int wi = -1, wti = -1;
+    if (adam) {
+      mi = f.m[i];
+      vi = f.v[i];
+      pv = f.p[i];
+      wi = f.w_map[i];
+      wti = f.wt_map[i];
+    }
+    const float gi = slab_sum_agent(a.slab + o, mt >> 4, (size_t)(mt & 15) << 12) * f.scale;
+    ss = fmaf(gi, gi, ss);
+    if (adam)
+      adam_apply<IDT>(i, gi, mi, vi, pv, wi, wti, f.g, f.p, f.m, f.v, f.b1, f.b2, step_size, rbc2, f.eps, wimg,
+                      f.qmul, f.f8);
+    else
+      f.g[i] = gi;
+  }
+  if (tid == 0) {   // the last task of the tile to leave resets its counters for the next launch
+    if (__hip_atomic_fetch_add(f.sync + 2 * tile + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1) {
+      __hip_atomic_store(f.sync + 2 * tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(f.sync + 2 * tile + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (!adam) return;
+  red[tid] = ss;
+  __syncthreads();
+  for (int w = NT / 2; w > 0; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) f.norm_part[nrb + blockIdx.x] = red[0];
+}
+
+// IDT >= 0: the fused slab reduction in the tail, weight image of precision IDT (-1: none)
+template <int DT, int S, int IDT = -1>
 __global__ __launch_bounds__(WG_WAVES * 64) void wgrad_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const WgradTask tk = a.tasks[blockIdx.x];
   if (4 * (tk.nq + tk.kq) <= 2 * WG_WAVES) wgrad_lds_body<DT, S, 2>(a, tk, smem);
   else wgrad_lds_body<DT, S, 3>(a, tk, smem);
+  if constexpr (IDT >= 0) wgrad_fixup<IDT>(a, smem);
 }
 
 // ring depth: fp32, split-bf16 and e4m3 3 stages (144 KiB), bf16 4 (96 KiB)
@@ -186,6 +330,36 @@ void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
   const size_t lds = wgrad_lds_bytes<DT, S>();
   set_max_lds_once<wgrad_kernel<DT, S>>(lds);
   hipLaunchKernelGGL((wgrad_kernel<DT, S>), dim3(a.ntasks), dim3(WG_WAVES * 64), lds, s, a);
+}
+
+// co-resident workgroups of the fused form (one below the occupancy answer per CU when it says
+// more than one: rollout.hip launch_nw)
+template <int DT, int S, int IDT>
+int fused_cap() {
+  const size_t lds = wgrad_lds_bytes<DT, S>();
+  set_max_lds_once<wgrad_kernel<DT, S, IDT>>(lds);
+  int per_cu = 0, dev = 0, ncu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(wgrad_kernel<DT, S, IDT>),
+                                                   WG_WAVES * 64, lds) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return ncu * (per_cu > 1 ? per_cu - 1 : per_cu);
+}
+
+template <int DT, int S, int IDT>
+void launch_wgrad_fused_t(const WgradArgs& a, hipStream_t s) {
+  static_assert(wgrad_lds_bytes<DT, S>() >= (WG_WAVES * 64 + 4) * sizeof(float), "fix-up scratch fits the ring");
+  const size_t lds = wgrad_lds_bytes<DT, S>();
+  const int cap = fused_cap<DT, S, IDT>();
+  if (a.ntasks > cap) {
+    dppo_note_error(hipErrorCooperativeLaunchTooLarge, __FILE__, __LINE__);
+    return;
+  }
+  WgradArgs aa = a;
+  void* args[] = {&aa};
+  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(wgrad_kernel<DT, S, IDT>),
+                                                  dim3(a.ntasks), dim3(WG_WAVES * 64), args, (unsigned)lds, s);
+  if (e != hipSuccess) dppo_note_error(e, __FILE__, __LINE__);
 }
 
 // Blocks [0, item_blocks(nitems)): the reduce items (log_std, loss-term sums, the per-head
@@ -235,6 +409,25 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
   else if (dt == DT_FP8) launch_wgrad_lds<DT_FP8, 3>(a, s);
   else launch_wgrad_lds<DT_BF16, 4>(a, s);
   HIP_CHECK_LAUNCH();
+}
+
+// (the image precision follows the update: split-bf16 / bf16 / fp32; the e4m3 wgrad of the fp8
+// mode updates the bf16 image)
+extern "C" void launch_wgrad_fused(int dt, int img_dt, const WgradArgs& a, hipStream_t s) {
+  if (a.ntasks <= 0) return;
+  if (dt == DT_S3 && img_dt == DT_S3) launch_wgrad_fused_t<DT_S3, 3, DT_S3>(a, s);
+  else if (dt == DT_BF16 && img_dt == DT_BF16) launch_wgrad_fused_t<DT_BF16, 4, DT_BF16>(a, s);
+  else if (dt == DT_FP8 && img_dt == DT_BF16) launch_wgrad_fused_t<DT_FP8, 3, DT_BF16>(a, s);
+  else if (dt == DT_F32 && img_dt == DT_F32) launch_wgrad_fused_t<DT_F32, 3, DT_F32>(a, s);
+  else dppo_note_error(hipErrorInvalidValue, __FILE__, __LINE__);
+}
+
+extern "C" int wgrad_fused_cap(int dt) {
+  if (dt == DT_S3) return fused_cap<DT_S3, 3, DT_S3>();
+  if (dt == DT_BF16) return fused_cap<DT_BF16, 4, DT_BF16>();
+  if (dt == DT_FP8) return fused_cap<DT_FP8, 3, DT_BF16>();
+  if (dt == DT_F32) return fused_cap<DT_F32, 3, DT_F32>();
+  return 0;
 }
 
 extern "C" void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part,

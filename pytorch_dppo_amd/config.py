@@ -99,6 +99,8 @@ class Params:
     stats_stream: str = "off"            # off | on | auto (on when an all-reduce sits in the chain): the
                                          # obs-stat reduce / all-reduce / merge on a side stream
     wgrad_wgs: int = 0                   # wgrad tasks per launch (0: one per CU of the device)
+    wgrad_gather: str = "auto"           # auto | fused (the split-K slab reduction and the Adam step in the
+                                         # wgrad launch's tail; needs every task co-resident) | separate
     mlp_rows: int = 0                    # diagnostics: force the tile update kernel's row tile (0: auto)
 
     # ------------------------------------------------------------------------------------
@@ -134,7 +136,8 @@ class Params:
         if self.obs_norm_update not in ("step", "rollout"):
             raise ValueError("obs_norm_update must be step|rollout")
         for name, ok in (("dist_backend", ("auto", "nccl", "gloo")), ("grad_comm", ("auto", "native", "process_group")),
-                         ("update_kernels", ("auto", "heads", "tile")), ("stats_stream", ("off", "on", "auto"))):
+                         ("update_kernels", ("auto", "heads", "tile")), ("stats_stream", ("off", "on", "auto")),
+                         ("wgrad_gather", ("auto", "fused", "separate"))):
             if getattr(self, name) not in ok:
                 raise ValueError(f"{name} must be {'|'.join(ok)}, got {getattr(self, name)}")
 

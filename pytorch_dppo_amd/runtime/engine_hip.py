@@ -244,7 +244,11 @@ class HipEngine:
         np_ = min(4096, self.A + 8 + (phi - self.A + 255) // 256)
         nv_ = min(4096, 8 + (vhi - vlo + 255) // 256)
         self.norm_regions = [(0, np_), (np_, np_ + nv_)]
-        self.norm_part = torch.zeros(max(n_whole, np_ + nv_), **f32)
+        # the fused wgrad + gather + Adam launch: one entry per reduce-item block and per task
+        self.norm_n_fused = 0
+        if self.heads:
+            self.norm_n_fused = (len(self.items["joint"][0]) + 31) // 32 + self.joint_bucket["tasks_host"].numel() // 8
+        self.norm_part = torch.zeros(max(n_whole, np_ + nv_, self.norm_n_fused), **f32)
         self.norm_n_whole = n_whole
         self._norm_n = n_whole       # entries the last Adam path wrote (metrics_pack sums them)
         # a value-head step not yet applied: ("work", all-reduce work, step, mean) on the
@@ -253,6 +257,17 @@ class HipEngine:
         self._side: Optional[torch.cuda.Stream] = None   # the side stream of the overlapped value step
         # world-size-1 fast path: grad_gather + no-clip Adam in one launch (fused_apply=False: off)
         self.fused_apply = bool(params.fused_apply)
+        # the joint wgrad with the slab reduction (+ Adam) in its tail (Params.wgrad_gather): needs
+        # every task co-resident (cooperative launch)
+        self.wgrad_fused = False
+        if self.heads and params.wgrad_gather != "separate":
+            cap = int(self.ext.wgrad_fused_cap(self._wgrad_dt())) if self.device.type == "cuda" else 0
+            ntask = self.joint_bucket["tasks_host"].numel() // 8
+            self.wgrad_fused = 0 < ntask <= cap
+            if params.wgrad_gather == "fused" and not self.wgrad_fused:
+                raise RuntimeError(f"wgrad_gather=fused: {ntask} wgrad tasks, {cap} co-resident workgroups")
+        self._fix_err = torch.zeros(1, dtype=torch.int32, **dev)
+        self._fix_err_host = torch.zeros(1, dtype=torch.int32, pin_memory=self.device.type == "cuda")
         self.idx_dev = torch.zeros(self.ldT, dtype=torch.int32, **dev)
         self.key_action = rng.base_key(params.seed, rng.STREAM_ACTION, action_rank)
         self.empty = torch.empty(0, dtype=torch.int32, **dev)
@@ -385,24 +400,80 @@ class HipEngine:
             self.buckets.append({
                 "tasks_host": tasks_host, "tasks": tasks_host.to(self.device),
                 "slab": torch.zeros(base, device=self.device, dtype=torch.float32),
-                "lo": lo, "hi": hi, "partials": partials[bi], "runs": self._slab_runs(sm, lo)})
+                "lo": lo, "hi": hi, "partials": partials[bi], "runs": self._slab_runs(sm, lo),
+                **self._fix_plan(order, tiles, tile_off, so, sm, lo)})
         src[src < 0] = 0  # reduce items (log_std, and with the per-head kernels mu / v)
         self.src_off = src.to(torch.int32).to(self.device)
         self.src_meta = meta.to(torch.int32).to(self.device)
+
+    def _fix_plan(self, order: list, tiles: list, tile_off: Dict, so: torch.Tensor, sm: torch.Tensor,
+                  lo: int) -> Dict:
+        """the wgrad launch's fused slab reduction (csrc/kernels.h WgradFix): per task [tile, nch,
+        e_lo, e_hi] — its 1/nch share of its tile's elements — and the elements (flat indices) of
+        every tile, tile by tile in ascending flat order (consecutive threads: consecutive
+        parameters and slab offsets).  The tile of an element is the one whose chunk-0 slab region
+        holds its src_off."""
+        bases = torch.tensor([tile_off[t][0] for t in tiles], dtype=torch.int64)
+        sizes = torch.tensor([tile_off[t][2] for t in tiles], dtype=torch.int64)
+        has = torch.nonzero(sm > 0).flatten()
+        off = so[has].to(torch.int64)
+        tid = torch.searchsorted(bases, off, right=True) - 1
+        assert bool((tid >= 0).all()) and bool((off < bases[tid] + sizes[tid]).all()), "slab element outside its tile"
+        perm = torch.sort(tid, stable=True).indices
+        elems = (has[perm] + lo).to(torch.int32)
+        cnt = torch.bincount(tid, minlength=len(tiles)).tolist()
+        start = [0]
+        for c in cnt:
+            start.append(start[-1] + c)
+        index = {t: k for k, t in enumerate(tiles)}
+        fix = []
+        for r in order:
+            t = (r[0], r[1], r[2], r[6], r[7])
+            k = index[t]
+            base, nch, size = tile_off[t]
+            ci = (r[5] - base) // size
+            e = cnt[k]
+            fix += [k, nch, start[k] + ci * e // nch, start[k] + (ci + 1) * e // nch]
+        fix_host = torch.tensor(fix, dtype=torch.int32)
+        return {"fix": fix_host.to(self.device), "fix_host": fix_host, "elems": elems.to(self.device),
+                "sync": torch.zeros(2 * len(tiles), dtype=torch.int32, device=self.device)}
 
     def q8_maxima(self) -> torch.Tensor:
         """[3 slots][4 tensors] gradient maxima (g1p, g2p, g1v, g2v) of the amax ring (diagnostics)"""
         return self.q8_amax.view(3, 4, Q8_SUB, 32)[..., 0].view(torch.float32).amax(-1)
 
+    def _wgrad_dt(self) -> int:
+        return native.DT_CODE["fp8"] if self.q8 else self.dt
+
+    def _q8_args(self) -> tuple:
+        if self.q8:
+            return (self.q8_amax, self._q8_step, [0, 1, -1, 2, 3, -1], [Q8_SX, Q8_SH, 1.0, Q8_SX, Q8_SH, 1.0])
+        return (self.empty, 0, [-1] * 6, [1.0] * 6)
+
+    def _wgrad_fused(self, b: Dict, mode: int, scale: float) -> None:
+        """bucket b's wgrad with the slab reduction in its tail (WgradFix): mode 1 = + grad_gather
+        into grad_flat, 2 = + gather_adam (the next Adam step).  A fix-up timeout of an earlier
+        launch (staged, no sync here) raises."""
+        if int(self._fix_err_host[0]) != 0:
+            raise RuntimeError("wgrad fused reduction timed out waiting for a tile's chunks")
+        p = self.p
+        b1, b2 = p.adam_betas
+        src_off, src_meta = self.joint_src
+        rc, rd = self.items["joint"]
+        self.ext.wgrad_fused(self._wgrad_dt(), self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
+                             b["tasks_host"], b["slab"], *self._q8_args(), mode, b["fix"], b["fix_host"], b["elems"],
+                             b["sync"], self._fix_err, src_off, src_meta, self.part_joint, self.nhead_blk,
+                             self.part_joint.shape[1], rc, rd, scale, self.loss_sums, self.grad_flat,
+                             self.model.flat.data, self.adam_m, self.adam_v, float(p.lr), float(b1), float(b2),
+                             float(p.adam_eps), self.adam_step + 1, self.adam_state,
+                             self.norm_part[:self.norm_n_fused], self.wimg, self.w_map, self.wt_map, self.dt,
+                             self.no_q, *self._f8())
+        self._fix_err_host.copy_(self._fix_err, non_blocking=True)
+
     def _wgrad(self, b: Dict) -> None:
         """one wgrad launch over bucket b's tasks (Q8: e4m3 operands, the step's scales)"""
-        if self.q8:
-            self.ext.wgrad(native.DT_CODE["fp8"], self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT,
-                           b["tasks"], b["tasks_host"], b["slab"], self.q8_amax, self._q8_step,
-                           [0, 1, -1, 2, 3, -1], [Q8_SX, Q8_SH, 1.0, Q8_SX, Q8_SH, 1.0])
-        else:
-            self.ext.wgrad(self.dt, self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                           b["tasks_host"], b["slab"], self.empty, 0, [-1] * 6, [1.0] * 6)
+        self.ext.wgrad(self._wgrad_dt(), self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
+                       b["tasks_host"], b["slab"], *self._q8_args())
 
     def _w8(self):
         """fp8 mode: (e4m3 image, per-layer scales) for the value head's e4m3 fc1; else off"""
@@ -984,6 +1055,9 @@ class HipEngine:
         gather of the whole gradient into grad_flat (no optimizer step)"""
         self._joint_heads(idx_t, first, xt_ready)
         b = self.joint_bucket
+        if self.wgrad_fused:
+            self._wgrad_fused(b, 1, 1.0 / self.mb)
+            return
         self._wgrad(b)
         src_off, src_meta = self.joint_src
         rc, rd = self.items["joint"]
@@ -996,6 +1070,11 @@ class HipEngine:
         p, M = self.p, self.mb
         self._joint_heads(idx_t, first, xt_ready)
         b = self.joint_bucket
+        if self.wgrad_fused:
+            self._wgrad_fused(b, 2, 1.0 / M)
+            self.adam_step += 1
+            self._norm_n = self.norm_n_fused
+            return
         self._wgrad(b)
         b1, b2 = p.adam_betas
         src_off, src_meta = self.joint_src

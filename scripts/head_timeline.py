@@ -67,6 +67,13 @@ def main():
                                                         for i, ph in enumerate(PHASES)},
                "fc1_first_span": float((t[:, :, 8] - t[:, :, 0]).max(dim=1).values.median()),
                "fc1_mid_span(4 k-steps value / 3 stages policy)": float((t[:, :, 9] - t[:, :, 8]).max(dim=1).values.median())}
+        # sub-spans (max over waves): fc3 MFMAs (3 -> 12) vs the loss (12 -> 4); the partials phase as
+        # the fused narrow-layer dW MFMAs (6 -> 10), the wave's store / DMA drain (10 -> 11) and the
+        # workgroup reduction + partial-row stores (11 -> 7)
+        res["sub_spans_median_cycles"] = {
+            name: float((t[:, :, b] - t[:, :, a_]).max(dim=1).values.median())
+            for name, a_, b in (("fc3", 3, 12), ("loss", 12, 4), ("narrow dW", 6, 10), ("drain", 10, 11),
+                                ("reduce + store", 11, 7))}
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
         blk = torch.arange(t.shape[0]) * EVERY
         rnd = blk // ncu

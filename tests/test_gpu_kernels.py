@@ -983,6 +983,58 @@ def test_fused_gather_adam_bit_identical_to_gather_then_adam(dtype, loss, monkey
     assert mt0["loss"] == mt1["loss"]
 
 
+@pytest.mark.parametrize("dtype", ["bf16x3", "bf16", "fp8"])
+def test_wgrad_fused_reduction_bit_identical(dtype, monkeypatch):
+    """The split-K slab reduction + Adam step in the wgrad launch's tail (wgrad_gather=fused:
+    cooperative launch, csrc/wgrad.hip wgrad_fixup — every task publishes its chunk, waits for its
+    tile's other chunks, reduces its share) == the wgrad launch followed by gather_adam
+    (wgrad_gather=separate), bit for bit after 2 iterations: parameters, Adam moments, the weight
+    images, the gradient and the loss sums, at a geometry where every weight tile is cut into many
+    batch chunks.  The per-tile counters reset themselves.  Mode 1 (the gather alone, then the
+    in-stream native RCCL all-reduce + the whole-vector Adam, forced at world size 1) == both."""
+    from pytorch_dppo_amd.parallel.dist import DistContext, init_single_rank_collective
+    from pytorch_dppo_amd.runtime.launcher import free_port
+    from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    common = dict(device="gpu", env_name="Humanoid-v2", num_envs=1024, exploration_size=1024 * 16,
+                  batch_size=1024 * 16, num_epoch=3, dtype=dtype, seed=7, update_kernels="heads")
+
+    def run(w):
+        ms = [w.iteration_step() for _ in range(2)]
+        w.flush_pending()
+        torch.cuda.synchronize()
+        e = w.engine
+        img8 = e.wimg_fwd.clone() if dtype == "fp8" else None
+        return (w.model.flat.data.clone(), e.adam_m.clone(), e.adam_v.clone(), e.wimg.view(torch.uint8).clone(),
+                img8, e.grad_flat.clone(), ms[-1])
+
+    outs = []
+    for mode in ("fused", "separate"):
+        w = DPPOWorker(dppo_preset(**common, wgrad_gather=mode), DistContext(device=DEV))
+        assert w.engine.wgrad_fused == (mode == "fused")
+        outs.append(run(w))
+        if mode == "fused":
+            b = w.engine.joint_bucket
+            assert b["tasks_host"].numel() // 8 > 100 and int(b["fix_host"].view(-1, 4)[:, 1].max()) > 8
+            assert int(w.engine._fix_err.item()) == 0 and int(b["sync"].abs().sum().item()) == 0
+    ctx = init_single_rank_collective(DEV, port=free_port(), grad_comm="native")
+    ctx.force_collectives = True
+    try:
+        w2 = DPPOWorker(dppo_preset(**common, wgrad_gather="fused"), ctx)
+        assert w2.engine.wgrad_fused and ctx.native is not None
+        outs.append(run(w2))
+    finally:
+        ctx.destroy()
+    ref = outs[1]
+    for o in (outs[0], outs[2]):
+        for k in range(4):
+            assert torch.equal(o[k], ref[k]), k
+        if dtype == "fp8":
+            assert torch.equal(o[4], ref[4])
+        assert torch.equal(o[5], ref[5])
+        assert o[6]["loss"] == ref[6]["loss"]
+        assert abs(o[6]["grad_norm"] - ref[6]["grad_norm"]) <= 1e-5 * (1 + ref[6]["grad_norm"])
+
+
 def test_side_stream_obs_stats_bit_identical(monkeypatch):
     """The rollout-mode obs-stat reduce + merge on a side stream (overlapping values/GAE/update)
     leaves parameters, normaliser state and metrics exactly as the inline path does."""
