@@ -99,8 +99,9 @@ class Params:
     stats_stream: str = "off"            # off | on | auto (on when an all-reduce sits in the chain): the
                                          # obs-stat reduce / all-reduce / merge on a side stream
     wgrad_wgs: int = 0                   # wgrad tasks per launch (0: one per CU of the device)
-    wgrad_gather: str = "auto"           # auto | fused (the split-K slab reduction and the Adam step in the
-                                         # wgrad launch's tail; needs every task co-resident) | separate
+    wgrad_gather: str = "auto"           # auto (= separate) | separate | fused (the split-K slab reduction and
+                                         # the Adam step in the wgrad launch's tail; needs every task
+                                         # co-resident; measured slower, profiles/r4/ab_wgrad_gather.md)
     mlp_rows: int = 0                    # diagnostics: force the tile update kernel's row tile (0: auto)
 
     # ------------------------------------------------------------------------------------

@@ -257,10 +257,12 @@ class HipEngine:
         self._side: Optional[torch.cuda.Stream] = None   # the side stream of the overlapped value step
         # world-size-1 fast path: grad_gather + no-clip Adam in one launch (fused_apply=False: off)
         self.fused_apply = bool(params.fused_apply)
-        # the joint wgrad with the slab reduction (+ Adam) in its tail (Params.wgrad_gather): needs
-        # every task co-resident (cooperative launch)
+        # the joint wgrad with the slab reduction (+ Adam) in its tail (Params.wgrad_gather=fused): needs
+        # every task co-resident (cooperative launch).  Opt-in: same-box A/B, it is 8 % (bf16x3) and
+        # 13 % (bf16) SLOWER per iteration than the separate gather launch (profiles/r4/ab_wgrad_gather.md),
+        # so "auto" keeps the separate launch.
         self.wgrad_fused = False
-        if self.heads and params.wgrad_gather != "separate":
+        if self.heads and params.wgrad_gather == "fused":
             cap = int(self.ext.wgrad_fused_cap(self._wgrad_dt())) if self.device.type == "cuda" else 0
             ntask = self.joint_bucket["tasks_host"].numel() // 8
             self.wgrad_fused = 0 < ntask <= cap
