@@ -18,6 +18,29 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
 #define DEV __device__ __forceinline__
+typedef __attribute__((ext_vector_type(8))) float f32x8v;
+// Elementwise fp32 vector arithmetic of the MFMA epilogues / operand splits.  Plain vector ops lower
+// to packed v_pk_{add,mul,fma}_f32, which beside MFMAs cost more than the two scalar ops they replace
+// (MI355X_MICROARCH.md, 'price of one filler beside MFMAs'); DPPO_NOPK (A/B, with -fno-slp-vectorize
+// so the SLP pass does not re-pack them) spells them as scalar ops.
+#ifdef DPPO_NOPK
+#define DPPO_EW(N, expr)                       \
+  do {                                         \
+    _Pragma("unroll") for (int i = 0; i < N; ++i) { expr; } \
+  } while (0)
+DEV f32x4 ew_sub(const f32x4& a, const f32x4& b) { f32x4 r; DPPO_EW(4, r[i] = a[i] - b[i]); return r; }
+DEV f32x8v ew_sub(const f32x8v& a, const f32x8v& b) { f32x8v r; DPPO_EW(8, r[i] = a[i] - b[i]); return r; }
+DEV f32x8v ew_add(const f32x8v& a, const f32x8v& b) { f32x8v r; DPPO_EW(8, r[i] = a[i] + b[i]); return r; }
+DEV f32x4 ew_mul(const f32x4& a, float s) { f32x4 r; DPPO_EW(4, r[i] = a[i] * s); return r; }
+// a * (1 - h * h) (the tanh derivative)
+DEV f32x4 ew_dtanh(const f32x4& a, const f32x4& h) { f32x4 r; DPPO_EW(4, r[i] = a[i] * __builtin_fmaf(-h[i], h[i], 1.0f)); return r; }
+#else
+DEV f32x4 ew_sub(const f32x4& a, const f32x4& b) { return a - b; }
+DEV f32x8v ew_sub(const f32x8v& a, const f32x8v& b) { return a - b; }
+DEV f32x8v ew_add(const f32x8v& a, const f32x8v& b) { return a + b; }
+DEV f32x4 ew_mul(const f32x4& a, float s) { return a * s; }
+DEV f32x4 ew_dtanh(const f32x4& a, const f32x4& h) { return a * (1.0f - h * h); }
+#endif
 
 enum { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2, DT_S3 = 3 };
 

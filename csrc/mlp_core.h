@@ -50,6 +50,12 @@ DEV f32x4 act_tanh4(f32x4 x) {
   if constexpr (DT == DT_F32) {
     return f32x4{tanhf(x[0]), tanhf(x[1]), tanhf(x[2]), tanhf(x[3])};
   } else {
+#ifdef DPPO_NOPK
+    f32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = act_tanh<DT>(x[i]);
+    return r;
+#else
     const f32x4 y = x * (2.0f * 1.4426950408889634f);
     f32x4 e;
 #pragma unroll
@@ -58,6 +64,7 @@ DEV f32x4 act_tanh4(f32x4 x) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_rcpf(e[i]);
     return __builtin_elementwise_fma(e, f32x4{-2.f, -2.f, -2.f, -2.f}, f32x4{1.f, 1.f, 1.f, 1.f});
+#endif
   }
 }
 

@@ -48,6 +48,7 @@ constexpr int MAX_STEPS = 64;
 #endif
 
 typedef __attribute__((ext_vector_type(8))) float f32x8;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4h;
 
 // Operand precision of the head kernels: how a 512-element fragment sits in global memory and in
@@ -70,17 +71,17 @@ template <> struct HT<DT_S3> {
   }
   DEV static Frag from8(const f32x8& x) {
     const bf16x8 h = __builtin_convertvector(x, bf16x8);
-    const bf16x8 l = __builtin_convertvector(x - __builtin_convertvector(h, f32x8), bf16x8);
+    const bf16x8 l = __builtin_convertvector(ew_sub(x, __builtin_convertvector(h, f32x8)), bf16x8);
     return Frag{h, l};
   }
   DEV static f32x8 to8(const Frag& f) {
-    return __builtin_convertvector(f.h, f32x8) + __builtin_convertvector(f.l, f32x8);
+    return ew_add(__builtin_convertvector(f.h, f32x8), __builtin_convertvector(f.l, f32x8));
   }
   DEV static char* eptr(void* buf, size_t i) { return reinterpret_cast<char*>(P::hi_ptr(reinterpret_cast<P::T*>(buf), i)); }
   // 4 consecutive elements of an 8-group (hi at p, lo 16 bytes on)
   DEV static void store4(char* p, const f32x4& v) {
     const bf16x4v hv = __builtin_convertvector(v, bf16x4v);
-    const bf16x4v lv = __builtin_convertvector(v - __builtin_convertvector(hv, f32x4), bf16x4v);
+    const bf16x4v lv = __builtin_convertvector(ew_sub(v, __builtin_convertvector(hv, f32x4)), bf16x4v);
     opnd_store(*reinterpret_cast<const u32x2*>(&hv), reinterpret_cast<u32x2*>(p));
     opnd_store(*reinterpret_cast<const u32x2*>(&lv), reinterpret_cast<u32x2*>(p + 16));
   }
@@ -138,9 +139,16 @@ template <> struct HeadCfg<1> {   // value: v_fc1 -> v_fc2 -> v
   static constexpr int NEED = 744;          // loss tile, partials, dW_v partials
 };
 
-// F8 (fp8 mode, value head, bf16 update): fc1 reads the e4m3 weight image and e4m3-rounded
-// observations (v_mfma_f32_16x16x32_fp8_fp8): a 1 KiB ring slot holds one tile's fragments of two
-// consecutive k-steps, so the fc1 stream and its LDS reads are half the bf16 bytes.
+// F8 (fp8 mode, bf16 update): the forward GEMMs read the e4m3 weight image (the Adam step's shadow,
+// csrc/adam_core.h f8_put; W / qscale[layer]).  A 1 KiB ring slot holds one tile's e4m3 fragments of
+// two consecutive k-steps, so the stream and its LDS reads are half the bf16 bytes.
+//  * value head: fc1 on v_mfma_f32_16x16x32_fp8_fp8 with e4m3-rounded observations (2 stages of 16
+//    tiles per k-step pair);
+//  * policy head: fc1 AND fc2 on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (twice the bf16
+//    MFMA rate): a stage holds 4 k-steps of the 8 tiles (slots 2t, 2t + 1), the A operand is the
+//    lane's 8 e4m3 bytes of each of the 4 k-steps (observations unscaled, h1 x Q8_SH), the same k
+//    order as the weight pieces, so the 128-term sum covers every k once (E8M0 scales 1; the epilogue
+//    multiplies by qscale, / Q8_SH for fc2).  fc1: ks1 / 4 stages, fc2: ONE stage (K = 128).
 template <int DT, int HEAD, bool F8 = false>
 constexpr int head_stages() { return DT == DT_S3 ? HeadCfg<HEAD>::S3 : (F8 ? 4 : HeadCfg<HEAD>::SBF); }
 // X ring slots (k-steps), a power of two.  An observation DMA must be OLDER than the weight batch
@@ -184,13 +192,22 @@ constexpr bool head_lds_ok() {
 }
 static_assert(head_lds_ok<DT_S3>() && head_lds_ok<DT_BF16>() && head_lds_ok<DT_BF16, true>(),
               "head kernel LDS carving / observation lead");
+// the fp8 policy: LDS, the dW_mu reduction through its ring, and an X ring two 4-k-step stages deep
+// (its waits retire every refill, so the observations need lead 2 >= 2, not >= S)
+static_assert(head_lds_bytes<DT_BF16, 0, true>() <= 160 * 1024 &&
+                  4 * 32 * 128 * 4 <= head_stages<DT_BF16, 0, true>() * stage_bytes<DT_BF16>() &&
+                  head_xs<DT_BF16, 0, true>() / 4 >= 2 && head_stages<DT_BF16, 0, true>() >= 3,
+              "fp8 policy head LDS carving / observation lead");
 static_assert(HeadCfg<0>::NW * wrows<0>() == ROWS && HeadCfg<1>::NW * wrows<1>() == ROWS, "128 rows per workgroup");
 // loss scratch (after fc1, in the X ring): dL/dmu | dL/dv [rows][SST], then the wave's partials
 static_assert(wrows<0>() * 32 <= HeadCfg<0>::RB * TILE_F, "mu tile fits the transpose tiles");
 static_assert(HeadCfg<0>::NW == 8 && HeadCfg<0>::RB == 1, "the fused dW_mu reduction assumes 8 waves of 16 rows");
 
 template <int HEAD, bool F8 = false>
-DEV int fc1_stages(int ks1) { return HEAD == 0 ? (ks1 + 1) >> 1 : (F8 ? ks1 : 2 * ks1); }
+DEV int fc1_stages(int ks1) { return HEAD == 0 ? (F8 ? ks1 >> 2 : (ks1 + 1) >> 1) : (F8 ? ks1 : 2 * ks1); }
+// fc2 stages: 2 k-steps each; e4m3 (F8) 4 k-steps each on the x128 MFMA (policy K = 128: one stage)
+template <int HEAD, bool F8 = false>
+constexpr int fc2_stages() { return F8 ? HeadCfg<HEAD>::K2 / 4 : HeadCfg<HEAD>::K2 / 2; }
 
 DEV int rot_ks(int ks, int rot, int ks1) {
   const int k = ks + rot;
@@ -203,12 +220,17 @@ DEV int rot_ks(int ks, int rot, int ks1) {
 template <int HEAD, bool FWD, bool F8>
 DEV int step_src(const MlpArgs& a, int st, int q, int rot, int ks1) {
   using C = HeadCfg<HEAD>;
-  const int ns1 = fc1_stages<HEAD, F8>(ks1), ns2 = C::K2 / 2;
+  const int ns1 = fc1_stages<HEAD, F8>(ks1), ns2 = fc2_stages<HEAD, F8>();
   const int s_fc3 = ns1 + ns2, s_dg2 = s_fc3 + 1, s_end = FWD ? s_dg2 : s_dg2 + C::NS4;
   if (st >= s_end) st = s_end - 1;
   if (st < ns1) {
     int ks, t;
-    if constexpr (HEAD == 0) {
+    if constexpr (HEAD == 0 && F8) {
+      // slots 2t, 2t + 1: tile t's k-step pairs 4 st, 4 st + 2 (rot a multiple of 4, ks1 too)
+      ks = 4 * st + 2 * (q & 1);
+      t = q >> 1;
+      if (t >= C::N1R) return -1;
+    } else if constexpr (HEAD == 0) {
       ks = 2 * st + (q >> 3);
       t = q & 7;
       if (t >= C::N1R || ks >= ks1) return -1;
@@ -219,6 +241,11 @@ DEV int step_src(const MlpArgs& a, int st, int q, int rot, int ks1) {
       t = 16 * (st & 1) + q;
     }
     return a.off_w[C::L1] + (int)fm_frag(t, rot_ks(ks, rot, ks1), a.d_in[C::L1], 0);
+  }
+  if (F8 && st < s_fc3) {   // the e4m3 fc2 stages: tile q >> 1, k-steps 4 (st - ns1) + 2 (q & 1) + {0, 1}
+    const int t = q >> 1;
+    if (t == 7) return -1;
+    return a.off_w[C::L2] + (int)fm_frag(t, 4 * (st - ns1) + 2 * (q & 1), a.d_in[C::L2], 0);
   }
   if (st < s_fc3) {
     const int i = 2 * (st - ns1) + (q >> 3), t = q & 7;
@@ -260,8 +287,7 @@ DEV void tp_put(float* tp, const f32x4& v0, const f32x4& v1, int lane) {
 
 // A operand (row lane & 15, k = 8 (lane >> 4) .. +7) of a [16][SST] tile; reads + wait in one asm
 // statement (a plain LDS load would wait vmcnt(0) for the ring's LDS-DMA)
-template <int DT>
-DEV typename HT<DT>::Frag tp_getA(const float* tp, int lane) {
+DEV f32x8 tp_get8(const float* tp, int lane) {
   const float* r = tp + (lane & 15) * SST + 8 * (lane >> 4);
   const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)r;
   float4 x0, x1;
@@ -269,7 +295,11 @@ DEV typename HT<DT>::Frag tp_getA(const float* tp, int lane) {
                : "=&v"(x0), "=&v"(x1)
                : "v"(addr)
                : "memory");
-  return HT<DT>::from8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w});
+  return f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+}
+template <int DT>
+DEV typename HT<DT>::Frag tp_getA(const float* tp, int lane) {
+  return HT<DT>::from8(tp_get8(tp, lane));
 }
 
 DEV f32x4 bias_col(const f32x4& v, int c, int nb) {
@@ -402,7 +432,7 @@ DEV float xsum(float x) {   // sum over the lanes that differ only in the bits o
 template <int DT, int HEAD, bool FWD = false, bool F8 = false, bool Q8 = false>
 __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(MlpArgs a) {
   static_assert(!FWD || HEAD == 1, "forward mode is the value head's");
-  static_assert(!F8 || (HEAD == 1 && DT == DT_BF16), "the e4m3 fc1 is the bf16 value head's");
+  static_assert(!F8 || DT == DT_BF16, "the e4m3 forward GEMMs are the bf16 update's (fp8 mode)");
   static_assert(!Q8 || (DT == DT_BF16 && !FWD), "e4m3 wgrad operands: the fp8 mode's (bf16) update");
   using C = HeadCfg<HEAD>;
   using H = HT<DT>;
@@ -483,8 +513,11 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   for (int rb = 0; rb < RB; ++rb)
     xsrc[rb] = reinterpret_cast<const char*>(a.x_buf) +
                (size_t)src_of(WROWS * wave + 16 * rb + lr) * (size_t)a.d_in[0] * sizeof(T) + H::xlane(lane);
-  // (F8: an even rotation keeps each fc1 k-step pair contiguous; the launcher checks ks1 even)
-  const int rot = F8 ? 2 * (int)(blockIdx.x % (unsigned)(ks1 >> 1)) : (int)(blockIdx.x % (unsigned)ks1);
+  // (F8: an even rotation keeps each fc1 k-step pair contiguous; the launcher checks ks1 even — the
+  // policy's: a multiple of 4, ks1 % 4 == 0)
+  const int rot = (F8 && HEAD == 0) ? 4 * (int)(blockIdx.x % (unsigned)(ks1 >> 2))
+                  : F8              ? 2 * (int)(blockIdx.x % (unsigned)(ks1 >> 1))
+                                    : (int)(blockIdx.x % (unsigned)ks1);
   auto code16 = [&](int st, int q) __attribute__((always_inline)) {
     int c = step_src<HEAD, FWD, F8>(a, st, q, rot, ks1);
     if (c < 0) c = step_src<HEAD, FWD, F8>(a, st, 0, rot, ks1);
@@ -509,7 +542,8 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
     for (int u = 0; u < SPW; ++u) {
       const uint32_t code = ((u < 2 ? w01 : w23) >> (16 * (u & 1))) & 0xffffu;
-      if (F8 && st < ns1) {   // fc1: two e4m3 fragments (512 B each) of the tile per slot
+      // the e4m3 stages (fc1, fc2): two e4m3 fragments (512 B each) of a tile per slot
+      if (F8 && st < ns1 + fc2_stages<HEAD, F8>()) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rw8, stg + u * FB, 16, vw, code * 512u, 0, 0);
       } else {
 #pragma unroll
@@ -558,15 +592,21 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
   for (int i = 0; i < NH; ++i) hist[i] = 0;
   auto flush = NoHook{};   // (A/B in round 4: the refill issued after the first fragment reads: no gain)
-  auto wait_step = [&](int younger) __attribute__((always_inline)) -> const char* {
+  // LEAD > 0: the wait also retires the next LEAD stages' batches (the fp8 policy's fc1: every
+  // refill, so an observation DMA issued two stages back is certified with them — its X ring leads
+  // by 2 stages of 4 k-steps; a batch then has LEAD fewer stages of compute to land in)
+  auto wait_step_l = [&](int younger, auto leadc) __attribute__((always_inline)) -> const char* {
+    constexpr int LEAD = decltype(leadc)::value;
+    static_assert(S - 2 - LEAD >= 0, "ring too shallow for the lead");
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = NH - 1; i > 0; --i) hist[i] = hist[i - 1];
     hist[0] = younger;
+    // (the younger ops that may stay outstanding: those issued after the oldest refill allowed to)
     int extra = 0;
 #pragma unroll
-    for (int i = 0; i < NH; ++i) extra += hist[i];
-    wait_vm<GL * (S - 2)>(extra);
+    for (int i = 0; i < NH - LEAD; ++i) extra += hist[i];
+    wait_vm<GL * (S - 2 - LEAD)>(extra);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #ifndef DPPO_ABL_NOBAR
     __builtin_amdgcn_s_barrier();
@@ -577,6 +617,9 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     cst = cst + 1 == S ? 0 : cst + 1;
     ++cur;
     return stg;
+  };
+  auto wait_step = [&](int younger) __attribute__((always_inline)) -> const char* {
+    return wait_step_l(younger, std::integral_constant<int, 0>{});
   };
 
   HD_STAMP(0);
@@ -652,17 +695,55 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
                    mw + 16 * rb + 8 * (lane & 1), a.ldT);
     }
   };
-  if constexpr (F8) {
+  // 8 fp32 -> 8 OCP e4m3 bytes (round to nearest even, saturating: v_cvt_pk_fp8_f32)
+  auto f8x8 = [&](const f32x8& v) __attribute__((always_inline)) -> long {
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], hi, true);
+    return (long)(((unsigned long)(unsigned)hi << 32) | (unsigned)lo);
+  };
+  // observations x Q8_SX (|x| <= 5 after the clamp: <= 320, below e4m3's 448) so the small normalised
+  // features stay out of e4m3's subnormal range; fc1's epilogue divides it out with the weight scale
+  auto to_f8 = [&](const Frag& x) __attribute__((always_inline)) -> long { return f8x8(H::to8(x) * Q8_SX); };
+  // the x128 B operand of tile t from a stage of the fp8 policy (slots 2t, 2t + 1: k-steps 4j .. 4j+3)
+  auto b128 = [&](const char* sb, int t) __attribute__((always_inline)) -> i32x8 {
+    const char* p = sb + 2 * t * FB + lane * 8;
+    const long x0 = *reinterpret_cast<const long*>(p), x1 = *reinterpret_cast<const long*>(p + 512);
+    const long x2 = *reinterpret_cast<const long*>(p + FB), x3 = *reinterpret_cast<const long*>(p + FB + 512);
+    return i32x8{(int)x0, (int)(x0 >> 32), (int)x1, (int)(x1 >> 32), (int)x2, (int)(x2 >> 32), (int)x3, (int)(x3 >> 32)};
+  };
+  auto a128 = [&](long q0, long q1, long q2, long q3) __attribute__((always_inline)) -> i32x8 {
+    return i32x8{(int)q0, (int)(q0 >> 32), (int)q1, (int)(q1 >> 32), (int)q2, (int)(q2 >> 32), (int)q3, (int)(q3 >> 32)};
+  };
+  if constexpr (F8 && HEAD == 0) {
+    // e4m3 fc1 of the policy on the x128 MFMA: stage st = k-steps 4 st .. 4 st + 3 of the 7 tiles.
+    // Every wait retires all refills (LEAD = S - 2): the observation k-steps a stage reads were
+    // issued two stages back, before the previous stage's refill, so that wait certifies them.
+    for (int st = 0; st < ns1; ++st) {
+      stg = wait_step_l(st > 0 ? 4 * XDMA : 0, std::integral_constant<int, S - 2>{});
+      Frag xf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xf[j] = read_x(4 * st + j, 0);
+      const i32x8 xq = a128(to_f8(xf[0]), to_f8(xf[1]), to_f8(xf[2]), to_f8(xf[3]));
+#pragma unroll
+      for (int t = 0; t < C::N1R; ++t)
+        acc1[0][t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(xq, b128(stg, t), acc1[0][t], 0, 0, 0, 127, 0, 127);
+      if (want_xT) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) put_xT(xf[j], 4 * st + j, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) issue_x(4 * st + j + XS);   // into the slots just read
+      if (st == 0) HD_STAMP(8);
+      if (st == 1) HD_STAMP(9);
+    }
+    const float s1 = a.qscale[C::L1] * (1.0f / Q8_SX);   // the e4m3 image holds W1 / qscale
+#pragma unroll
+    for (int t = 0; t < C::N1; ++t) acc1[0][t] *= s1;
+  } else if constexpr (F8) {
     // e4m3 fc1: per k-step pair 2 stages (tiles 0-15, 16-31), each slot one tile's two fragments;
     // the observation fragments (bf16 in the X ring) rounded to e4m3 in registers
-    auto to_f8 = [&](const Frag& x) __attribute__((always_inline)) -> long {
-      const f32x8 v = H::to8(x);
-      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
-      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
-      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false);
-      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], hi, true);
-      return (long)(((unsigned long)(unsigned)hi << 32) | (unsigned)lo);
-    };
     long xq0 = 0, xq1 = 0;
     for (int j = 0; j < (ks1 >> 1); ++j) {
       static_for<0, 2>([&](auto sc) __attribute__((always_inline)) {
@@ -687,7 +768,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         }
       });
     }
-    const float s1 = a.qscale[C::L1];   // the e4m3 image holds W1 / qscale
+    const float s1 = a.qscale[C::L1] * (1.0f / Q8_SX);   // the e4m3 image holds W1 / qscale
 #pragma unroll
     for (int t = 0; t < C::N1; ++t) acc1[0][t] *= s1;
   } else if constexpr (HEAD == 1) {
@@ -793,9 +874,42 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int t = 0; t < 8; ++t) acc2[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int nst = 0;
+  if constexpr (F8) {
+    // e4m3 fc2: h1 (4 k-steps per stage, e4m3 x Q8_SH) x the e4m3 W2 image on the x128 MFMA — the
+    // policy's K = 128 in ONE stage, the value's 512 in 4; a stage's operand preparation (tanh, h1^T
+    // stores, transposes) precedes its wait, and issues beside the previous stage's MFMAs
+    // (+ the first wait: the policy's last fc1 stage's past-the-end X re-loads)
+    nst = HEAD == 0 ? 4 * XDMA : 0;
+    static_for<0, fc2_stages<HEAD, F8>()>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      i32x8 ha;
+      static_for<0, 4>([&](auto Ic) __attribute__((always_inline)) {
+        constexpr int I = decltype(Ic)::value;
+        prep_a(std::integral_constant<int, 4 * j + I>{});
+        const long q = f8x8(tp_get8(tpb, lane) * Q8_SH);
+        ha[2 * I] = (int)q;
+        ha[2 * I + 1] = (int)(q >> 32);
+      });
+      stg = wait_step(nst + 4 * NSTA);
+      nst = 0;
+      // (tile pairs between scheduling barriers: at most two tiles' 8-register B operands live —
+      // the value head has no registers for all seven)
+      static_for<0, 7>([&](auto tc) __attribute__((always_inline)) {
+        constexpr int t = decltype(tc)::value;
+        acc2[0][t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ha, b128(stg, t), acc2[0][t], 0, 0, 0, 127, 0, 127);
+        if constexpr (t & 1) __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+    const float s2 = a.qscale[C::L2] * (1.0f / Q8_SH);
+    // h2 = tanh(fc2), kept in registers for fc3, dgrad fc3 and the fused narrow-layer wgrad
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc2[0][t] = act_tanh4<DT_S3>(acc2[0][t] * s2);
+  } else {
   Frag a0[RB], a1[RB];
   // (+ the X loads of the last fc1 step: policy past-the-end re-loads)
-  int nst = prep(std::integral_constant<int, 0>{}, a0) + (HEAD == 0 ? 2 * XDMA : 0);
+  nst = prep(std::integral_constant<int, 0>{}, a0) + (HEAD == 0 ? 2 * XDMA : 0);
   static_for<0, C::K2 / 2>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     stg = wait_step(nst);
@@ -829,6 +943,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
         for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = act_tanh4<DT_S3>(acc2[rb][t]);
     }
   });
+  }
 
   HD_STAMP(2);
   // ---------------- fc3 + loss + dgrad fc3: one stage ----------------
@@ -1092,7 +1207,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     const int c = 16 * t + lr;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
-      d2[rb][t] = c < n2 ? d2[rb][t] * (1.0f - acc2[rb][t] * acc2[rb][t]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      d2[rb][t] = c < n2 ? ew_dtanh(d2[rb][t], acc2[rb][t]) : f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (Q8) am2 = fmaxf(am2, absmax4(d2[rb][t]));
       opnd4(bg2[rb] + (size_t)t * tsb, d2[rb][t], sg2);
     }
@@ -1120,7 +1235,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
           const f32x4 h = acc1[rb][tt];
-          const f32x4 gv = gq[decltype(uc)::value][rb] * (1.0f - h * h);
+          const f32x4 gv = ew_dtanh(gq[decltype(uc)::value][rb], h);
           if constexpr (Q8) am1 = fmaxf(am1, absmax4(gv));
           opnd4(bg1[rb] + (size_t)tt * tsb, gv, sg1);
         }
@@ -1281,22 +1396,27 @@ void head_launch_t(const MlpArgs& a, hipStream_t s) {
 
 // the value head in fp8 mode (a.W8: the e4m3 image, a.qscale its per-layer scales) takes the
 // e4m3 fc1 when the k-steps pair up (d_in a multiple of 64)
+// (F8 needs the fc1 k-steps to group: pairs for the value head, quads for the policy's x128 MFMA)
+template <int HEAD>
+bool f8_applies(const MlpArgs& a) {
+  const int ks1 = a.d_in[0] >> 5;
+  return a.W8 != nullptr && a.qscale != nullptr && (HEAD == 0 ? (ks1 & 3) == 0 : (ks1 & 1) == 0);
+}
+
 template <int DT, int HEAD, bool FWD = false>
 void head_launch(const MlpArgs& a, hipStream_t s) {
   if constexpr (DT == DT_BF16 && !FWD) {
-    if (a.q8_rd != nullptr) {   // fp8 mode: e4m3 wgrad operands (+ the value head's e4m3 fc1)
-      if constexpr (HEAD == 1) {
-        if (a.W8 != nullptr && a.qscale != nullptr && ((a.d_in[0] >> 5) & 1) == 0) {
-          head_launch_t<DT, HEAD, FWD, true, true>(a, s);
-          return;
-        }
+    if (a.q8_rd != nullptr) {   // fp8 mode: e4m3 wgrad operands (+ the e4m3 forward GEMMs)
+      if (f8_applies<HEAD>(a)) {
+        head_launch_t<DT, HEAD, FWD, true, true>(a, s);
+        return;
       }
       head_launch_t<DT, HEAD, FWD, false, true>(a, s);
       return;
     }
   }
-  if constexpr (DT == DT_BF16 && HEAD == 1) {
-    if (a.W8 != nullptr && a.qscale != nullptr && ((a.d_in[0] >> 5) & 1) == 0) {
+  if constexpr (DT == DT_BF16 && (HEAD == 1 || !FWD)) {
+    if (f8_applies<HEAD>(a)) {
       head_launch_t<DT, HEAD, FWD, true>(a, s);
       return;
     }
