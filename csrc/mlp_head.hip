@@ -205,9 +205,13 @@ static_assert(HeadCfg<0>::NW == 8 && HeadCfg<0>::RB == 1, "the fused dW_mu reduc
 
 template <int HEAD, bool F8 = false>
 DEV int fc1_stages(int ks1) { return HEAD == 0 ? (F8 ? ks1 >> 2 : (ks1 + 1) >> 1) : (F8 ? ks1 : 2 * ks1); }
-// fc2 stages: 2 k-steps each; e4m3 (F8) 4 k-steps each on the x128 MFMA (policy K = 128: one stage)
+// fc2 stages: 2 k-steps each; the fp8 policy's e4m3 fc2 (K = 128) on the x128 MFMA in ONE.  (The value
+// head's fc2 on e4m3 — 4 stages of 4 k-steps — was measured slower: 2.095 vs 1.983 ms per fp8
+// iteration, the value kernel spilling 27 VGPRs; profiles/r4/fp8_heads.md)
 template <int HEAD, bool F8 = false>
-constexpr int fc2_stages() { return F8 ? HeadCfg<HEAD>::K2 / 4 : HeadCfg<HEAD>::K2 / 2; }
+constexpr int fc2_stages() { return (F8 && HEAD == 0) ? HeadCfg<HEAD>::K2 / 4 : HeadCfg<HEAD>::K2 / 2; }
+template <int HEAD, bool F8 = false>
+constexpr bool f8_fc2() { return F8 && HEAD == 0; }
 
 DEV int rot_ks(int ks, int rot, int ks1) {
   const int k = ks + rot;
@@ -242,7 +246,7 @@ DEV int step_src(const MlpArgs& a, int st, int q, int rot, int ks1) {
     }
     return a.off_w[C::L1] + (int)fm_frag(t, rot_ks(ks, rot, ks1), a.d_in[C::L1], 0);
   }
-  if (F8 && st < s_fc3) {   // the e4m3 fc2 stages: tile q >> 1, k-steps 4 (st - ns1) + 2 (q & 1) + {0, 1}
+  if (f8_fc2<HEAD, F8>() && st < s_fc3) {   // the e4m3 fc2 stage(s): tile q >> 1, k-steps 4 (st - ns1) + 2 (q & 1) + {0, 1}
     const int t = q >> 1;
     if (t == 7) return -1;
     return a.off_w[C::L2] + (int)fm_frag(t, 4 * (st - ns1) + 2 * (q & 1), a.d_in[C::L2], 0);
@@ -542,8 +546,8 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
     for (int u = 0; u < SPW; ++u) {
       const uint32_t code = ((u < 2 ? w01 : w23) >> (16 * (u & 1))) & 0xffffu;
-      // the e4m3 stages (fc1, fc2): two e4m3 fragments (512 B each) of a tile per slot
-      if (F8 && st < ns1 + fc2_stages<HEAD, F8>()) {
+      // the e4m3 stages (fc1; the policy's fc2): two e4m3 fragments (512 B each) of a tile per slot
+      if (F8 && st < ns1 + (f8_fc2<HEAD, F8>() ? fc2_stages<HEAD, F8>() : 0)) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rw8, stg + u * FB, 16, vw, code * 512u, 0, 0);
       } else {
 #pragma unroll
@@ -875,12 +879,11 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
     for (int t = 0; t < 8; ++t) acc2[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   int nst = 0;
-  if constexpr (F8) {
-    // e4m3 fc2: h1 (4 k-steps per stage, e4m3 x Q8_SH) x the e4m3 W2 image on the x128 MFMA — the
-    // policy's K = 128 in ONE stage, the value's 512 in 4; a stage's operand preparation (tanh, h1^T
-    // stores, transposes) precedes its wait, and issues beside the previous stage's MFMAs
-    // (+ the first wait: the policy's last fc1 stage's past-the-end X re-loads)
-    nst = HEAD == 0 ? 4 * XDMA : 0;
+  if constexpr (f8_fc2<HEAD, F8>()) {
+    // e4m3 fc2 of the policy: h1 (4 k-steps per stage, e4m3 x Q8_SH) x the e4m3 W2 image on the x128
+    // MFMA — K = 128 in ONE stage; the operand preparation (tanh, h1^T stores, transposes) precedes
+    // the wait (+ the first wait: the last fc1 stage's past-the-end X re-loads)
+    nst = 4 * XDMA;
     static_for<0, fc2_stages<HEAD, F8>()>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       __builtin_amdgcn_sched_barrier(0);
