@@ -1268,10 +1268,10 @@ def test_fp8_device_refresh_matches_torch_quantisation():
 
 
 def test_fp8_update_per_layer_error_and_shadow_image(monkeypatch):
-    """fp8 mode (BASELINE config 5) on the per-head path: the forward GEMMs of both heads run on the
-    e4m3 MFMA (csrc/mlp_head.hip F8: e4m3 weight image x e4m3-rounded observations / activations —
-    value fc1 on the 16x16x32 form, policy fc1, policy fc2 and value fc2 on the block-scaled 16x16x128
-    form), in the update and in values().  Per-layer relative error of the gradient vs fp32 autograd on the fp32 rows, the
+    """fp8 mode (BASELINE config 5) on the per-head path: forward GEMMs on the e4m3 MFMA
+    (csrc/mlp_head.hip F8: e4m3 weight image x e4m3-rounded observations / activations — the value
+    fc1 on the 16x16x32 form, the policy's fc1 and fc2 on the block-scaled 16x16x128 form), in the
+    update and in values().  Per-layer relative error of the gradient vs fp32 autograd on the fp32 rows, the
     value forward vs the fp32 model, and the shadow e4m3 image the Adam step refreshes (== torch's
     float8_e4m3fn rounding of p / qscale for the new parameters)."""
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=2048, exploration_size=2048 * 16,
@@ -1302,12 +1302,12 @@ def test_fp8_update_per_layer_error_and_shadow_image(monkeypatch):
         errs[name] = (eng.grad_flat[o:o + n] - g_ref[o:o + n]).norm().item() / (g_ref[o:o + n].norm().item() + 1e-12)
     print("fp8 value forward max rel err", verr, "per-layer gradient rel err", errs)
     assert verr < 0.05, verr
-    # (every forward GEMM of both heads on e4m3 since round 4 — policy fc1 + fc2, value fc1 + fc2 —
-    # measured on MI355X with the policy's two e4m3 GEMMs: p_fc1 14.3 %, p_fc2 15.7 %, mu 15.9 %; the
-    # value's fc1 alone: v_fc1 8.6 %, v_fc2 9.7 %, v 8.0 %.  e4m3's 3-bit mantissa on both operands of
-    # each GEMM, ~3.6 % RMS per rounding, compounds through the chain into a gradient that is mostly noise)
+    # (measured on MI355X with the policy's two e4m3 GEMMs: p_fc1 14.3 %, p_fc2 15.7 %, mu 15.9 %; the
+    # value's e4m3 fc1: v_fc1 8.6 %, v_fc2 9.7 %, v 8.0 % (profiles/r4/fp8_heads.md).  e4m3's 3-bit
+    # mantissa on both operands of each GEMM, ~3.6 % RMS per rounding, compounds through the chain into
+    # a gradient that is mostly noise)
     for name, e in errs.items():
-        assert e < (0.22 if name.startswith(("p_", "mu")) else 0.18), (name, e)
+        assert e < (0.22 if name.startswith(("p_", "mu")) else 0.12), (name, e)
     # the Adam step refreshes the e4m3 shadow image with the iteration's scales
     eng.apply()
     L = model.packed_layout()
