@@ -566,9 +566,35 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
 #pragma unroll
       for (int h = 0; h < H::NI; ++h) glds16(xsrc[rb] + xo + 64 * h, d + rb * FB + 1024 * h);
   };
+  auto xaddr = [&](int ks, int rb) __attribute__((always_inline)) -> uint32_t {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(
+               xring + (ks & (XS - 1)) * (RB * FB) + rb * FB) + H::lane_off(lane);
+  };
+  // the observation fragments of two k-steps (row block 0) behind ONE wait (the policy's fc1 stage)
+  auto read_x2 = [&](int ka, int kb, Frag& fa, Frag& fb) __attribute__((always_inline)) {
+    const uint32_t aa = xaddr(ka, 0), ab = xaddr(kb, 0);
+    if constexpr (DT == DT_S3) {
+      bf16x8 h0, l0, h1, l1;
+      asm volatile(
+          "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:512\n\tds_read_b128 %2, %5\n\t"
+          "ds_read_b128 %3, %5 offset:512\n\ts_waitcnt lgkmcnt(0)"
+          : "=&v"(h0), "=&v"(l0), "=&v"(h1), "=&v"(l1)
+          : "v"(aa), "v"(ab)
+          : "memory");
+      fa = Frag{h0, l0};
+      fb = Frag{h1, l1};
+    } else {
+      bf16x8 h0, h1;
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(h0), "=&v"(h1)
+                   : "v"(aa), "v"(ab)
+                   : "memory");
+      fa = h0;
+      fb = h1;
+    }
+  };
   auto read_x = [&](int ks, int rb) __attribute__((always_inline)) {
-    const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(
-                              xring + (ks & (XS - 1)) * (RB * FB) + rb * FB) + H::lane_off(lane);
+    const uint32_t addr = xaddr(ks, rb);
     if constexpr (DT == DT_S3) {
       bf16x8 h, l;
       asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:512\n\ts_waitcnt lgkmcnt(0)"
@@ -801,21 +827,20 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
       const int ka = 2 * st, kb = 2 * st + 1;
       const bool two = kb < ks1;
       Frag xa[RB], xb[RB];
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        xa[rb] = read_x(ka, rb);
-        xb[rb] = read_x(kb, rb);
-      }
-      for_slots<DT, 0x7f7fu, 0, 16, 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      read_x2(ka, kb, xa[0], xb[0]);   // (RB == 1: static_assert above)
+      // an odd ks1's last stage: its second k-step is past the end — a zero operand instead of a
+      // branch around those MFMAs (a branch splits the stage's read / MFMA schedule in two)
+      if (!two) xb[0] = Frag{};
+      // (split-bf16: read groups of 2 fragments = 4 ds_read_b128, so two groups in flight stay within
+      // lgkmcnt's 15 and the compiler can wait for one group instead of lgkmcnt(0))
+      for_slots<DT, 0x7f7fu, 0, 16, DT == DT_S3 ? 2 : 4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
         constexpr int q = decltype(qc)::value;
         if constexpr (q < 8) {
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb) acc1[rb][q] = hmma<DT>(acc1[rb][q], xa[rb], b);
         } else {
-          if (two) {
 #pragma unroll
-            for (int rb = 0; rb < RB; ++rb) acc1[rb][q - 8] = hmma<DT>(acc1[rb][q - 8], xb[rb], b);
-          }
+          for (int rb = 0; rb < RB; ++rb) acc1[rb][q - 8] = hmma<DT>(acc1[rb][q - 8], xb[rb], b);
         }
       }, flush);
       if (want_xT) {
