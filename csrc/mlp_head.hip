@@ -1,6 +1,6 @@
 // Per-head, row-stationary, weight-streaming fused PPO update, in split-bf16 (bf16x3, the
-// fp32-accurate headline precision) and bf16 (BASELINE configs 2 and 5: the fp8 mode's update
-// runs in bf16).  SURVEY K4, K5, K8, K10, K11; loss = corrected ppo.py:148-167 or the reference
+// fp32-accurate headline precision) and bf16 (BASELINE config 2; config 5's fp8 mode runs the bf16
+// kernels with e4m3 forward GEMMs — value fc1, policy fc1 + fc2 — and e4m3 wgrad operands).  SURVEY K4, K5, K8, K10, K11; loss = corrected ppo.py:148-167 or the reference
 // DPPO loss train.py:142-161; the backward of model.py:35-45 through one head.
 //
 // The actor-critic's two heads share only their input rows: the policy loss (clip + entropy,
