@@ -44,7 +44,10 @@ constexpr int NSLOT = 16;                   // fragments per ring stage
 constexpr int SST = 36, TILE_F = 16 * SST;  // [16][SST] fp32 transpose tile (conflict-free)
 constexpr int MAX_STEPS = 64;
 #ifndef HD_G1
-#define HD_G1 4   // value fc1: fragments per LDS read group (A/B: -DHD_G1=2 / 8)
+// value fc1: fragments per LDS read group.  2: bf16 2.320 vs 2.345 ms, bf16x3 4.258 vs 4.264 ms per
+// iteration against 4 (same box, profiles/r4/ab_value_fc1_g2/; split-bf16 groups of 4 put 16 reads in
+// flight, past lgkmcnt's 15)
+#define HD_G1 2
 #endif
 
 typedef __attribute__((ext_vector_type(8))) float f32x8;
