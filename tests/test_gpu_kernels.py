@@ -1007,6 +1007,9 @@ def test_wgrad_fused_reduction_bit_identical(dtype, monkeypatch):
         return (w.model.flat.data.clone(), e.adam_m.clone(), e.adam_v.clone(), e.wimg.view(torch.uint8).clone(),
                 img8, e.grad_flat.clone(), ms[-1])
 
+    # (the default "auto" is the separate launch: the fused tail measured 8-13 % slower per
+    # iteration, profiles/r4/ab_wgrad_gather.md)
+    assert not DPPOWorker(dppo_preset(**common), DistContext(device=DEV)).engine.wgrad_fused
     outs = []
     for mode in ("fused", "separate"):
         w = DPPOWorker(dppo_preset(**common, wgrad_gather=mode), DistContext(device=DEV))
