@@ -145,13 +145,13 @@ template <> struct HeadCfg<1> {   // value: v_fc1 -> v_fc2 -> v
 // F8 (fp8 mode, bf16 update): the forward GEMMs read the e4m3 weight image (the Adam step's shadow,
 // csrc/adam_core.h f8_put; W / qscale[layer]).  A 1 KiB ring slot holds one tile's e4m3 fragments of
 // two consecutive k-steps, so the stream and its LDS reads are half the bf16 bytes.
-//  * value head: fc1 on v_mfma_f32_16x16x32_fp8_fp8 with e4m3-rounded observations (2 stages of 16
-//    tiles per k-step pair);
+//  * value head: fc1 on v_mfma_f32_16x16x32_fp8_fp8 with e4m3-rounded observations x Q8_SX (2 stages
+//    of 16 tiles per k-step pair);
 //  * policy head: fc1 AND fc2 on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (twice the bf16
 //    MFMA rate): a stage holds 4 k-steps of the 8 tiles (slots 2t, 2t + 1), the A operand is the
-//    lane's 8 e4m3 bytes of each of the 4 k-steps (observations unscaled, h1 x Q8_SH), the same k
+//    lane's 8 e4m3 bytes of each of the 4 k-steps (observations x Q8_SX, h1 x Q8_SH), the same k
 //    order as the weight pieces, so the 128-term sum covers every k once (E8M0 scales 1; the epilogue
-//    multiplies by qscale, / Q8_SH for fc2).  fc1: ks1 / 4 stages, fc2: ONE stage (K = 128).
+//    multiplies by qscale / the activation scale).  fc1: ks1 / 4 stages, fc2: ONE stage (K = 128).
 template <int DT, int HEAD, bool F8 = false>
 constexpr int head_stages() { return DT == DT_S3 ? HeadCfg<HEAD>::S3 : (F8 ? 4 : HeadCfg<HEAD>::SBF); }
 // X ring slots (k-steps), a power of two.  An observation DMA must be OLDER than the weight batch
