@@ -43,6 +43,9 @@ constexpr int ROWS = 128;                   // rows per workgroup (both heads)
 constexpr int NSLOT = 16;                   // fragments per ring stage
 constexpr int SST = 36, TILE_F = 16 * SST;  // [16][SST] fp32 transpose tile (conflict-free)
 constexpr int MAX_STEPS = 64;
+#ifndef HD_VPM
+#define HD_VPM 3  // fc2: VALU instructions the scheduler may place after each MFMA (mma_mix; A/B -DHD_VPM=n)
+#endif
 #ifndef HD_G1
 // value fc1: fragments per LDS read group.  2: bf16 2.320 vs 2.345 ms, bf16x3 4.258 vs 4.264 ms per
 // iteration against 4 (same box, profiles/r4/ab_value_fc1_g2/; split-bf16 groups of 4 put 16 reads in
@@ -946,7 +949,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     stg = wait_step(nst);
     // k-step 2j's MFMAs with k-step 2j+1's operand preparation in their shadow, then k-step
     // 2j+1's with 2j+2's
-    mma_mix<DT, 0x7fu, 0, 8, 7 * RB * MPP, 3>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    mma_mix<DT, 0x7fu, 0, 8, 7 * RB * MPP, HD_VPM>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int t = decltype(qc)::value;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = hmma<DT>(acc2[rb][t], a0[rb], b);
@@ -954,7 +957,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     prep_b(a1);
     nst = NSTA;
     if constexpr (2 * j + 2 < C::K2) {
-      mma_mix<DT, 0x7f00u, 8, 16, 7 * RB * MPP, 3>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      mma_mix<DT, 0x7f00u, 8, 16, 7 * RB * MPP, HD_VPM>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
         constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = hmma<DT>(acc2[rb][t], a1[rb], b);
