@@ -43,8 +43,14 @@ constexpr int ROWS = 128;                   // rows per workgroup (both heads)
 constexpr int NSLOT = 16;                   // fragments per ring stage
 constexpr int SST = 36, TILE_F = 16 * SST;  // [16][SST] fp32 transpose tile (conflict-free)
 constexpr int MAX_STEPS = 64;
-#ifndef HD_VPM
-#define HD_VPM 3  // fc2: VALU instructions the scheduler may place after each MFMA (mma_mix; A/B -DHD_VPM=n)
+// fc2: VALU instructions the scheduler may place after each MFMA (mma_mix).  Same-box A/B
+// (profiles/r4/ab_fc2_vpm/): split-bf16 3 (4.118 ms) vs 2 (4.187) vs 6 (4.156); bf16 2 (2.239) vs 3
+// (2.259) vs 6 (2.257) — the bf16 MFMA chain is a third as long, so fewer fillers per MFMA fit
+#ifndef HD_VPM_S3
+#define HD_VPM_S3 3
+#endif
+#ifndef HD_VPM_BF16
+#define HD_VPM_BF16 2
 #endif
 #ifndef HD_G1
 // value fc1: fragments per LDS read group.  2: bf16 2.320 vs 2.345 ms, bf16x3 4.258 vs 4.264 ms per
@@ -457,6 +463,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   constexpr int TPR = 64 / WROWS;                     // loss lanes per row
   constexpr int WS_F = ws_floats<DT, HEAD, F8>();
   constexpr int MPP = DT == DT_S3 ? 3 : 1;            // MFMAs per fragment product
+  constexpr int VPM = DT == DT_S3 ? HD_VPM_S3 : HD_VPM_BF16;
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -949,7 +956,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     stg = wait_step(nst);
     // k-step 2j's MFMAs with k-step 2j+1's operand preparation in their shadow, then k-step
     // 2j+1's with 2j+2's
-    mma_mix<DT, 0x7fu, 0, 8, 7 * RB * MPP, HD_VPM>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+    mma_mix<DT, 0x7fu, 0, 8, 7 * RB * MPP, VPM>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int t = decltype(qc)::value;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = hmma<DT>(acc2[rb][t], a0[rb], b);
@@ -957,7 +964,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     prep_b(a1);
     nst = NSTA;
     if constexpr (2 * j + 2 < C::K2) {
-      mma_mix<DT, 0x7f00u, 8, 16, 7 * RB * MPP, HD_VPM>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
+      mma_mix<DT, 0x7f00u, 8, 16, 7 * RB * MPP, VPM>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
         constexpr int t = decltype(qc)::value - 8;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc2[rb][t] = hmma<DT>(acc2[rb][t], a1[rb], b);
