@@ -52,6 +52,9 @@ constexpr int MAX_STEPS = 64;
 #ifndef HD_VPM_BF16
 #define HD_VPM_BF16 2
 #endif
+#ifndef HD_G4_BF16
+#define HD_G4_BF16 4   // bf16 dgrad fc2: fragments per LDS read group (A/B: -DHD_G4_BF16=2)
+#endif
 #ifndef HD_G1
 // value fc1: fragments per LDS read group.  2: bf16 2.320 vs 2.345 ms, bf16x3 4.258 vs 4.264 ms per
 // iteration against 4 (same box, profiles/r4/ab_value_fc1_g2/; split-bf16 groups of 4 put 16 reads in
@@ -1296,7 +1299,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     constexpr unsigned M4 = (4 * s + 3 < C::N1R) ? 0xffffu : ((1u << (4 * ((C::N1R - 4 * s) & 3))) - 1u);
     // (fragment reads in groups of 2 where the registers are tight: split-bf16, and the value
     // head with the e4m3 operand stores' scales / maxima)
-    constexpr int G4 = (DT == DT_S3 || (Q8 && HEAD == 1)) ? 2 : 4;
+    constexpr int G4 = (DT == DT_S3 || (Q8 && HEAD == 1)) ? 2 : HD_G4_BF16;
     for_slots<DT, M4, 0, 16, G4>(stg, lane, [&](auto qc, const Frag& b) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
 #pragma unroll
