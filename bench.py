@@ -113,8 +113,9 @@ def main():
                     help="comma list of extra dtypes timed after the headline on the same config "
                          "(reported under 'variants'; '' = none)")
     ap.add_argument("--batch-size", type=int, default=0, help="0 = full buffer (reference DPPO)")
-    ap.add_argument("--overlap-rollout", action="store_true",
-                    help="the last value-head all-reduce + Adam overlap the next rollout (exact: the rollout reads only the policy)")
+    ap.add_argument("--overlap-rollout", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
+                    help="the last value-head all-reduce + Adam overlap the next rollout on a side stream (exact: "
+                         "the rollout reads only the policy); auto = on when the world has more than one rank")
     ap.add_argument("--force-collectives", action="store_true",
                     help="diagnostics: run the hot-path RCCL collectives even at world size 1")
     ap.add_argument("--phase-timing", type=int, default=0,
@@ -130,8 +131,6 @@ def main():
     ap.add_argument("--dist-timeout-s", type=float, default=300.0,
                     help="bound of every wait on peers (collective watchdog; abort + non-zero exit)")
     ap.add_argument("--heartbeat-timeout-s", type=float, default=60.0)
-    ap.add_argument("--wgrad-gather", default="auto", choices=["auto", "fused", "separate"],
-                    help="the split-K slab reduction + Adam in the wgrad launch's tail (fused) or a launch after it")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -142,6 +141,9 @@ def main():
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     check_world(args.gpus, args.dist_backend)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # the north-star configuration at N > 1: the last epoch's value all-reduce + Adam beside the
+    # next rollout (bit-identical to stream order: test_head_chains_through_rccl_bit_identical_to_fused)
+    args.overlap_rollout = args.overlap_rollout == "on" or (args.overlap_rollout == "auto" and world > 1)
     if world > 1:
         ctx = init_distributed("gpu", timeout_s=args.dist_timeout_s, backend=args.dist_backend,
                                grad_comm=args.grad_comm)
@@ -161,7 +163,7 @@ def main():
                         batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=dtype,
                         num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
                         dist_backend=args.dist_backend, grad_comm=args.grad_comm,
-                        dist_timeout_s=args.dist_timeout_s, wgrad_gather=args.wgrad_gather,
+                        dist_timeout_s=args.dist_timeout_s,
                         phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
         w = DPPOWorker(p, ctx)
         m = {}
@@ -201,7 +203,6 @@ def main():
     total_steps = rows * ctx.world_size * args.steps
     value = total_steps / elapsed
     heads = bool(getattr(w.engine, "heads", False))
-    wgrad_gather = "fused" if getattr(w.engine, "wgrad_fused", False) else "separate"
     # the gradient all-reduce in use: native RCCL on the compute stream (csrc/comm.cpp), the gloo
     # adapter of the same in-stream engine branch, the process group's (per-head chains), or none
     # (world size 1, not forced)
@@ -231,7 +232,7 @@ def main():
                                               and ctx.backend == "nccl" else 0),
                           "rollout_len": T, "num_epoch": args.num_epoch,
                           "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout,
-                          "per_head_kernels": heads, "grad_allreduce": grad_ar, "wgrad_gather": wgrad_gather,
+                          "per_head_kernels": heads, "grad_allreduce": grad_ar,
                           # --overlap-rollout on the in-stream path: the last value-head all-reduce +
                           # Adam run on a side stream (second communicator) beside the next rollout
                           "overlap_value_step": ("side_stream" if args.overlap_rollout and ctx.native_side is not None

@@ -329,12 +329,15 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   check(actions, "actions", at::kFloat, A);
   const int64_t nrows = actions.numel() / A;
   MlpArgs a = base_mlp((int)dt, L, scales, x_buf, idx, row0, M, wimg, flat, A, check_idx, nrows);
-  TORCH_CHECK(opts.size() == 5 || opts.size() == 7,
-              "opts: loss_kind, value_loss, std_var, first_step, npart[, head, part_dw]");
+  TORCH_CHECK(opts.size() == 5 || opts.size() == 7 || opts.size() == 8,
+              "opts: loss_kind, value_loss, std_var, first_step, npart[, head, part_dw[, vhead]]");
   // head >= 0: one head's per-head streaming kernel (csrc/mlp_head.hip; 0 policy, 1 value) with
   // its fused narrow-layer weight gradient at partial column part_dw (policy [32][128], value [128])
-  const int head = opts.size() == 7 ? (int)opts[5] : -1;
-  const int part_dw = opts.size() == 7 ? (int)opts[6] : 0;
+  const int head = opts.size() >= 7 ? (int)opts[5] : -1;
+  const int part_dw = opts.size() >= 7 ? (int)opts[6] : 0;
+  // vhead (head 1): the transposed-chain 32x32 value head (csrc/vhead.hip), which writes h1v / g1v /
+  // g2v ROW-MAJOR ([ldT][512] / [ldT][512] / [ldT][128]): the engine's wgrad must read them so
+  const bool vhead = opts.size() == 8 && opts[7] != 0;
   TORCH_CHECK(head >= -1 && head <= 1, "head: -1 (both heads, one kernel), 0 policy, 1 value");
   TORCH_CHECK(fopts.size() == 2, "fopts: clip, ent_coeff");
   TORCH_CHECK(tbufs.size() == 11, "11 transposed buffers");
@@ -405,12 +408,25 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   a.part = part.data_ptr<float>();
   TORCH_CHECK(!(w8.defined() && w8.numel() > 0) || (dt == 1 && head >= 0), "w8: the fp8 mode's per-head bf16 update only");
   set_w8(a, w8, qscale, L);
-  if (head >= 0) {
+  if (vhead) {
+    TORCH_CHECK(head == 1 && !q8 && a.W8 == nullptr && vhead_shape_ok(a), "vhead: the value head at bf16x3 / bf16");
+    TORCH_CHECK(ldT * 512 * (dt == 3 ? 4 : 2) < (int64_t(1) << 31), "vhead: row-major operands beyond 2 GiB");
+    TORCH_CHECK(ldT % vhead_rows() == 0 && Mpad <= ldT, "vhead: ldT covers whole workgroups");
+    launch_vhead_train((int)dt, a, cur_stream());
+  } else if (head >= 0) {
     launch_mlp_head((int)dt, (int)head, a, cur_stream());
   } else {
     launch_mlp_train((int)dt, a, cur_stream());
   }
   after_launch(__func__);
+}
+
+// the transposed-chain value head covers this (dtype, network)
+bool vhead_train_applies(int64_t dt, std::vector<int64_t> layout) {
+  const Layout L = parse_layout(layout);
+  MlpArgs a{};
+  for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
+  return (dt == 3 || dt == 1) && vhead_shape_ok(a) != 0;
 }
 
 // the per-head kernels cover this (dtype, network); x_bytes is irrelevant to them (64-bit rows)
@@ -455,7 +471,7 @@ F8Shadow f8_shadow(torch::Tensor img, torch::Tensor lid, torch::Tensor qs, int64
 WgradArgs wgrad_args(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor> xT,
                      std::vector<int64_t> g_rows, std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks,
                      torch::Tensor tasks_host, torch::Tensor slab, torch::Tensor q8_amax, int64_t q8_step,
-                     std::vector<int64_t> q8_t, std::vector<double> q8_xs) {
+                     std::vector<int64_t> q8_t, std::vector<double> q8_xs, std::vector<int64_t> rm) {
   const int wmax = 8, smax = 6;   // quadrants per task: one per wave of the 8-wave workgroup
   TORCH_CHECK(gT.size() == 6 && xT.size() == 6 && g_rows.size() == 6 && x_rows.size() == 6, "6 layers");
   check(tasks, "tasks", at::kInt, WGRAD_TASK_INTS);
@@ -489,6 +505,16 @@ WgradArgs wgrad_args(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torc
     a.xT[i] = xT[i].data_ptr();
   }
   a.ld = (int)ld;
+  // rm: 12 flags (dY side of layers 0-5, then X side): row-major operands of row length g_rows /
+  // x_rows (csrc/vhead.hip); split-bf16 / bf16 only, 64-feature quadrants inside the row
+  TORCH_CHECK(rm.empty() || rm.size() == 12, "rm: 12 row-major flags");
+  for (size_t i = 0; i < rm.size(); ++i) {
+    if (!rm[i]) continue;
+    TORCH_CHECK(dt == 1 || dt == 3, "row-major wgrad operands: split-bf16 / bf16 only");
+    const int64_t len = i < 6 ? g_rows[i] : x_rows[i - 6];
+    TORCH_CHECK(len % 64 == 0 && ld * len * (dt == 3 ? 4 : 2) < (int64_t(1) << 40), "row-major operand rows");
+    (i < 6 ? a.g_rm[i] : a.x_rm[i - 6]) = (int)len;
+  }
   a.tasks = reinterpret_cast<const WgradTask*>(tasks.data_ptr<int>());
   a.ntasks = ntasks;
   a.slab = slab.data_ptr<float>();
@@ -509,110 +535,10 @@ WgradArgs wgrad_args(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torc
 
 void wgrad(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor> xT, std::vector<int64_t> g_rows,
            std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host, torch::Tensor slab,
-           torch::Tensor q8_amax, int64_t q8_step, std::vector<int64_t> q8_t, std::vector<double> q8_xs) {
-  const WgradArgs a = wgrad_args(dt, gT, xT, g_rows, x_rows, ld, tasks, tasks_host, slab, q8_amax, q8_step, q8_t, q8_xs);
+           torch::Tensor q8_amax, int64_t q8_step, std::vector<int64_t> q8_t, std::vector<double> q8_xs,
+           std::vector<int64_t> rm) {
+  const WgradArgs a = wgrad_args(dt, gT, xT, g_rows, x_rows, ld, tasks, tasks_host, slab, q8_amax, q8_step, q8_t, q8_xs, rm);
   launch_wgrad((int)dt, a, cur_stream());
-  after_launch(__func__);
-}
-
-// The wgrad launch with the split-K slab reduction in its tail (csrc/kernels.h WgradFix): mode 1
-// = wgrad + grad_gather (the gradient into g), mode 2 = wgrad + gather_adam (world size 1) — the
-// same sums in the same order, bit-identical to the two-launch forms.  fix: per task [tile, nch,
-// e_lo, e_hi] (int32, device) with its CPU mirror fix_host (validated here against the task list,
-// elems and the flat range); sync: 2 int32 per tile, zero; err: one int32.
-void wgrad_fused(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torch::Tensor> xT, std::vector<int64_t> g_rows,
-                 std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks, torch::Tensor tasks_host,
-                 torch::Tensor slab, torch::Tensor q8_amax, int64_t q8_step, std::vector<int64_t> q8_t,
-                 std::vector<double> q8_xs, int64_t mode, torch::Tensor fix, torch::Tensor fix_host, torch::Tensor elems,
-                 torch::Tensor sync, torch::Tensor err, torch::Tensor src_off, torch::Tensor src_meta, torch::Tensor part,
-                 int64_t npblk, int64_t npart, torch::Tensor red_col, torch::Tensor red_dst, double scale,
-                 torch::Tensor loss_out, torch::Tensor g, torch::Tensor p, torch::Tensor m, torch::Tensor v, double lr,
-                 double b1, double b2, double eps, int64_t step, torch::Tensor state, torch::Tensor norm_part,
-                 torch::Tensor wimg, torch::Tensor w_map, torch::Tensor wt_map, int64_t img_dt, torch::Tensor qmul,
-                 torch::Tensor f8_img, torch::Tensor f8_lid, torch::Tensor f8_qs) {
-  WgradArgs a = wgrad_args(dt, gT, xT, g_rows, x_rows, ld, tasks, tasks_host, slab, q8_amax, q8_step, q8_t, q8_xs);
-  TORCH_CHECK(mode == 1 || mode == 2, "mode: 1 gather, 2 gather + Adam");
-  const int64_t n = g.numel();
-  const int ntasks = a.ntasks;
-  check(fix, "fix", at::kInt, 4 * (int64_t)ntasks);
-  TORCH_CHECK(!fix_host.is_cuda() && fix_host.numel() == 4 * (int64_t)ntasks && fix_host.scalar_type() == at::kInt,
-              "fix_host must mirror fix on the CPU");
-  const int64_t ne = elems.numel();
-  check(elems, "elems", at::kInt, ne);
-  check(err, "err", at::kInt, 1);
-  const int64_t nsync = sync.numel();
-  check(sync, "sync", at::kInt, nsync);
-  {
-    // every task: a tile with a sync slot, a share inside elems; the tiles' task counts add up
-    auto fh = fix_host.contiguous();
-    const int* fp = fh.data_ptr<int>();
-    std::vector<int> seen(nsync / 2, 0), want(nsync / 2, -1);
-    for (int t = 0; t < ntasks; ++t) {
-      const int tile = fp[4 * t], nch = fp[4 * t + 1], lo = fp[4 * t + 2], hi = fp[4 * t + 3];
-      TORCH_CHECK(tile >= 0 && 2 * (int64_t)tile + 1 < nsync, "fix: tile without a sync slot");
-      TORCH_CHECK(nch >= 1 && (want[tile] < 0 || want[tile] == nch), "fix: chunk count of a tile");
-      TORCH_CHECK(0 <= lo && lo <= hi && hi <= ne, "fix: share outside elems");
-      want[tile] = nch;
-      ++seen[tile];
-    }
-    for (size_t k = 0; k < seen.size(); ++k)
-      TORCH_CHECK(seen[k] == 0 || seen[k] == want[k], "fix: a tile's task count differs from its chunk count");
-  }
-  check(g, "g", at::kFloat, n);
-  check(src_off, "src_off", at::kInt, n);
-  check(src_meta, "src_meta", at::kInt, n);
-  check(part, "part", at::kFloat, npblk * npart);
-  check(loss_out, "loss_out", at::kFloat, 8);
-  const int64_t nitems = red_col.numel();
-  check(red_col, "red_col", at::kInt, nitems);
-  check(red_dst, "red_dst", at::kInt, nitems);
-  TORCH_CHECK(item_blocks((int)nitems) <= ntasks, "more reduce-item blocks than tasks");
-  WgradFix& f = a.fx;
-  f.mode = (int)mode;
-  f.sync = sync.data_ptr<int>();
-  f.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
-  f.ftask = fix.data_ptr<int>();
-  f.elems = elems.data_ptr<int>();
-  f.src_off = src_off.data_ptr<int>();
-  f.src_meta = src_meta.data_ptr<int>();
-  f.scale = (float)scale;
-  f.g = g.data_ptr<float>();
-  f.part = part.data_ptr<float>();
-  f.npblk = (int)npblk;
-  f.npart = (int)npart;
-  f.nitems = (int)nitems;
-  f.red_col = red_col.data_ptr<int>();
-  f.red_dst = red_dst.data_ptr<int>();
-  f.loss_out = loss_out.data_ptr<float>();
-  f.f8 = F8Shadow{nullptr, nullptr, nullptr};
-  if (mode == 2) {
-    check(p, "p", at::kFloat, n);
-    check(m, "m", at::kFloat, n);
-    check(v, "v", at::kFloat, n);
-    check(state, "state", at::kFloat, 4);
-    check(w_map, "w_map", at::kInt, n);
-    check(wt_map, "wt_map", at::kInt, n);
-    check(wimg, "wimg", storage_type((int)img_dt), 1);
-    TORCH_CHECK(step >= 1, "the host step number");
-    check(norm_part, "norm_part", at::kFloat, item_blocks((int)nitems) + (int64_t)ntasks);
-    f.p = p.data_ptr<float>();
-    f.m = m.data_ptr<float>();
-    f.v = v.data_ptr<float>();
-    f.lr = (float)lr;
-    f.b1 = (float)b1;
-    f.b2 = (float)b2;
-    f.eps = (float)eps;
-    f.step = (float)step;
-    f.state = state.data_ptr<float>();
-    f.norm_part = norm_part.data_ptr<float>();
-    f.wimg = wimg.data_ptr();
-    f.w_map = w_map.data_ptr<int>();
-    f.wt_map = wt_map.data_ptr<int>();
-    f.qmul = nullptr;
-    if (qmul.defined() && qmul.numel() > 0) { check(qmul, "qmul", at::kFloat, n); f.qmul = qmul.data_ptr<float>(); }
-    f.f8 = f8_shadow(f8_img, f8_lid, f8_qs, n);
-  }
-  launch_wgrad_fused((int)dt, (int)img_dt, a, cur_stream());
   after_launch(__func__);
 }
 
@@ -882,7 +808,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_value", &mlp_value);
   m.def("mlp_train", &mlp_train);
   m.def("head_applies", &head_applies);
+  m.def("vhead_train_applies", &vhead_train_applies);
   m.def("head_rows", []() { return (int64_t)mlp_head_rows(); });
+  m.def("set_vhead", [](int64_t on) { set_vhead((int)on); });
   m.def("head_waves", [](int64_t h) { return (int64_t)mlp_head_waves((int)h); });
   m.def("set_head_kernels", [](bool on) { set_head_kernels(on ? 1 : 0); });
   m.def("head_kernels_enabled", []() { return head_kernels_enabled() != 0; });
@@ -906,8 +834,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_train_tstamp", &set_train_tstamp);
   m.def("set_rollout_tstamp", &set_rollout_tstamp);
   m.def("wgrad", &wgrad);
-  m.def("wgrad_fused", &wgrad_fused);
-  m.def("wgrad_fused_cap", [](int64_t dt) { return (int64_t)wgrad_fused_cap((int)dt); });
   m.def("grad_gather", &grad_gather);
   m.def("gae", &gae);
   m.def("set_adam_fused", [](int64_t on) { set_adam_fused((int)on); });

@@ -19,28 +19,14 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
 #define DEV __device__ __forceinline__
 typedef __attribute__((ext_vector_type(8))) float f32x8v;
-// Elementwise fp32 vector arithmetic of the MFMA epilogues / operand splits.  Plain vector ops lower
-// to packed v_pk_{add,mul,fma}_f32, which beside MFMAs cost more than the two scalar ops they replace
-// (MI355X_MICROARCH.md, 'price of one filler beside MFMAs'); DPPO_NOPK (A/B, with -fno-slp-vectorize
-// so the SLP pass does not re-pack them) spells them as scalar ops.
-#ifdef DPPO_NOPK
-#define DPPO_EW(N, expr)                       \
-  do {                                         \
-    _Pragma("unroll") for (int i = 0; i < N; ++i) { expr; } \
-  } while (0)
-DEV f32x4 ew_sub(const f32x4& a, const f32x4& b) { f32x4 r; DPPO_EW(4, r[i] = a[i] - b[i]); return r; }
-DEV f32x8v ew_sub(const f32x8v& a, const f32x8v& b) { f32x8v r; DPPO_EW(8, r[i] = a[i] - b[i]); return r; }
-DEV f32x8v ew_add(const f32x8v& a, const f32x8v& b) { f32x8v r; DPPO_EW(8, r[i] = a[i] + b[i]); return r; }
-DEV f32x4 ew_mul(const f32x4& a, float s) { f32x4 r; DPPO_EW(4, r[i] = a[i] * s); return r; }
-// a * (1 - h * h) (the tanh derivative)
-DEV f32x4 ew_dtanh(const f32x4& a, const f32x4& h) { f32x4 r; DPPO_EW(4, r[i] = a[i] * __builtin_fmaf(-h[i], h[i], 1.0f)); return r; }
-#else
+// Elementwise fp32 vector arithmetic of the MFMA epilogues / operand splits (packed v_pk_* f32 ops;
+// scalar spellings measured mixed in round 4, profiles/r4/ab_nopk/)
 DEV f32x4 ew_sub(const f32x4& a, const f32x4& b) { return a - b; }
 DEV f32x8v ew_sub(const f32x8v& a, const f32x8v& b) { return a - b; }
 DEV f32x8v ew_add(const f32x8v& a, const f32x8v& b) { return a + b; }
 DEV f32x4 ew_mul(const f32x4& a, float s) { return a * s; }
+// a * (1 - h * h) (the tanh derivative)
 DEV f32x4 ew_dtanh(const f32x4& a, const f32x4& h) { return a * (1.0f - h * h); }
-#endif
 
 enum { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2, DT_S3 = 3 };
 
@@ -171,15 +157,11 @@ __host__ __device__ inline size_t fm_frag(int rt, int ks, int cols, int lane) {
 }
 
 // Store of a wgrad operand (the feature-major activations / gradients the fused update writes
-// and the wgrad kernel reads back): non-temporal by default (streaming: keeps the weight images
-// in L2); DPPO_T_CACHED: plain stores (A/B of Infinity-Cache residency).
+// and the wgrad kernel reads back): non-temporal (streaming: keeps the weight images in L2; cached
+// stores measured neutral, round 2)
 template <typename V>
 DEV void opnd_store(const V& v, V* p) {
-#ifdef DPPO_T_CACHED
-  *p = v;
-#else
   __builtin_nontemporal_store(v, p);
-#endif
 }
 
 // ---- fp8 mode's e4m3 wgrad operands ("Q8", csrc/mlp_head.hip + csrc/wgrad.hip) ----

@@ -133,6 +133,13 @@ extern "C" void launch_mlp_head(int dt, int head, const MlpArgs& a, hipStream_t 
 extern "C" void launch_mlp_head_value(int dt, const MlpArgs& a, hipStream_t s);   // V(x) on the value head kernel
 extern "C" void set_head_kernels(int enable);
 extern "C" int head_kernels_enabled();
+// value head on 32x32x16 MFMAs, transposed chain (csrc/vhead.hip): 128 rows per workgroup
+extern "C" int vhead_applies(const MlpArgs& a);   // the forward (set_vhead flag and shapes)
+extern "C" int vhead_shape_ok(const MlpArgs& a);
+extern "C" void launch_vhead_train(int dt, const MlpArgs& a, hipStream_t s);   // the update chain
+extern "C" int vhead_rows();
+extern "C" void launch_vhead_fwd(int dt, const MlpArgs& a, hipStream_t s);   // V(x): dt bf16x3 or bf16
+extern "C" void set_vhead(int enable);
 
 // fp8 mode: the Adam kernels also refresh the e4m3 image the update's fc1 reads (csrc/mlp_head.hip
 // F8), element i as p / qs[lid[i]] with the iteration's per-layer scales; img == nullptr: off
@@ -172,40 +179,6 @@ struct WgradTask {
   int nq, kq;     // tile extent in 64x64 quadrants (one per wave): nq*kq <= 8, nq + kq <= 6
 };
 
-// The split-K slab reduction (+ the no-clip Adam step) fused into the wgrad launch's tail
-// (csrc/wgrad.hip wgrad_fixup; cooperative launch, every task co-resident): each task publishes
-// its chunk of its output tile, then — once all nch chunks of the tile are in — reduces its 1/nch
-// share of the tile's elements over the chunks in the fixed chunk order of grad_gather.  Items:
-// the reduce items (the head kernels' partial-row columns) of grad_gather, done by tasks
-// [0, item_blocks(nitems)) while they wait.  norm_part: [items' blocks | one per task].
-struct WgradFix {
-  int mode;                // 0 off, 1 gather into g, 2 gather + no-clip Adam (world size 1)
-  int* sync;               // [2 per tile]: arrivals, departures (zero between launches: self-resetting)
-  unsigned* err;           // set when a task timed out waiting for its tile's chunks
-  const int* ftask;        // per task: tile, nch, e_lo, e_hi (its share of elems)
-  const int* elems;        // flat indices of every tile's slab elements, tile by tile
-  const int* src_off;      // flat index -> chunk-0 slab offset / (nch * 16 + stride / 4096), as grad_gather
-  const int* src_meta;
-  float scale;
-  float* g;
-  const float* part;       // reduce items (grad_gather's)
-  int npblk, npart, nitems;
-  const int* red_col;
-  const int* red_dst;
-  float* loss_out;
-  float* p;                // mode 2: Adam (gather_adam's arguments)
-  float* m;
-  float* v;
-  float lr, b1, b2, eps, step;
-  float* state;
-  float* norm_part;
-  void* wimg;
-  const int* w_map;
-  const int* wt_map;
-  const float* qmul;
-  F8Shadow f8;
-};
-
 struct WgradArgs {
   const void* gT[6];   // dY^T per layer  [rows >= n tile][ld]
   const void* xT[6];   // X^T per layer   [rows >= k tile][ld]
@@ -219,7 +192,9 @@ struct WgradArgs {
   const unsigned* q8_rd;
   int q8_t[6];
   float q8_xs[6];
-  WgradFix fx;         // fx.mode 0: the slabs only (a grad_gather / gather_adam launch follows)
+  // row-major operands (csrc/vhead.hip: [ld rows][features]): the row length in elements of layer
+  // l's dY (g_rm) / X (x_rm) operand, 0 = fragment-major
+  int g_rm[6], x_rm[6];
 };
 
 extern "C" {
@@ -239,10 +214,6 @@ void set_s3_train_waves(int nw);                // split-bf16 32-row tile: 4 or 
 void set_s3_value_waves(int nw);                // split-bf16 value forward: 4 or 8 waves (A/B)
 int mlp_train_waves(int dt, const MlpArgs& a);  // workgroup waves the launcher will use
 void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
-// a.fx.mode != 0: cooperative launch with the fused slab reduction (img_dt: the weight image's
-// precision for mode 2); wgrad_fused_cap: the largest task count it accepts (0: none)
-void launch_wgrad_fused(int dt, int img_dt, const WgradArgs& a, hipStream_t s);
-int wgrad_fused_cap(int dt);
 // grad[i] for i in [i_lo, i_hi) from the slabs (src_off / src_meta: see grad_gather_kernel);
 // with_partials: also log_std grads [0, A) and the 8 loss sums from the per-workgroup partials
 void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part, int nblk,

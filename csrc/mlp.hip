@@ -627,6 +627,14 @@ void value_t(const MlpArgs& a, hipStream_t s);
 // 2.125 rounds, and the 32-workgroup third round costs as much as a full one.  Rows past the last
 // full round (when they are at most a quarter round) go to the 32-row tile kernel instead, whose
 // small workgroups spread over all CUs.
+// (the transposed-chain 32x32 value head, csrc/vhead.hip, takes the rows when it applies; the e4m3
+// fc1 of the fp8 mode stays on the head kernel)
+template <int DT>
+void head_fwd(const MlpArgs& a, hipStream_t s) {
+  if (a.W8 == nullptr && vhead_applies(a)) launch_vhead_fwd(DT, a, s);
+  else launch_mlp_head_value(DT, a, s);
+}
+
 template <int DT>
 void value_head_t(const MlpArgs& a, hipStream_t s) {
   const int round = mlp_head_rows() * cu_count();
@@ -634,7 +642,7 @@ void value_head_t(const MlpArgs& a, hipStream_t s) {
   if (full > 0 && full < a.M && a.M - full <= round / 4) {
     MlpArgs h = a;
     h.M = full;
-    launch_mlp_head_value(DT, h, s);
+    head_fwd<DT>(h, s);
     MlpArgs t = a;
     t.M = a.M - full;
     if (t.idx) t.idx += full;
@@ -643,7 +651,7 @@ void value_head_t(const MlpArgs& a, hipStream_t s) {
     value_t<DT>(t, s);   // (t.M < one round: takes the tile kernel below)
     return;
   }
-  launch_mlp_head_value(DT, a, s);
+  head_fwd<DT>(a, s);
 }
 
 template <int DT>

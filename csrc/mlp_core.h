@@ -50,12 +50,6 @@ DEV f32x4 act_tanh4(f32x4 x) {
   if constexpr (DT == DT_F32) {
     return f32x4{tanhf(x[0]), tanhf(x[1]), tanhf(x[2]), tanhf(x[3])};
   } else {
-#ifdef DPPO_NOPK
-    f32x4 r;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = act_tanh<DT>(x[i]);
-    return r;
-#else
     const f32x4 y = x * (2.0f * 1.4426950408889634f);
     f32x4 e;
 #pragma unroll
@@ -64,7 +58,6 @@ DEV f32x4 act_tanh4(f32x4 x) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_rcpf(e[i]);
     return __builtin_elementwise_fma(e, f32x4{-2.f, -2.f, -2.f, -2.f}, f32x4{1.f, 1.f, 1.f, 1.f});
-#endif
   }
 }
 
@@ -104,10 +97,8 @@ DEV void store4q_T(typename Prec<DT>::T* dst, const typename Prec<DT>::T (&q)[4]
 // register sets in the layer_gemm rotation (prefetch distance NB - 1 steps).  split-bf16 at 8
 // waves runs one k-step per chunk with VGPRs to spare, so it prefetches deeper: a step is only
 // 12 MFMAs there, far shorter than the L2 latency of the weight fragments it waits for.
-#ifndef DPPO_S3_NBUF
-#define DPPO_S3_NBUF 2
-#endif
-template <int DT, int NW> struct GemmDepth { static constexpr int NB = (IsSplit<DT>::value && NW == 8) ? DPPO_S3_NBUF : 2; };
+// (3 sets for split-bf16 at 8 waves measured neutral: profiles/r4/ab_rollout_nb3/)
+template <int DT, int NW> struct GemmDepth { static constexpr int NB = 2; };
 
 template <int DT, int RB> struct KChunk { static constexpr int KC = IsSplit<DT>::value ? 1 : 2; };
 

@@ -46,21 +46,12 @@ constexpr int MAX_STEPS = 64;
 // fc2: VALU instructions the scheduler may place after each MFMA (mma_mix).  Same-box A/B
 // (profiles/r4/ab_fc2_vpm/): split-bf16 3 (4.118 ms) vs 2 (4.187) vs 6 (4.156); bf16 2 (2.239) vs 3
 // (2.259) vs 6 (2.257) — the bf16 MFMA chain is a third as long, so fewer fillers per MFMA fit
-#ifndef HD_VPM_S3
-#define HD_VPM_S3 3
-#endif
-#ifndef HD_VPM_BF16
-#define HD_VPM_BF16 2
-#endif
-#ifndef HD_G4_BF16
-#define HD_G4_BF16 4   // bf16 dgrad fc2: fragments per LDS read group (A/B: -DHD_G4_BF16=2)
-#endif
-#ifndef HD_G1
+constexpr int HD_VPM_S3 = 3, HD_VPM_BF16 = 2;
+constexpr int HD_G4_BF16 = 4;   // bf16 dgrad fc2: fragments per LDS read group (groups of 2: no gain, r4)
 // value fc1: fragments per LDS read group.  2: bf16 2.320 vs 2.345 ms, bf16x3 4.258 vs 4.264 ms per
 // iteration against 4 (same box, profiles/r4/ab_value_fc1_g2/; split-bf16 groups of 4 put 16 reads in
 // flight, past lgkmcnt's 15)
-#define HD_G1 2
-#endif
+constexpr int HD_G1 = 2;
 
 typedef __attribute__((ext_vector_type(8))) float f32x8;
 typedef __attribute__((ext_vector_type(8))) int i32x8;
@@ -284,13 +275,9 @@ DEV int step_src(const MlpArgs& a, int st, int q, int rot, int ks1) {
   return a.off_wt[C::L2] + (int)fm_frag(t, ks, a.d_out[C::L2], 0);
 }
 
-// the head kernels' fragment product (ABLATION DPPO_ABL_MFMA1, timing only: split-bf16 products
-// as ONE MFMA, hi x hi — the operands are still read, a third of the matrix work is issued)
+// the head kernels' fragment product
 template <int DT>
 DEV f32x4 hmma(f32x4 c, const typename HT<DT>::Frag& a, const typename HT<DT>::Frag& b) {
-#ifdef DPPO_ABL_MFMA1
-  if constexpr (DT == DT_S3) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
-#endif
   return HT<DT>::P::mma(c, a, b);
 }
 
@@ -484,12 +471,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   float* mus = tpb;                        // (loss) mu [32][32] | v [32]
 
   auto src_of = [&](int r) __attribute__((always_inline)) {
-#ifdef DPPO_ABL_XL2
-    // ABLATION (timing only, wrong numerics): every workgroup reads the same 1,024 rows (L2-resident)
-    const int rr = (int)(blockIdx.x & 7) * ROWS + r;
-#else
     const int rr = (m0 + r < a.M) ? m0 + r : m0;   // rows past M re-read row m0 (zero gradient)
-#endif
     return a.idx ? a.idx[rr] : a.row0 + rr;
   };
   const int mw = m0 + WROWS * wave;
@@ -550,10 +532,6 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
   __amdgpu_buffer_rsrc_t rw8 = rw;
   if constexpr (F8) rw8 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W8), (short)0, 0x7fffffff, 0x00020000);
   auto issue = [&](int st, int stage) __attribute__((always_inline)) {
-#ifdef DPPO_ABL_NOWDMA
-    // ABLATION (timing only, wrong numerics): the ring keeps its primed fragments
-    if (st >= S - 1) return;
-#endif
     const int l = min(st, MAX_STEPS - 1);
     const uint32_t w01 = __builtin_amdgcn_readlane(cw0, l);
     const uint32_t w23 = SPW > 2 ? __builtin_amdgcn_readlane(cw1, l) : 0u;
@@ -654,9 +632,7 @@ __global__ __launch_bounds__(HeadCfg<HEAD>::NW * 64, 1) void mlp_head_kernel(Mlp
     for (int i = 0; i < NH - LEAD; ++i) extra += hist[i];
     wait_vm<GL * (S - 2 - LEAD)>(extra);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#ifndef DPPO_ABL_NOBAR
     __builtin_amdgcn_s_barrier();
-#endif
     asm volatile("" ::: "memory");
     const char* stg = ring + cst * SB;
     issue(cur + S - 1, cst == 0 ? S - 1 : cst - 1);

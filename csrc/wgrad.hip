@@ -11,7 +11,6 @@
 // 384 rows per step for 2x the outputs of a 128x128 tile's 256 (v_fc1: 2304 instead of 3072
 // rows per step).  Results go to per-chunk fp32 slabs ([nq*64][kq*64] per task) that
 // grad_gather sums in a fixed order — deterministic, no float atomics (SURVEY §7.4 part 2).
-#include "adam_core.h"
 #include "kernels.h"
 #include "mlp_core.h"
 
@@ -43,6 +42,35 @@ typedef __attribute__((ext_vector_type(8))) int i32x8;
 template <int DT, int S>
 constexpr size_t wgrad_lds_bytes() { return (size_t)S * WG_SLOTS * wgrad_frag_bytes<DT>(); }
 
+// the 16-byte chunk swizzle of a row-major operand image (128-byte rows): even XOR values keep the two
+// chunks of a 16-feature column group adjacent; rows r, r + 2, r + 8, r + 10 (the rows of a 32-lane
+// half's transposed reads that share banks) get distinct chunk pairs — conflict-free
+__host__ __device__ inline int wgrad_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
+
+// an MFMA operand (lane l: feature 16 s + (l & 15) of the quadrant, rows 8 (l >> 4) .. + 7) from a
+// row-major quadrant image at qb: two ds_read_b64_tr_b16 of 4 rows each (lane 4 q' + p' of a 16-lane
+// group addresses row q', columns 4 p' .. 4 p' + 3; lane i receives column i) per precision part
+template <int DT>
+DEV typename Prec<DT>::Frag rm_frag(const char* qb, int s, int lane) {
+  typedef __attribute__((ext_vector_type(4))) short s16x4;
+  const int li = lane & 15, g = lane >> 4;
+  auto rd = [&](const char* base, int sub) __attribute__((always_inline)) {
+    const int row = 8 * g + 4 * sub + (li >> 2), col = 16 * s + 4 * (li & 3);
+    const char* p = base + row * 128 + (((col >> 3) ^ wgrad_swz(row)) << 4) + (col & 7) * 2;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  };
+  auto cat = [&](s16x4 a0, s16x4 a1) __attribute__((always_inline)) {
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    const s16x8 v{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    return *reinterpret_cast<const bf16x8*>(&v);
+  };
+  if constexpr (IsSplit<DT>::value) {
+    return S3Frag{cat(rd(qb, 0), rd(qb, 1)), cat(rd(qb + 4096, 0), rd(qb + 4096, 1))};
+  } else {
+    return cat(rd(qb, 0), rd(qb, 1));
+  }
+}
+
 template <int DT, int S, int C>
 DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   using P = Prec<DT>;
@@ -60,14 +88,42 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   const int NF = 4 * tk.nq, F = NF + 4 * tk.kq;
   // slot f of a stage holds fragment f: f < NF -> dY^T row tile n0/16 + f, else X^T row tile
   // k0/16 + f - NF.  Wave w DMAs slots C*w .. C*w + C-1 (a slot >= F re-loads fragment f mod F).
-  const char* src[C];
+  // FM operands: a fragment is contiguous (FB bytes per k-step).  Row-major operands (RM: the
+  // transposed-chain value head's h1 / g1 / g2, csrc/vhead.hip; row length a.g_rm / a.x_rm): a
+  // quadrant's 4 slots hold its [32 rows][64 features] image per k-step (split: hi 4 KiB | lo 4 KiB),
+  // 128-byte rows with the 16-byte chunks XOR-swizzled by wgrad_swz(row), DMA'd row by row (8 rows
+  // per instruction) and read back transposed (ds_read_b64_tr_b16).
+  const char* srcp[C][NI];
+  size_t kstride[C];
   int dst[C];
 #pragma unroll
   for (int q = 0; q < C; ++q) {
     const int f = wave * C + q;
     const int ff = f < F ? f : f % F;   // dummy slot: re-load one of the task's fragments
-    src[q] = (ff < NF) ? g + fm_frag((tk.n0 >> 4) + ff, ks0, a.ld, 0) * sizeof(T)
-                       : x + fm_frag((tk.k0 >> 4) + ff - NF, ks0, a.ld, 0) * sizeof(T);
+    const bool gs = ff < NF;
+    const int fl = gs ? ff : ff - NF;
+    const int feat0 = (gs ? tk.n0 : tk.k0) + 16 * fl;
+    const int rm = (DT == DT_S3 || DT == DT_BF16) ? (gs ? a.g_rm[tk.layer] : a.x_rm[tk.layer]) : 0;
+    const char* ob = gs ? g : x;
+    if (rm == 0) {
+      const char* src = ob + fm_frag(feat0 >> 4, ks0, a.ld, 0) * sizeof(T);
+#pragma unroll
+      for (int hh = 0; hh < NI; ++hh)
+        srcp[q][hh] = src + (IsSplit<DT>::value ? (size_t)hh * 1024 + (lane & 31) * 32 + (lane >> 5) * 16
+                                                 : (size_t)hh * 1024 + lane * 16);
+      kstride[q] = FB;
+    } else {
+      const int sq = fl & 3, f0 = feat0 - 16 * sq;   // slot in the quadrant, the quadrant's first feature
+#pragma unroll
+      for (int hh = 0; hh < NI; ++hh) {
+        const int n = NI * sq + hh;                   // 1 KiB DMA instruction of the quadrant image
+        const int part = IsSplit<DT>::value ? n >> 2 : 0, rb = IsSplit<DT>::value ? (n & 3) : n;
+        const int row = 8 * rb + (lane >> 3);
+        const int c = (lane & 7) ^ wgrad_swz(row);
+        srcp[q][hh] = ob + ((size_t)(tk.m0 + row) * rm + f0 + 8 * c) * sizeof(T) + 16 * part;
+      }
+      kstride[q] = (size_t)32 * rm * sizeof(T);
+    }
     dst[q] = f * FB;
   }
   auto issue = [&](int k) {
@@ -76,17 +132,15 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
 #pragma unroll
     for (int q = 0; q < C; ++q)
 #pragma unroll
-      for (int h = 0; h < NI; ++h) {
-        const size_t go = IsSplit<DT>::value ? (size_t)h * 1024 + (lane & 31) * 32 + (lane >> 5) * 16
-                                             : (size_t)h * 1024 + lane * 16;
-        glds16(src[q] + (size_t)kk * FB + go, st + dst[q] + h * 1024);
-      }
+      for (int h = 0; h < NI; ++h) glds16(srcp[q][h] + (size_t)kk * kstride[q], st + dst[q] + h * 1024);
   };
   // Q8: this lane's sub-slot maximum of the layer's gradient tensor, loaded before any DMA (the
   // oldest vector-memory op: it never holds up a counted wait), folded in the epilogue
   uint32_t q8v = 0;
   if constexpr (DT == DT_FP8) q8v = a.q8_rd[(a.q8_t[tk.layer] * Q8_SUB + lane) * Q8_LINE];
   const bool active = wave < tk.nq * tk.kq;
+  constexpr bool RMOK = DT == DT_S3 || DT == DT_BF16;   // (fp32 / e4m3 operands are fragment-major only)
+  const bool g_rm = RMOK && a.g_rm[tk.layer] != 0, x_rm = RMOK && a.x_rm[tk.layer] != 0;
   const int wn = wave / tk.kq, wk = wave - (wave / tk.kq) * tk.kq;
   f32x4 acc[4][4];
 #pragma unroll
@@ -132,7 +186,9 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
             acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8[i], b8[j], acc[i][j], 0, 0, 0, 127, 0, 127);
         continue;
       }
-      auto lds_frag = [&](int f) {
+      auto lds_frag = [&](int f, bool rm) {
+        if constexpr (DT == DT_S3 || DT == DT_BF16)
+          if (rm) return rm_frag<DT>(st + (f & ~3) * FB, f & 3, lane);
         if constexpr (IsSplit<DT>::value) {
           const char* b = st + f * FB + (lane >> 5) * 1024 + (lane & 31) * 16;
           return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + 512)};
@@ -142,8 +198,8 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
       };
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        af[i] = lds_frag(wn * 4 + i);
-        bf[i] = lds_frag(NF + wk * 4 + i);
+        af[i] = lds_frag(wn * 4 + i, g_rm);
+        bf[i] = lds_frag(NF + wk * 4 + i, x_rm);
       }
       if constexpr (LATE) issue(k + S - 1);
 #pragma unroll
@@ -173,155 +229,12 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
       for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * KE + col + 16 * j] = acc[i][j][q];
 }
 
-// ---- the fused split-K reduction (WgradFix, a.fx.mode != 0) ----
-// A stream-K style fix-up in the launch's tail instead of a grad_gather / gather_adam launch after
-// it: the task publishes its chunk (release: the XCD's L2 written back, then an agent-scope
-// arrival count on its tile), reduces grad_gather's reduce items if it has some (tasks [0, nrb)),
-// waits for the tile's other chunks, and reduces its share of the tile's elements over all nch
-// chunks in grad_gather's order (slab_sum) — the same sums, so the same bits; no float atomics.
-// The chunks of other workgroups are read with agent-scope loads (coherent across the XCDs' L2s).
-// Every wait is bounded: a timeout sets fx.err and skips the share (the host raises).
-constexpr unsigned FIX_SPIN_MAX = 1u << 22;
-
-DEV float ld_agent(const float* p) {
-  return __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// slab_sum (csrc/common.h) with agent-scope loads: the same adds in the same order
-DEV float slab_sum_agent(const float* p, int nch, size_t st) {
-  float s = 0.f;
-  for (int c0 = 0; c0 < nch; c0 += 16) {
-    float x[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) x[c] = (c0 + c < nch) ? ld_agent(p + (size_t)(c0 + c) * st) : 0.f;
-#pragma unroll
-    for (int c = 0; c < 16; ++c)
-      if (c0 + c < nch) s += x[c];
-  }
-  return s;
-}
-
-template <int IDT>
-DEV void wgrad_fixup(const WgradArgs& a, char* smem) {
-  using PI = Prec<IDT>;
-  constexpr int NT = WG_WAVES * 64;
-  const WgradFix& f = a.fx;
-  const int tid = threadIdx.x;
-  const int* ft = f.ftask + 4 * blockIdx.x;
-  const int tile = ft[0], nch = ft[1], e_lo = ft[2], e_hi = ft[3];
-  float* red = reinterpret_cast<float*>(smem);          // [NT] (the ring is free: every DMA has landed)
-  int* okf = reinterpret_cast<int*>(smem + NT * sizeof(float));
-  typename PI::T* wimg = reinterpret_cast<typename PI::T*>(f.wimg);
-  const bool adam = f.mode == 2;
-  const float bc1 = 1.f - powf(f.b1, f.step);
-  const float bc2 = 1.f - powf(f.b2, f.step);
-  const float step_size = f.lr / bc1;
-  const float rbc2 = 1.f / sqrtf(bc2);
-  WAIT_VMCNT(0);      // this wave's slab stores are done
-  __syncthreads();    // ... every wave's, and every LDS read of the ring
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the chunk leaves this XCD's L2
-    __hip_atomic_fetch_add(f.sync + 2 * tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // the reduce items while the tile's other chunks finish (grad_gather / gather_adam's blocks
-  // [0, nrb): same sums, same order)
-  const int nrb = item_blocks(f.nitems);
-  if ((int)blockIdx.x < nrb) {
-    if (adam && blockIdx.x == 0 && tid == 0) {
-      f.state[0] = f.step;
-      f.state[1] = f.step;
-    }
-    float tot = 0.f, ss = 0.f;
-    int j;
-    if (item_reduce(f.part, f.npblk, f.npart, f.red_col, f.nitems, blockIdx.x, red, tot, j)) {
-      const int d = f.red_dst[j];
-      if (d >= 0) {
-        const float gi = tot * f.scale;
-        if (adam)
-          adam_apply<IDT>(d, gi, f.m[d], f.v[d], f.p[d], f.w_map[d], f.wt_map[d], f.g, f.p, f.m, f.v, f.b1, f.b2,
-                          step_size, rbc2, f.eps, wimg, f.qmul, f.f8);
-        else
-          f.g[d] = gi;
-        ss = gi * gi;
-      } else {
-        f.loss_out[-1 - d] = tot;
-      }
-    }
-    __syncthreads();
-    red[tid] = tid < ITEM_IPB ? ss : 0.f;
-    __syncthreads();
-    for (int w = 32; w > 0; w >>= 1) {
-      if (tid < w) red[tid] += red[tid + w];
-      __syncthreads();
-    }
-    if (adam && tid == 0) f.norm_part[blockIdx.x] = red[0];
-    __syncthreads();
-  }
-  if (tid == 0) {
-    int ok = 1;
-    for (unsigned spins = 0; __hip_atomic_load(f.sync + 2 * tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch;
-         ++spins) {
-      if (spins > FIX_SPIN_MAX) {
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    *okf = ok;
-  }
-  __syncthreads();
-  if (!*okf) {
-    if (tid == 0) __hip_atomic_store(f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  float ss = 0.f;
-  for (int j = e_lo + tid; j < e_hi; j += NT) {
-    // (no data-dependent branch before the slab loads: the per-element loads issue together)
-    const int i = f.elems[j];
-    const int mt = f.src_meta[i];
-    const int o = f.src_off[i];
-    float mi = 0.f, vi = 0.f, pv = 0.f;
-    int wi = -1, wti = -1;
-    if (adam) {
-      mi = f.m[i];
-      vi = f.v[i];
-      pv = f.p[i];
-      wi = f.w_map[i];
-      wti = f.wt_map[i];
-    }
-    const float gi = slab_sum_agent(a.slab + o, mt >> 4, (size_t)(mt & 15) << 12) * f.scale;
-    ss = fmaf(gi, gi, ss);
-    if (adam)
-      adam_apply<IDT>(i, gi, mi, vi, pv, wi, wti, f.g, f.p, f.m, f.v, f.b1, f.b2, step_size, rbc2, f.eps, wimg,
-                      f.qmul, f.f8);
-    else
-      f.g[i] = gi;
-  }
-  if (tid == 0) {   // the last task of the tile to leave resets its counters for the next launch
-    if (__hip_atomic_fetch_add(f.sync + 2 * tile + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1) {
-      __hip_atomic_store(f.sync + 2 * tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(f.sync + 2 * tile + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if (!adam) return;
-  red[tid] = ss;
-  __syncthreads();
-  for (int w = NT / 2; w > 0; w >>= 1) {
-    if (tid < w) red[tid] += red[tid + w];
-    __syncthreads();
-  }
-  if (tid == 0) f.norm_part[nrb + blockIdx.x] = red[0];
-}
-
-// IDT >= 0: the fused slab reduction in the tail, weight image of precision IDT (-1: none)
-template <int DT, int S, int IDT = -1>
+template <int DT, int S>
 __global__ __launch_bounds__(WG_WAVES * 64) void wgrad_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const WgradTask tk = a.tasks[blockIdx.x];
   if (4 * (tk.nq + tk.kq) <= 2 * WG_WAVES) wgrad_lds_body<DT, S, 2>(a, tk, smem);
   else wgrad_lds_body<DT, S, 3>(a, tk, smem);
-  if constexpr (IDT >= 0) wgrad_fixup<IDT>(a, smem);
 }
 
 // ring depth: fp32, split-bf16 and e4m3 3 stages (144 KiB), bf16 4 (96 KiB)
@@ -330,36 +243,6 @@ void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
   const size_t lds = wgrad_lds_bytes<DT, S>();
   set_max_lds_once<wgrad_kernel<DT, S>>(lds);
   hipLaunchKernelGGL((wgrad_kernel<DT, S>), dim3(a.ntasks), dim3(WG_WAVES * 64), lds, s, a);
-}
-
-// co-resident workgroups of the fused form (one below the occupancy answer per CU when it says
-// more than one: rollout.hip launch_nw)
-template <int DT, int S, int IDT>
-int fused_cap() {
-  const size_t lds = wgrad_lds_bytes<DT, S>();
-  set_max_lds_once<wgrad_kernel<DT, S, IDT>>(lds);
-  int per_cu = 0, dev = 0, ncu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(wgrad_kernel<DT, S, IDT>),
-                                                   WG_WAVES * 64, lds) != hipSuccess ||
-      hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return 0;
-  return ncu * (per_cu > 1 ? per_cu - 1 : per_cu);
-}
-
-template <int DT, int S, int IDT>
-void launch_wgrad_fused_t(const WgradArgs& a, hipStream_t s) {
-  static_assert(wgrad_lds_bytes<DT, S>() >= (WG_WAVES * 64 + 4) * sizeof(float), "fix-up scratch fits the ring");
-  const size_t lds = wgrad_lds_bytes<DT, S>();
-  const int cap = fused_cap<DT, S, IDT>();
-  if (a.ntasks > cap) {
-    dppo_note_error(hipErrorCooperativeLaunchTooLarge, __FILE__, __LINE__);
-    return;
-  }
-  WgradArgs aa = a;
-  void* args[] = {&aa};
-  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(wgrad_kernel<DT, S, IDT>),
-                                                  dim3(a.ntasks), dim3(WG_WAVES * 64), args, (unsigned)lds, s);
-  if (e != hipSuccess) dppo_note_error(e, __FILE__, __LINE__);
 }
 
 // Blocks [0, item_blocks(nitems)): the reduce items (log_std, loss-term sums, the per-head
@@ -409,25 +292,6 @@ extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
   else if (dt == DT_FP8) launch_wgrad_lds<DT_FP8, 3>(a, s);
   else launch_wgrad_lds<DT_BF16, 4>(a, s);
   HIP_CHECK_LAUNCH();
-}
-
-// (the image precision follows the update: split-bf16 / bf16 / fp32; the e4m3 wgrad of the fp8
-// mode updates the bf16 image)
-extern "C" void launch_wgrad_fused(int dt, int img_dt, const WgradArgs& a, hipStream_t s) {
-  if (a.ntasks <= 0) return;
-  if (dt == DT_S3 && img_dt == DT_S3) launch_wgrad_fused_t<DT_S3, 3, DT_S3>(a, s);
-  else if (dt == DT_BF16 && img_dt == DT_BF16) launch_wgrad_fused_t<DT_BF16, 4, DT_BF16>(a, s);
-  else if (dt == DT_FP8 && img_dt == DT_BF16) launch_wgrad_fused_t<DT_FP8, 3, DT_BF16>(a, s);
-  else if (dt == DT_F32 && img_dt == DT_F32) launch_wgrad_fused_t<DT_F32, 3, DT_F32>(a, s);
-  else dppo_note_error(hipErrorInvalidValue, __FILE__, __LINE__);
-}
-
-extern "C" int wgrad_fused_cap(int dt) {
-  if (dt == DT_S3) return fused_cap<DT_S3, 3, DT_S3>();
-  if (dt == DT_BF16) return fused_cap<DT_BF16, 4, DT_BF16>();
-  if (dt == DT_FP8) return fused_cap<DT_FP8, 3, DT_BF16>();
-  if (dt == DT_F32) return fused_cap<DT_F32, 3, DT_F32>();
-  return 0;
 }
 
 extern "C" void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part,

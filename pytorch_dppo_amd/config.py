@@ -96,12 +96,12 @@ class Params:
                                          # tile (one-kernel update, csrc/mlp.hip)
     fused_apply: bool = True             # world size 1: gradient gather + Adam in one launch
     fp8_wgrad_operands: bool = True      # dtype fp8 on the per-head path: e4m3 wgrad operands (else bf16)
+    fp8_policy_gemms: bool = False       # dtype fp8: the policy head's fc1 / fc2 on the e4m3 x128 MFMA too (opt-in:
+                                         # speed-neutral and 3x the policy-gradient error, profiles/r4/fp8_heads.md)
     stats_stream: str = "off"            # off | on | auto (on when an all-reduce sits in the chain): the
                                          # obs-stat reduce / all-reduce / merge on a side stream
     wgrad_wgs: int = 0                   # wgrad tasks per launch (0: one per CU of the device)
-    wgrad_gather: str = "auto"           # auto (= separate) | separate | fused (the split-K slab reduction and
-                                         # the Adam step in the wgrad launch's tail; needs every task
-                                         # co-resident; measured slower, profiles/r4/ab_wgrad_gather.md)
+    vhead_kernel: bool = True            # the value head on the transposed-chain 32x32 kernel (csrc/vhead.hip)
     mlp_rows: int = 0                    # diagnostics: force the tile update kernel's row tile (0: auto)
 
     # ------------------------------------------------------------------------------------
@@ -137,8 +137,7 @@ class Params:
         if self.obs_norm_update not in ("step", "rollout"):
             raise ValueError("obs_norm_update must be step|rollout")
         for name, ok in (("dist_backend", ("auto", "nccl", "gloo")), ("grad_comm", ("auto", "native", "process_group")),
-                         ("update_kernels", ("auto", "heads", "tile")), ("stats_stream", ("off", "on", "auto")),
-                         ("wgrad_gather", ("auto", "fused", "separate"))):
+                         ("update_kernels", ("auto", "heads", "tile")), ("stats_stream", ("off", "on", "auto"))):
             if getattr(self, name) not in ok:
                 raise ValueError(f"{name} must be {'|'.join(ok)}, got {getattr(self, name)}")
 

@@ -159,6 +159,11 @@ class HipEngine:
         # for the gradients (csrc/common.h Q8) — and the wgrad runs on the e4m3 MFMA: half the
         # operand bytes of the bf16 update's HBM round trip.  fp8_wgrad_operands=False: bf16 operands.
         self.q8 = self.fp8 and self.heads and bool(params.fp8_wgrad_operands)
+        # the value head on the transposed-chain 32x32 kernel (csrc/vhead.hip) at bf16x3 / bf16: it
+        # writes its wgrad operands h1v / g1v / g2v ROW-MAJOR ([ldT][features]), which the wgrad reads
+        # with transposing LDS reads (self.rm); the fp8 mode's e4m3 operands / fc1 keep the 16x16 head
+        self.vhead = (self.heads and not self.fp8 and bool(params.vhead_kernel)
+                      and bool(self.ext.vhead_train_applies(self.dt, self.layout)))
         # the gradient-amax ring: 3 slots x 4 tensors x 64 sub-slot lines of 32 dwords (csrc/kernels.h)
         self.q8_amax = torch.zeros(3 * 4 * Q8_SUB * 32, dtype=torch.int32, device=device)
         self._q8_next = 0          # step counter of the amax ring
@@ -212,8 +217,16 @@ class HipEngine:
         # row n_out == 1 makes the wgrad GEMM emit the bias gradient as column K).  The operand
         # buffers are fragment-major, so "row r" is a scattered index set.
         cols = torch.arange(self.ldT, device=device)
-        for buf, r in ((self.h1pT, lp1.fan_out), (self.h2pT, lp2.fan_out), (self.h1vT, lv1.fan_out),
-                       (self.h2vT, lv2.fan_out)):
+        # (row-major h1v: the value kernel writes its bias column itself)
+        bias_rows = [(self.h1pT, lp1.fan_out), (self.h2pT, lp2.fan_out), (self.h2vT, lv2.fan_out)]
+        if not self.vhead:
+            bias_rows.append((self.h1vT, lv1.fan_out))
+        # wgrad operand layout flags (dY side of the 6 layers, then X side): row-major for v_fc1's dY
+        # (g1v) and v_fc2's dY (g2v) / X (h1v) under the 32x32 value head
+        self.rm = [0] * 12
+        if self.vhead:
+            self.rm[3] = self.rm[4] = self.rm[6 + 4] = 1
+        for buf, r in bias_rows:
             if self.q8:       # e4m3 bytes of the activation scale (Q8_SH = 256: exact)
                 storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), Q8_SH, 2)
             else:
@@ -244,11 +257,7 @@ class HipEngine:
         np_ = min(4096, self.A + 8 + (phi - self.A + 255) // 256)
         nv_ = min(4096, 8 + (vhi - vlo + 255) // 256)
         self.norm_regions = [(0, np_), (np_, np_ + nv_)]
-        # the fused wgrad + gather + Adam launch: one entry per reduce-item block and per task
-        self.norm_n_fused = 0
-        if self.heads:
-            self.norm_n_fused = (len(self.items["joint"][0]) + 31) // 32 + self.joint_bucket["tasks_host"].numel() // 8
-        self.norm_part = torch.zeros(max(n_whole, np_ + nv_, self.norm_n_fused), **f32)
+        self.norm_part = torch.zeros(max(n_whole, np_ + nv_), **f32)
         self.norm_n_whole = n_whole
         self._norm_n = n_whole       # entries the last Adam path wrote (metrics_pack sums them)
         # a value-head step not yet applied: ("work", all-reduce work, step, mean) on the
@@ -257,19 +266,6 @@ class HipEngine:
         self._side: Optional[torch.cuda.Stream] = None   # the side stream of the overlapped value step
         # world-size-1 fast path: grad_gather + no-clip Adam in one launch (fused_apply=False: off)
         self.fused_apply = bool(params.fused_apply)
-        # the joint wgrad with the slab reduction (+ Adam) in its tail (Params.wgrad_gather=fused): needs
-        # every task co-resident (cooperative launch).  Opt-in: same-box A/B, it is 8 % (bf16x3) and
-        # 13 % (bf16) SLOWER per iteration than the separate gather launch (profiles/r4/ab_wgrad_gather.md),
-        # so "auto" keeps the separate launch.
-        self.wgrad_fused = False
-        if self.heads and params.wgrad_gather == "fused":
-            cap = int(self.ext.wgrad_fused_cap(self._wgrad_dt())) if self.device.type == "cuda" else 0
-            ntask = self.joint_bucket["tasks_host"].numel() // 8
-            self.wgrad_fused = 0 < ntask <= cap
-            if params.wgrad_gather == "fused" and not self.wgrad_fused:
-                raise RuntimeError(f"wgrad_gather=fused: {ntask} wgrad tasks, {cap} co-resident workgroups")
-        self._fix_err = torch.zeros(1, dtype=torch.int32, **dev)
-        self._fix_err_host = torch.zeros(1, dtype=torch.int32, pin_memory=self.device.type == "cuda")
         self.idx_dev = torch.zeros(self.ldT, dtype=torch.int32, **dev)
         self.key_action = rng.base_key(params.seed, rng.STREAM_ACTION, action_rank)
         self.empty = torch.empty(0, dtype=torch.int32, **dev)
@@ -402,43 +398,10 @@ class HipEngine:
             self.buckets.append({
                 "tasks_host": tasks_host, "tasks": tasks_host.to(self.device),
                 "slab": torch.zeros(base, device=self.device, dtype=torch.float32),
-                "lo": lo, "hi": hi, "partials": partials[bi], "runs": self._slab_runs(sm, lo),
-                **self._fix_plan(order, tiles, tile_off, so, sm, lo)})
+                "lo": lo, "hi": hi, "partials": partials[bi], "runs": self._slab_runs(sm, lo)})
         src[src < 0] = 0  # reduce items (log_std, and with the per-head kernels mu / v)
         self.src_off = src.to(torch.int32).to(self.device)
         self.src_meta = meta.to(torch.int32).to(self.device)
-
-    def _fix_plan(self, order: list, tiles: list, tile_off: Dict, so: torch.Tensor, sm: torch.Tensor,
-                  lo: int) -> Dict:
-        """the wgrad launch's fused slab reduction (csrc/kernels.h WgradFix): per task [tile, nch,
-        e_lo, e_hi] — its 1/nch share of its tile's elements — and the elements (flat indices) of
-        every tile, tile by tile in ascending flat order (consecutive threads: consecutive
-        parameters and slab offsets).  The tile of an element is the one whose chunk-0 slab region
-        holds its src_off."""
-        bases = torch.tensor([tile_off[t][0] for t in tiles], dtype=torch.int64)
-        sizes = torch.tensor([tile_off[t][2] for t in tiles], dtype=torch.int64)
-        has = torch.nonzero(sm > 0).flatten()
-        off = so[has].to(torch.int64)
-        tid = torch.searchsorted(bases, off, right=True) - 1
-        assert bool((tid >= 0).all()) and bool((off < bases[tid] + sizes[tid]).all()), "slab element outside its tile"
-        perm = torch.sort(tid, stable=True).indices
-        elems = (has[perm] + lo).to(torch.int32)
-        cnt = torch.bincount(tid, minlength=len(tiles)).tolist()
-        start = [0]
-        for c in cnt:
-            start.append(start[-1] + c)
-        index = {t: k for k, t in enumerate(tiles)}
-        fix = []
-        for r in order:
-            t = (r[0], r[1], r[2], r[6], r[7])
-            k = index[t]
-            base, nch, size = tile_off[t]
-            ci = (r[5] - base) // size
-            e = cnt[k]
-            fix += [k, nch, start[k] + ci * e // nch, start[k] + (ci + 1) * e // nch]
-        fix_host = torch.tensor(fix, dtype=torch.int32)
-        return {"fix": fix_host.to(self.device), "fix_host": fix_host, "elems": elems.to(self.device),
-                "sync": torch.zeros(2 * len(tiles), dtype=torch.int32, device=self.device)}
 
     def q8_maxima(self) -> torch.Tensor:
         """[3 slots][4 tensors] gradient maxima (g1p, g2p, g1v, g2v) of the amax ring (diagnostics)"""
@@ -452,30 +415,10 @@ class HipEngine:
             return (self.q8_amax, self._q8_step, [0, 1, -1, 2, 3, -1], [Q8_SX, Q8_SH, 1.0, Q8_SX, Q8_SH, 1.0])
         return (self.empty, 0, [-1] * 6, [1.0] * 6)
 
-    def _wgrad_fused(self, b: Dict, mode: int, scale: float) -> None:
-        """bucket b's wgrad with the slab reduction in its tail (WgradFix): mode 1 = + grad_gather
-        into grad_flat, 2 = + gather_adam (the next Adam step).  A fix-up timeout of an earlier
-        launch (staged, no sync here) raises."""
-        if int(self._fix_err_host[0]) != 0:
-            raise RuntimeError("wgrad fused reduction timed out waiting for a tile's chunks")
-        p = self.p
-        b1, b2 = p.adam_betas
-        src_off, src_meta = self.joint_src
-        rc, rd = self.items["joint"]
-        self.ext.wgrad_fused(self._wgrad_dt(), self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                             b["tasks_host"], b["slab"], *self._q8_args(), mode, b["fix"], b["fix_host"], b["elems"],
-                             b["sync"], self._fix_err, src_off, src_meta, self.part_joint, self.nhead_blk,
-                             self.part_joint.shape[1], rc, rd, scale, self.loss_sums, self.grad_flat,
-                             self.model.flat.data, self.adam_m, self.adam_v, float(p.lr), float(b1), float(b2),
-                             float(p.adam_eps), self.adam_step + 1, self.adam_state,
-                             self.norm_part[:self.norm_n_fused], self.wimg, self.w_map, self.wt_map, self.dt,
-                             self.no_q, *self._f8())
-        self._fix_err_host.copy_(self._fix_err, non_blocking=True)
-
     def _wgrad(self, b: Dict) -> None:
         """one wgrad launch over bucket b's tasks (Q8: e4m3 operands, the step's scales)"""
         self.ext.wgrad(self._wgrad_dt(), self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                       b["tasks_host"], b["slab"], *self._q8_args())
+                       b["tasks_host"], b["slab"], *self._q8_args(), self.rm)
 
     def _w8(self):
         """fp8 mode: (e4m3 image, per-layer scales) for the value head's e4m3 fc1; else off"""
@@ -675,6 +618,19 @@ class HipEngine:
         self._sn_epoch += self.T
         ls.n += float(self.N)
         err_host.copy_(err, non_blocking=True)
+
+    def raise_if_failed(self, sync: bool = False) -> None:
+        """A per-step normalisation launch that timed out waiting for a workgroup left its buffers
+        partly written: raise before anything built on them is reported or saved.  The host copy
+        of the timeout word is staged behind each launch; ``sync`` waits for it (checkpoints), the
+        worker's metrics resolution calls it after the iteration's event has completed."""
+        if self._sn_bufs is None:
+            return
+        if sync:
+            torch.cuda.synchronize(self.device)
+        if int(self._sn_bufs[3][0]) != 0:
+            raise RuntimeError("per-step observation normalisation launch timed out waiting for a workgroup: "
+                               "the iteration's rollout is incomplete")
 
     def _observe_step(self, norm: RunningObsStats, obs: torch.Tensor, shift: torch.Tensor) -> None:
         """norm.observes(obs) as three device launches (csrc/obs.hip obs_observe), moments about
@@ -1024,14 +980,18 @@ class HipEngine:
     def _head_kernel(self, h: int, idx_t, first: bool, xt_ready: bool, part: torch.Tensor, part_dw: int) -> None:
         p, M = self.p, self.mb
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
-                1 if p.std_convention == "var" else 0, 1 if first else 0, part.shape[1], h, part_dw]
+                1 if p.std_convention == "var" else 0, 1 if first else 0, part.shape[1], h, part_dw,
+                1 if (h == 1 and self.vhead) else 0]
+
+        # fp8: the value head's fc1 on the e4m3 image; the policy's GEMMs only with fp8_policy_gemms
+        w8 = self._w8() if (h == 1 or p.fp8_policy_gemms) else (self.no_u8, self.no_q)
 
         def launch(q8_step):
             self.ext.mlp_train(self.dt, self.x_buf, idx_t, 0, M, self.wimg, self.layout, self.scales,
                                self.model.flat.data, self.log_std_old, self.A, self.actions, self.logp, self.adv,
                                self.ret, self.values_buf, self.mu_prev, self.v_prev, opts,
                                [float(p.clip), float(p.ent_coeff)], self.tbufs, self.ldT, part, False, xt_ready,
-                               *self._w8(), self.q8_amax if self.q8 else self.empty, q8_step)
+                               *w8, self.q8_amax if self.q8 else self.empty, q8_step)
         if self.q8 and not self._q8_cal[h]:
             # the first step of this engine: one pass as step -1 only to record the gradient maxima
             # the step-0 scales come from (its stores and partials are overwritten by the real one;
@@ -1057,9 +1017,6 @@ class HipEngine:
         gather of the whole gradient into grad_flat (no optimizer step)"""
         self._joint_heads(idx_t, first, xt_ready)
         b = self.joint_bucket
-        if self.wgrad_fused:
-            self._wgrad_fused(b, 1, 1.0 / self.mb)
-            return
         self._wgrad(b)
         src_off, src_meta = self.joint_src
         rc, rd = self.items["joint"]
@@ -1072,11 +1029,6 @@ class HipEngine:
         p, M = self.p, self.mb
         self._joint_heads(idx_t, first, xt_ready)
         b = self.joint_bucket
-        if self.wgrad_fused:
-            self._wgrad_fused(b, 2, 1.0 / M)
-            self.adam_step += 1
-            self._norm_n = self.norm_n_fused
-            return
         self._wgrad(b)
         b1, b2 = p.adam_betas
         src_off, src_meta = self.joint_src

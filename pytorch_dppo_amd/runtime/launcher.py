@@ -137,6 +137,8 @@ def save(w, ctx: DistContext, path: str) -> None:
     # every deferred step applied BEFORE the weights are copied out: model.pt and the Adam state
     # of trainer_state.pt must describe the same step
     w.flush_pending()
+    if hasattr(w.engine, "raise_if_failed"):
+        w.engine.raise_if_failed(sync=True)   # never checkpoint a step built on a failed launch
     env_state = w.engine.env_state() if hasattr(w.engine, "env_state") else None
     ckpt.save_checkpoint(path, w.model.state_dict(), w.trainer_state(), ctx.rank, env_state)
     ctx.barrier()

@@ -290,6 +290,8 @@ class DPPOWorker:
         p = self.p
         if st["event"] is not None:
             self.ctx.wait_event(st["event"])     # bounded by dist_timeout_s (collective watchdog)
+        if hasattr(self.engine, "raise_if_failed"):
+            self.engine.raise_if_failed()        # (a timed-out per-step filter launch: never report it)
         v = st["host"].tolist()
         ep_ret, ep_cnt = v[0], v[1]
         if st["has_loss"]:

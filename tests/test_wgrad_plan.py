@@ -3,7 +3,6 @@ wgrad_tiles): every layer's [fan_out][fan_in + 1] gradient is covered exactly on
 kernel accepts (csrc/wgrad.hip: nq*kq <= 8 waves, nq + kq <= 6 fragment slots, tiles inside the
 128-row padded operand buffers).  CPU only — the kernel itself is checked against autograd in
 tests/test_gpu_kernels.py."""
-import functools
 
 import pytest
 import torch
@@ -62,7 +61,6 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads, q8):
     stub = SimpleNamespace(L=model.packed_layout(), ldT=65536, A=spec.act_dim, device=torch.device("cpu"),
                            heads=heads, q8=q8, head_range=[model.head_ranges["policy"], model.head_ranges["value"]],
                            _slab_index=HipEngine._slab_index, _slab_runs=HipEngine._slab_runs)
-    stub._fix_plan = functools.partial(HipEngine._fix_plan, stub)
     HipEngine._build_wgrad_plan(stub, model, target_wgs=256)
     total = 0
     for b in stub.buckets:
@@ -100,40 +98,6 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads, q8):
         want = torch.zeros(model.num_params, dtype=torch.bool)
         want[b["lo"]:b["hi"]] = slab_fed[b["lo"]:b["hi"]]
         assert torch.equal(covered, want)
-    # the fused slab reduction's plan (HipEngine._fix_plan): the tasks of a tile split its elements
-    # into nch consecutive shares, each element lies inside its tile, and every slab-fed element of
-    # the bucket is in exactly one share
-    row = torch.full((model.num_params,), -1, dtype=torch.int64)
-    col = torch.full((model.num_params,), -1, dtype=torch.int64)
-    lay = torch.full((model.num_params,), -1, dtype=torch.int64)
-    for li, l in enumerate(model.packed_layout().layers):
-        wo, wn = model.offsets[f"{l.name}.weight"]
-        bo, bn = model.offsets[f"{l.name}.bias"]
-        row[wo:wo + wn] = torch.arange(wn) // l.fan_in
-        col[wo:wo + wn] = torch.arange(wn) % l.fan_in
-        row[bo:bo + bn], col[bo:bo + bn] = torch.arange(bn), l.fan_in
-        lay[wo:wo + wn] = lay[bo:bo + bn] = li
-    for b in stub.buckets:
-        t = b["tasks_host"].view(-1, 8).tolist()
-        fx = b["fix_host"].view(-1, 4).tolist()
-        assert len(fx) == len(t)
-        el = b["elems"].to(torch.int64)
-        shares = {}
-        for (li, n0, k0, m0, m1, off, nq, kq), (tile, nch, e0, e1) in zip(t, fx):
-            shares.setdefault(tile, []).append((e0, e1, nch, (li, n0, k0, nq, kq)))
-        hit = torch.zeros(model.num_params, dtype=torch.int32)
-        for tile, sh in shares.items():
-            sh.sort()
-            assert len(sh) == sh[0][2] and len({s_[3] for s_ in sh}) == 1, tile   # nch tasks, one tile
-            assert all(a[1] == c[0] for a, c in zip(sh, sh[1:]))
-            li, n0, k0, nq, kq = sh[0][3]
-            e = el[sh[0][0]:sh[-1][1]]
-            hit.index_add_(0, e, torch.ones_like(e, dtype=torch.int32))
-            assert bool((lay[e] == li).all())
-            assert bool(((row[e] >= n0) & (row[e] < n0 + 64 * nq) & (col[e] >= k0) & (col[e] < k0 + 64 * kq)).all())
-        want = torch.zeros(model.num_params, dtype=torch.int32)
-        want[b["lo"]:b["hi"]] = slab_fed[b["lo"]:b["hi"]].to(torch.int32)
-        assert torch.equal(hit, want)
     if heads:   # per-head buckets: policy [A, v_fc1.weight), value [v_fc1.weight, n)
         (b0, b1) = stub.buckets
         assert (b0["lo"], b0["hi"]) == (spec.act_dim, model.head_ranges["policy"][1]) and b0["partials"]
