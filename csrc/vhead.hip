@@ -24,17 +24,11 @@
 // lane-linear.  Observation rows: per pair a 2 KiB X slot per stage, its two DMA instructions
 // split between the pair's waves (64-bit per-lane row addresses: any buffer size).  Counted vmcnt
 // waits + a raw s_barrier per stage (cdna_hip_programming.md 'Pipelining across barriers').
-#include <type_traits>
-
-#include "kernels.h"
-#include "common.h"
+#include "t32.h"
 
 namespace {
 
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-typedef __attribute__((ext_vector_type(2))) unsigned int u32x2v;
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
+using namespace t32;
 
 constexpr int VH_ROWS = 128;            // rows per workgroup
 constexpr int VH_WAVES = 8;
@@ -45,38 +39,6 @@ constexpr int VH_XB = 2048;             // X bytes per pair and stage
 constexpr int VH_GL = 4;                // ring DMA instructions per wave and stage
 constexpr int VH_W3 = 128;              // fc3 weights staged in LDS (fp32, zero past n_out[4])
 constexpr int VH_SCR = 32 * 1024;       // X ring (fc1) / pair-sum scratch: 8 waves x one 4 KiB tile
-
-template <int DT> struct VT;
-template <> struct VT<DT_S3> {           // split-bf16: fragment = hi 1 KiB | lo 1 KiB
-  using Frag = S3Frag;
-  static constexpr int FB = 2048, KPS = 1, EB = 4;
-  DEV static f32x16 mma(f32x16 c, const Frag& a, const Frag& b) {
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, c, 0, 0, 0);
-  }
-  // ring slot u of a stage (lane l: hi at (l / 32) KiB + 16 (l % 32), lo 512 B on)
-  DEV static Frag ring(const char* stg, int u, int lane) {
-    const char* p = stg + u * FB + (lane >> 5) * 1024 + (lane & 31) * 16;
-    return Frag{*reinterpret_cast<const bf16x8*>(p), *reinterpret_cast<const bf16x8*>(p + 512)};
-  }
-  // the element (n, k) of a packed image, as fp32
-  DEV static float img(const void* W, size_t i) {
-    const __bf16* p = reinterpret_cast<const __bf16*>(W) + 2 * (i & ~size_t(7)) + (i & 7);
-    return (float)p[0] + (float)p[8];
-  }
-};
-template <> struct VT<DT_BF16> {
-  using Frag = bf16x8;
-  static constexpr int FB = 1024, KPS = 2, EB = 2;
-  DEV static f32x16 mma(f32x16 c, const Frag& a, const Frag& b) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-  }
-  DEV static Frag ring(const char* stg, int u, int lane) {
-    return *reinterpret_cast<const bf16x8*>(stg + u * FB + lane * 16);
-  }
-  DEV static float img(const void* W, size_t i) { return (float)reinterpret_cast<const __bf16*>(W)[i]; }
-};
 
 constexpr size_t vh_lds_bytes() { return (size_t)VH_S * VH_SB + VH_SCR + (VH_W3 + 4) * sizeof(float); }
 static_assert(vh_lds_bytes() <= 160 * 1024, "value head LDS");
@@ -94,137 +56,21 @@ constexpr int vh_ns2() { return 32 / (4 * VT<DT>::KPS); }
 template <int DT>
 constexpr int vh_nsd() { return DT == DT_S3 ? 8 : 4; }
 
-DEV f32x16 tanh16(f32x16 x) {
-  // tanh x = 1 - 2 / (1 + 2^(2 log2(e) x)) (csrc/mlp_core.h act_tanh: exp + rcp, |err| ~1e-7)
-  f32x16 r;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float e = __builtin_amdgcn_exp2f(x[i] * (2.0f * 1.4426950408889634f));
-    r[i] = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + e), 1.0f);
-  }
-  return r;
-}
-
-// 4 fp32 -> 4 bf16 in 2 dwords
-DEV u32x2v pk4(float a, float b, float c, float d) {
-  const bf16x4 h = __builtin_convertvector((f32x4){a, b, c, d}, bf16x4);
-  return *reinterpret_cast<const u32x2v*>(&h);
-}
-DEV f32x4 unpk4(u32x2v v) {
-  const bf16x4 h = *reinterpret_cast<const bf16x4*>(&v);
-  return __builtin_convertvector(h, f32x4);
-}
-
-// The B operand of k-step s (features 16 s .. 16 s + 15 of a 32-feature accumulator tile x) in
-// natural k order: lanes 0-31 need features 0-7, lanes 32-63 features 8-15; each lane holds
-// P = features 4h + 0..3 (regs 8s .. 8s+3) and Q = 8 + 4h + 0..3 (regs 8s+4 .. 8s+7), so ONE
-// v_permlane32_swap per dword (P of the upper half <-> Q of the lower half) completes both.
-DEV bf16x8 swap_b(u32x2v P, u32x2v Q) {
-  u32x4v o;
-#pragma unroll
-  for (int d = 0; d < 2; ++d) {
-    const auto r = __builtin_amdgcn_permlane32_swap(P[d], Q[d], false, false);
-    o[d] = r[0];
-    o[2 + d] = r[1];
-  }
-  return *reinterpret_cast<const bf16x8*>(&o);
-}
-template <int DT>
-DEV typename VT<DT>::Frag b_operand(const f32x16& x, int s) {
-  const f32x4 p{x[8 * s], x[8 * s + 1], x[8 * s + 2], x[8 * s + 3]};
-  const f32x4 q{x[8 * s + 4], x[8 * s + 5], x[8 * s + 6], x[8 * s + 7]};
-  const u32x2v ph = pk4(p[0], p[1], p[2], p[3]), qh = pk4(q[0], q[1], q[2], q[3]);
-  if constexpr (DT == DT_S3) {
-    const f32x4 pr = p - unpk4(ph), qr = q - unpk4(qh);
-    const u32x2v pl = pk4(pr[0], pr[1], pr[2], pr[3]), ql = pk4(qr[0], qr[1], qr[2], qr[3]);
-    return S3Frag{swap_b(ph, qh), swap_b(pl, ql)};
-  } else {
-    return swap_b(ph, qh);
-  }
-}
-
-// s_waitcnt vmcnt(n) for a runtime n in [0, 8] (undercounting is safe)
-DEV void wait_vm_rt(int n) {
-  switch (n) {
-    case 0: WAIT_VMCNT(0); break;
-    case 1: WAIT_VMCNT(1); break;
-    case 2: WAIT_VMCNT(2); break;
-    case 3: WAIT_VMCNT(3); break;
-    case 4: WAIT_VMCNT(4); break;
-    case 5: WAIT_VMCNT(5); break;
-    case 6: WAIT_VMCNT(6); break;
-    case 7: WAIT_VMCNT(7); break;
-    default: WAIT_VMCNT(8); break;
-  }
-}
-
-template <int B, int E, typename F>
-DEV void static_for_vh(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for_vh<B + 1, E>(f);
-  }
-}
-
-// MFMAs over N ring fragments slot(0 .. N-1) of a stage, read in groups of G: group g + 1's LDS
-// reads are in flight while group g's MFMAs run.  f(i, fragment).
-template <int DT, int N, int G, typename SLOT, typename F>
-DEV void ring_mma(const char* stg, int lane, SLOT&& slot, F&& f) {
-  using Frag = typename VT<DT>::Frag;
-  constexpr int NG = N / G;
-  static_assert(N % G == 0, "groups");
-  Frag b[2][G];
-  static_for_vh<0, G>([&](auto ic) __attribute__((always_inline)) {
-    b[0][decltype(ic)::value] = VT<DT>::ring(stg, slot(decltype(ic)::value), lane);
-  });
-  static_for_vh<0, NG>([&](auto gc) __attribute__((always_inline)) {
-    constexpr int g = decltype(gc)::value;
-    if constexpr (g + 1 < NG) {
-      static_for_vh<0, G>([&](auto ic) __attribute__((always_inline)) {
-        b[(g + 1) & 1][decltype(ic)::value] = VT<DT>::ring(stg, slot((g + 1) * G + decltype(ic)::value), lane);
-      });
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    static_for_vh<0, G>([&](auto ic) __attribute__((always_inline)) {
-      f(g * G + decltype(ic)::value, b[g & 1][decltype(ic)::value]);
-    });
-  });
-}
-
-// one lane's 16 features of an operand row (natural order: the b_operand / swap_b layout) ->
-// the row-major wgrad operand (split: the 32-byte [8 hi | 8 lo] group of each 8 features) by a
-// non-temporal buffer store: vrow = the lane's row byte offset + its 8-feature group, fsoff = the
-// wave-uniform feature offset (bytes) — no 64-bit address registers live across the chain
-template <int DT>
-DEV void st_op(__amdgpu_buffer_rsrc_t rs, unsigned vrow, unsigned fsoff, const typename VT<DT>::Frag& f) {
-  if constexpr (DT == DT_S3) {
-    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4v*>(&f.h), rs, vrow, fsoff, 2);
-    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4v*>(&f.l), rs, vrow + 16, fsoff, 2);
-  } else {
-    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4v*>(&f), rs, vrow, fsoff, 2);
-  }
-}
-
-// sum over the 32 lanes of each half-wave of 32 values per lane (a butterfly: each level keeps half
-// the values, so 31 shuffles instead of 5 x 32); lane l ends with the sum of value l & 31 (fixed order)
-DEV float half_sum32(float (&v)[32], int lane) {
-#pragma unroll
-  for (int m = 16; m >= 1; m >>= 1) {
-    const bool up = (lane & m) != 0;
-#pragma unroll
-    for (int i = 0; i < m; ++i) {
-      const float send = up ? v[i] : v[i + m];
-      const float got = __shfl_xor(send, m, 64);
-      v[i] = (up ? v[i + m] : v[i]) + got;
-    }
-  }
-  return v[0];
-}
+// phase timeline (diagnostics, scripts/head_timeline.py --vhead): lane 0 of each wave of every
+// tstamp_every-th workgroup records the shader clock at the phase boundaries (a vector store no
+// counted wait covers: an undercount, safe); null in real runs
+#define VH_STAMP(i)                                                                               \
+  do {                                                                                            \
+    if (STAMP && (blockIdx.x % a.tstamp_every) == 0 && lane == 0)                                 \
+      a.tstamp[((size_t)(blockIdx.x / a.tstamp_every) * VH_WAVES + wave) * 16 + (i)] =            \
+          __builtin_amdgcn_s_memtime();                                                           \
+  } while (0)
 
 // TRAIN: the value head's update chain (the loss of train.py:154-157 / ppo.py:164, its backward
 // through fc3 and fc2; the fused narrow-layer weight gradient dW_v; h1 / g1 / g2 stored row-major
 // for the wgrad, csrc/wgrad.hip RM operands).  !TRAIN: V(x) into v_out (the GAE input).
-template <int DT, bool TRAIN>
+// STAMP: the diagnostic instantiation with the phase stamps (a.tstamp set); real runs take STAMP = false
+template <int DT, bool TRAIN, bool STAMP>
 __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
   using V = VT<DT>;
   using Frag = typename V::Frag;
@@ -336,6 +182,7 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
   const int ntot = ns1 + NS2 + NSD;
   // ---- prime: X stages 0, 1 and ring stages 0, 1 (the launcher checks ns1 >= 3) ----
   static_assert(VH_S == 3 && VH_XS == 3, "the wait counts below are written for 3-stage rings");
+  VH_STAMP(0);
   issue_x(0);
   issue_x(1);
   issue(0);
@@ -389,6 +236,7 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
   sync(VH_GL);
   issue(ns1 + 1);
   fc1(ring + ((ns1 - 1) % VH_S) * VH_SB, ns1 - 1);
+  VH_STAMP(1);
   {
     // h1 = tanh, the bias column (feature n_out[3]) = 1
     const int nb = a.n_out[3] - 256 * q, tb = nb >> 5, rb = nb & 31;
@@ -427,6 +275,7 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
                               });
   });
 
+  VH_STAMP(2);
   // ---- the pair's two fc2 partials, summed in a fixed order (both waves get the same bits), one
   // tile per round through the scratch (the X ring is idle; raw barriers: the dgrad stream stays
   // in flight) ----
@@ -450,6 +299,7 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
     }
     bar();
   }
+  VH_STAMP(3);
   // ---- h2 = tanh, fc3 on the VALU (fp32): v = b3 + sum_k w3[k] h2[k] ----
   float part = 0.f;
 #pragma unroll
@@ -465,6 +315,7 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
   const float v = w3s[VH_W3] + (part + __shfl_xor(part, 32, 64));
   if constexpr (!TRAIN) {
     if (q == 0 && h == 0 && valid) a.v_out[mr] = v;
+    VH_STAMP(7);
     WAIT_VMCNT(0);   // (nothing in flight: the stream ended with fc2)
     return;
   } else {
@@ -532,6 +383,7 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
       for (int qq = 0; qq < 2; ++qq)
         if (q == qq) st_op<DT>(rs_g2, v128, 16 * (4 * qq + k) * EB, gb[4 * qq + k]);
 
+    VH_STAMP(4);
     // ---- dgrad fc2: g1 = (W2^T g2) (1 - h1^2) over this wave's h1 tiles, two per pass ----
     constexpr int SPP = DT == DT_S3 ? 2 : 1;   // ring stages per pass
     constexpr int GD = DT == DT_S3 ? 1 : 2;    // fragments per read group (registers)
@@ -557,7 +409,9 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
         for (int s = 0; s < 2; ++s)
           st_op<DT>(rs_g1, v512, (256 * q + 32 * (2 * ip + tt) + 16 * s) * EB, b_operand<DT>(g1, s));
       }
+      if constexpr (ip == 1) VH_STAMP(5);
     });
+    VH_STAMP(6);
     // ---- per-workgroup partials (fixed order): the value loss (column 1) and dW_v ----
     WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
     float* dst = a.part + (size_t)blockIdx.x * a.npart;
@@ -571,6 +425,7 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
     } else if (tid == 128) {
       dst[1] = ((red[512] + red[513]) + red[514]) + red[515];
     }
+    VH_STAMP(7);
   }
 }
 
@@ -593,8 +448,13 @@ extern "C" int vhead_rows() { return VH_ROWS; }
 template <int DT, bool TRAIN>
 void vhead_launch_t(const MlpArgs& a, hipStream_t s) {
   const int nblk = (a.M + VH_ROWS - 1) / VH_ROWS;
-  set_max_lds_once<vhead_kernel<DT, TRAIN>>(vh_lds_bytes());
-  hipLaunchKernelGGL((vhead_kernel<DT, TRAIN>), dim3(nblk), dim3(VH_WAVES * 64), vh_lds_bytes(), s, a);
+  if (a.tstamp != nullptr) {
+    set_max_lds_once<vhead_kernel<DT, TRAIN, true>>(vh_lds_bytes());
+    hipLaunchKernelGGL((vhead_kernel<DT, TRAIN, true>), dim3(nblk), dim3(VH_WAVES * 64), vh_lds_bytes(), s, a);
+  } else {
+    set_max_lds_once<vhead_kernel<DT, TRAIN, false>>(vh_lds_bytes());
+    hipLaunchKernelGGL((vhead_kernel<DT, TRAIN, false>), dim3(nblk), dim3(VH_WAVES * 64), vh_lds_bytes(), s, a);
+  }
   HIP_CHECK_LAUNCH();
 }
 

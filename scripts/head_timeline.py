@@ -22,6 +22,8 @@ from pytorch_dppo_amd.utils.obs_stats import RunningObsStats  # noqa: E402
 
 # stamp i -> i+1 phases (HD_STAMP 0..7), plus fc1 sub-spans from stamps 8 / 9
 PHASES = ["fc1", "fc2", "fc3 wait", "fc3 + loss", "dgrad fc3", "dgrad fc2", "partials"]
+# the 32x32 transposed-chain value head (csrc/vhead.hip VH_STAMP)
+VPHASES = ["fc1", "fc2", "pair sum", "fc3 + loss + g2", "dgrad passes 1-2", "dgrad passes 3-4", "partials"]
 EVERY = 8
 
 
@@ -61,12 +63,22 @@ def main():
         t = buf.view(-1, nw, 16).cpu().double()
         d = t[:, :, 1:8] - t[:, :, 0:7]
         tot = t[:, :, 7] - t[:, :, 0]
-        res = {"sampled_blocks": t.shape[0], "total_cycles_median": float(tot.max(dim=1).values.median()),
+        vh = h == 1 and bool(getattr(eng, "vhead", False))
+        res = {"kernel": "vhead_kernel (32x32 transposed chain)" if vh else "mlp_head_kernel",
+               "sampled_blocks": t.shape[0], "total_cycles_median": float(tot.max(dim=1).values.median()),
                "chain_ms": ev[0].elapsed_time(ev[1]),
                "phases_median_cycles(max over waves)": {ph: float(d[:, :, i].max(dim=1).values.median())
-                                                        for i, ph in enumerate(PHASES)},
-               "fc1_first_span": float((t[:, :, 8] - t[:, :, 0]).max(dim=1).values.median()),
-               "fc1_mid_span(4 k-steps value / 3 stages policy)": float((t[:, :, 9] - t[:, :, 8]).max(dim=1).values.median())}
+                                                        for i, ph in enumerate(VPHASES if vh else PHASES)},
+               }
+        if vh:
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            rnd = (torch.arange(t.shape[0]) * EVERY) // ncu
+            res["total_by_round"] = {int(r): float(tot[rnd == r].max(dim=1).values.median())
+                                     for r in sorted(set(rnd.tolist()))}
+            out["value"] = res
+            continue
+        res["fc1_first_span"] = float((t[:, :, 8] - t[:, :, 0]).max(dim=1).values.median())
+        res["fc1_mid_span(4 k-steps value / 3 stages policy)"] = float((t[:, :, 9] - t[:, :, 8]).max(dim=1).values.median())
         # sub-spans (max over waves): fc3 MFMAs (3 -> 12) vs the loss (12 -> 4); the partials phase as
         # the fused narrow-layer dW MFMAs (6 -> 10), the wave's store / DMA drain (10 -> 11) and the
         # workgroup reduction + partial-row stores (11 -> 7)
