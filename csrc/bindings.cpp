@@ -330,14 +330,16 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   const int64_t nrows = actions.numel() / A;
   MlpArgs a = base_mlp((int)dt, L, scales, x_buf, idx, row0, M, wimg, flat, A, check_idx, nrows);
   TORCH_CHECK(opts.size() == 5 || opts.size() == 7 || opts.size() == 8,
-              "opts: loss_kind, value_loss, std_var, first_step, npart[, head, part_dw[, vhead]]");
+              "opts: loss_kind, value_loss, std_var, first_step, npart[, head, part_dw[, t32]]");
   // head >= 0: one head's per-head streaming kernel (csrc/mlp_head.hip; 0 policy, 1 value) with
   // its fused narrow-layer weight gradient at partial column part_dw (policy [32][128], value [128])
   const int head = opts.size() >= 7 ? (int)opts[5] : -1;
   const int part_dw = opts.size() >= 7 ? (int)opts[6] : 0;
-  // vhead (head 1): the transposed-chain 32x32 value head (csrc/vhead.hip), which writes h1v / g1v /
-  // g2v ROW-MAJOR ([ldT][512] / [ldT][512] / [ldT][128]): the engine's wgrad must read them so
-  const bool vhead = opts.size() == 8 && opts[7] != 0;
+  // t32: the head's transposed-chain 32x32 kernel — value (csrc/vhead.hip): h1v / g1v / g2v
+  // ROW-MAJOR ([ldT][512] / [ldT][512] / [ldT][128]); policy (csrc/phead.hip): h1p / g1p / g2p
+  // ([ldT][128]) and, unless xT_ready, the observation rows into xT ([ldT][d0]).  The engine's
+  // wgrad must read them so (its rm flags)
+  const bool t32 = opts.size() == 8 && opts[7] != 0;
   TORCH_CHECK(head >= -1 && head <= 1, "head: -1 (both heads, one kernel), 0 policy, 1 value");
   TORCH_CHECK(fopts.size() == 2, "fopts: clip, ent_coeff");
   TORCH_CHECK(tbufs.size() == 11, "11 transposed buffers");
@@ -397,7 +399,9 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   for (int i = 0; i < 11; ++i) *dst[i] = tbufs[i].data_ptr();
   a.ldT = (int)ldT;
   // a precomputed xT is only valid for the identity row order covering the whole buffer
-  TORCH_CHECK(!xT_ready || (a.idx == nullptr && row0 == 0 && ldT == M), "xT_ready needs a full-batch call");
+  // (t32 policy: x_buf itself is the wgrad's X operand then, so only the row order matters)
+  TORCH_CHECK(!xT_ready || (a.idx == nullptr && row0 == 0 && (ldT == M || (t32 && head == 0))),
+              "xT_ready needs a full-batch call");
   a.xT_ready = xT_ready ? 1 : 0;
   if (g_tstamp != nullptr) {
     const int64_t nw = head >= 0 ? mlp_head_waves(head) : mlp_train_waves((int)dt, a);
@@ -408,11 +412,25 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   a.part = part.data_ptr<float>();
   TORCH_CHECK(!(w8.defined() && w8.numel() > 0) || (dt == 1 && head >= 0), "w8: the fp8 mode's per-head bf16 update only");
   set_w8(a, w8, qscale, L);
-  if (vhead) {
-    TORCH_CHECK(head == 1 && !q8 && a.W8 == nullptr && vhead_shape_ok(a), "vhead: the value head at bf16x3 / bf16");
+  if (t32) {   // the row-major operand rows the kernels write are whole padded widths
+    const int64_t wid[11] = {head == 0 && !xT_ready ? L.d_in[0] : 0, head == 0 ? 128 : 0, 0, head == 1 ? 512 : 0, 0,
+                             head == 0 ? 128 : 0, head == 0 ? 128 : 0, 0, head == 1 ? 512 : 0, head == 1 ? 128 : 0, 0};
+    for (int i = 0; i < 11; ++i)
+      TORCH_CHECK(tbufs[i].numel() >= wid[i] * ldT, "t32 head: row-major operand buffer ", i, " too small");
+  }
+  if (t32 && head == 1) {
+    TORCH_CHECK(!q8 && a.W8 == nullptr && vhead_shape_ok(a), "vhead: the value head at bf16x3 / bf16");
     TORCH_CHECK(ldT * 512 * (dt == 3 ? 4 : 2) < (int64_t(1) << 31), "vhead: row-major operands beyond 2 GiB");
     TORCH_CHECK(ldT % vhead_rows() == 0 && Mpad <= ldT, "vhead: ldT covers whole workgroups");
     launch_vhead_train((int)dt, a, cur_stream());
+  } else if (t32) {
+    TORCH_CHECK(head == 0 && !q8 && a.W8 == nullptr && phead_shape_ok(a), "phead: the policy head at bf16x3 / bf16");
+    const int64_t eb = dt == 3 ? 4 : 2;
+    TORCH_CHECK(ldT * std::max<int64_t>(L.d_in[0], 128) * eb < (int64_t(1) << 31), "phead: row-major operands beyond 2 GiB");
+    TORCH_CHECK((int64_t)nblk * npart * 4 < (int64_t(1) << 31), "phead: partial buffer beyond 2 GiB");
+    TORCH_CHECK(ldT % phead_rows() == 0 && Mpad <= ldT && (L.d_in[0] >> 4) / (dt == 3 ? 1 : 2) >= 3,
+                "phead: ldT covers whole workgroups; fc1 has >= 3 stages");
+    launch_phead_train((int)dt, a, cur_stream());
   } else if (head >= 0) {
     launch_mlp_head((int)dt, (int)head, a, cur_stream());
   } else {
@@ -427,6 +445,15 @@ bool vhead_train_applies(int64_t dt, std::vector<int64_t> layout) {
   MlpArgs a{};
   for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
   return (dt == 3 || dt == 1) && vhead_shape_ok(a) != 0;
+}
+
+// the transposed-chain policy head covers this (dtype, network, action width)
+bool phead_train_applies(int64_t dt, std::vector<int64_t> layout, int64_t A) {
+  const Layout L = parse_layout(layout);
+  MlpArgs a{};
+  for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
+  a.A = (int)A;
+  return (dt == 3 || dt == 1) && phead_shape_ok(a) != 0 && (L.d_in[0] >> 4) / (dt == 3 ? 1 : 2) >= 3;
 }
 
 // the per-head kernels cover this (dtype, network); x_bytes is irrelevant to them (64-bit rows)
@@ -809,6 +836,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_train", &mlp_train);
   m.def("head_applies", &head_applies);
   m.def("vhead_train_applies", &vhead_train_applies);
+  m.def("phead_train_applies", &phead_train_applies);
+  m.def("set_phead", [](int64_t on) { set_phead((int)on); });
   m.def("head_rows", []() { return (int64_t)mlp_head_rows(); });
   m.def("set_vhead", [](int64_t on) { set_vhead((int)on); });
   m.def("head_waves", [](int64_t h) { return (int64_t)mlp_head_waves((int)h); });

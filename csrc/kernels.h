@@ -140,6 +140,12 @@ extern "C" void launch_vhead_train(int dt, const MlpArgs& a, hipStream_t s);   /
 extern "C" int vhead_rows();
 extern "C" void launch_vhead_fwd(int dt, const MlpArgs& a, hipStream_t s);   // V(x): dt bf16x3 or bf16
 extern "C" void set_vhead(int enable);
+// policy head update on 32x32x16 MFMAs, transposed chain (csrc/phead.hip): 128 rows per workgroup
+extern "C" int phead_applies(const MlpArgs& a);   // set_phead flag and shapes
+extern "C" int phead_shape_ok(const MlpArgs& a);
+extern "C" int phead_rows();
+extern "C" void launch_phead_train(int dt, const MlpArgs& a, hipStream_t s);
+extern "C" void set_phead(int enable);
 
 // fp8 mode: the Adam kernels also refresh the e4m3 image the update's fc1 reads (csrc/mlp_head.hip
 // F8), element i as p / qs[lid[i]] with the iteration's per-layer scales; img == nullptr: off

@@ -13,6 +13,8 @@
 
 namespace t32 {
 
+constexpr float T32_LOG_2PI = 1.8378770664093453f;
+
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2v;
@@ -150,14 +152,23 @@ DEV void ring_mma(const char* stg, int lane, SLOT&& slot, F&& f) {
 // one lane's 16 features of an operand row (natural order: the b_operand / swap_b layout) ->
 // the row-major wgrad operand (split: the 32-byte [8 hi | 8 lo] group of each 8 features) by a
 // non-temporal buffer store: vrow = the lane's row byte offset + its 8-feature group, fsoff = the
-// wave-uniform feature offset (bytes) — no 64-bit address registers live across the chain
+// wave-uniform feature offset (bytes) — no 64-bit address registers live across the chain.
+//
+// The store's data registers stay untouched for two wait states after it issues: a VALU write
+// of a 16-byte store's data right behind the store replaced what it stored for the last 4 lanes
+// of each 16-lane group (measured: the bf16 value head's g1 rows, scripts/debug_t32_nan.py), a
+// store-data WAR the compiler did not pad here
+DEV void st_b128(u32x4v v, __amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 2);
+  asm volatile("s_nop 1" ::"v"(v));
+}
 template <int DT>
 DEV void st_op(__amdgpu_buffer_rsrc_t rs, unsigned vrow, unsigned fsoff, const typename VT<DT>::Frag& f) {
   if constexpr (DT == DT_S3) {
-    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4v*>(&f.h), rs, vrow, fsoff, 2);
-    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4v*>(&f.l), rs, vrow + 16, fsoff, 2);
+    st_b128(*reinterpret_cast<const u32x4v*>(&f.h), rs, vrow, fsoff);
+    st_b128(*reinterpret_cast<const u32x4v*>(&f.l), rs, vrow + 16, fsoff);
   } else {
-    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4v*>(&f), rs, vrow, fsoff, 2);
+    st_b128(*reinterpret_cast<const u32x4v*>(&f), rs, vrow, fsoff);
   }
 }
 
@@ -166,6 +177,24 @@ DEV void st_op(__amdgpu_buffer_rsrc_t rs, unsigned vrow, unsigned fsoff, const t
 DEV float half_sum32(float (&v)[32], int lane) {
 #pragma unroll
   for (int m = 16; m >= 1; m >>= 1) {
+    const bool up = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < m; ++i) {
+      const float send = up ? v[i] : v[i + m];
+      const float got = __shfl_xor(send, m, 64);
+      v[i] = (up ? v[i + m] : v[i]) + got;
+    }
+  }
+  return v[0];
+}
+
+// the same over 16 values per lane: lanes l and l ^ 16 first add (the 32-lane sum then halves
+// over 4 levels); lane l ends with the sum of value l & 15
+DEV float half_sum16(float (&v)[16], int lane) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] += __shfl_xor(v[i], 16, 64);
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) {
     const bool up = (lane & m) != 0;
 #pragma unroll
     for (int i = 0; i < m; ++i) {

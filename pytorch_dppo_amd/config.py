@@ -102,6 +102,7 @@ class Params:
                                          # obs-stat reduce / all-reduce / merge on a side stream
     wgrad_wgs: int = 0                   # wgrad tasks per launch (0: one per CU of the device)
     vhead_kernel: bool = True            # the value head on the transposed-chain 32x32 kernel (csrc/vhead.hip)
+    phead_kernel: bool = False           # ... and the policy head (csrc/phead.hip; needs vhead_kernel)
     mlp_rows: int = 0                    # diagnostics: force the tile update kernel's row tile (0: auto)
 
     # ------------------------------------------------------------------------------------

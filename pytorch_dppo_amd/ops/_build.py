@@ -24,7 +24,7 @@ OUT_DIR = os.path.dirname(os.path.abspath(__file__))
 EXT_NAME = "_dppo_hip"
 ARCH = os.environ.get("DPPO_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-DEVICE_SRCS = ["rollout.hip", "mlp.hip", "mlp_head.hip", "vhead.hip", "wgrad.hip", "optim.hip", "obs.hip"]
+DEVICE_SRCS = ["rollout.hip", "mlp.hip", "mlp_head.hip", "vhead.hip", "phead.hip", "wgrad.hip", "optim.hip", "obs.hip"]
 HOST_SRCS = ["bindings.cpp", "comm.cpp"]   # compiled with the torch include paths
 HEADERS = ["common.h", "mlp_core.h", "kernels.h", "t32.h"]
 

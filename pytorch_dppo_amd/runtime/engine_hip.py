@@ -164,6 +164,12 @@ class HipEngine:
         # with transposing LDS reads (self.rm); the fp8 mode's e4m3 operands / fc1 keep the 16x16 head
         self.vhead = (self.heads and not self.fp8 and bool(params.vhead_kernel)
                       and bool(self.ext.vhead_train_applies(self.dt, self.layout)))
+        # the policy head's update on the transposed-chain kernel too (csrc/phead.hip): h1p / g1p /
+        # g2p row-major, and the observation operand of p_fc1 AND v_fc1 row-major — x_buf itself
+        # for a full-batch step (no x^T anywhere: the rollout skips writing it), the kernel's
+        # gathered rows in xT for a minibatch
+        self.phead = (self.vhead and bool(params.phead_kernel)
+                      and bool(self.ext.phead_train_applies(self.dt, self.layout, A)))
         # the gradient-amax ring: 3 slots x 4 tensors x 64 sub-slot lines of 32 dwords (csrc/kernels.h)
         self.q8_amax = torch.zeros(3 * 4 * Q8_SUB * 32, dtype=torch.int32, device=device)
         self._q8_next = 0          # step counter of the amax ring
@@ -217,15 +223,29 @@ class HipEngine:
         # row n_out == 1 makes the wgrad GEMM emit the bias gradient as column K).  The operand
         # buffers are fragment-major, so "row r" is a scattered index set.
         cols = torch.arange(self.ldT, device=device)
-        # (row-major h1v: the value kernel writes its bias column itself)
-        bias_rows = [(self.h1pT, lp1.fan_out), (self.h2pT, lp2.fan_out), (self.h2vT, lv2.fan_out)]
+        # (row-major h1v / h1p: the t32 kernels write their bias columns themselves)
+        bias_rows = [(self.h2pT, lp2.fan_out), (self.h2vT, lv2.fan_out)]
         if not self.vhead:
             bias_rows.append((self.h1vT, lv1.fan_out))
+        if not self.phead:
+            bias_rows.append((self.h1pT, lp1.fan_out))
         # wgrad operand layout flags (dY side of the 6 layers, then X side): row-major for v_fc1's dY
         # (g1v) and v_fc2's dY (g2v) / X (h1v) under the 32x32 value head
         self.rm = [0] * 12
         if self.vhead:
             self.rm[3] = self.rm[4] = self.rm[6 + 4] = 1
+        # ... and under the 32x32 policy head p_fc1's / p_fc2's dY (g1p, g2p), p_fc2's X (h1p) and
+        # the observation operand of both fc1 layers
+        self.wg_x_full = self.wg_x
+        if self.phead:
+            self.rm[0] = self.rm[1] = self.rm[6 + 0] = self.rm[6 + 1] = self.rm[6 + 3] = 1
+            assert self.x_rows[0] == self.d0, "row-major observation operand: x_buf rows are d0 wide"
+            # a full-batch step reads the observation rows straight from x_buf (rows [0, ldT) of
+            # its N + E rows)
+            if self.ldT <= self.x_buf.shape[0]:
+                xb = self.x_buf.view(-1)
+                self.wg_x_full = [xb, self.h1pT, self.h2pT, xb, self.h1vT, self.h2vT]
+        self._x_full = False   # the current step's X operand: x_buf (full batch, phead) or xT
         for buf, r in bias_rows:
             if self.q8:       # e4m3 bytes of the activation scale (Q8_SH = 256: exact)
                 storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), Q8_SH, 2)
@@ -281,7 +301,7 @@ class HipEngine:
         # the rollout can emit the full-batch x^T operand when the update is one full-batch step
         # (Q8: the policy kernel writes the e4m3 x^T in the first full-batch step instead)
         self.xT_from_rollout = (self.mb == self.N and self.ldT == self.N and E % 16 == 0 and self.N % 32 == 0
-                                and params.obs_norm_update == "rollout" and not self.q8)
+                                and params.obs_norm_update == "rollout" and not self.q8 and not self.phead)
         self._xT_valid = False   # True once a rollout wrote x^T for the current buffer contents
         self.s12 = torch.zeros(2, O, dtype=torch.float64, **dev)
         stats.device_merge = self._device_merge
@@ -417,7 +437,8 @@ class HipEngine:
 
     def _wgrad(self, b: Dict) -> None:
         """one wgrad launch over bucket b's tasks (Q8: e4m3 operands, the step's scales)"""
-        self.ext.wgrad(self._wgrad_dt(), self.wg_g, self.wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
+        wg_x = self.wg_x_full if self._x_full else self.wg_x
+        self.ext.wgrad(self._wgrad_dt(), self.wg_g, wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
                        b["tasks_host"], b["slab"], *self._q8_args(), self.rm)
 
     def _w8(self):
@@ -979,9 +1000,15 @@ class HipEngine:
 
     def _head_kernel(self, h: int, idx_t, first: bool, xt_ready: bool, part: torch.Tensor, part_dw: int) -> None:
         p, M = self.p, self.mb
+        t32 = (h == 1 and self.vhead) or (h == 0 and self.phead)
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
                 1 if p.std_convention == "var" else 0, 1 if first else 0, part.shape[1], h, part_dw,
-                1 if (h == 1 and self.vhead) else 0]
+                1 if t32 else 0]
+        if h == 0 and self.phead:
+            # full batch: the wgrad reads x_buf (no X rows written); a minibatch: the kernel
+            # gathers its observation rows into xT (row-major)
+            self._x_full = idx_t is self.empty and self.wg_x_full is not self.wg_x
+            xt_ready = self._x_full
 
         # fp8: the value head's fc1 on the e4m3 image; the policy's GEMMs only with fp8_policy_gemms
         w8 = self._w8() if (h == 1 or p.fp8_policy_gemms) else (self.no_u8, self.no_q)

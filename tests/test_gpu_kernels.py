@@ -170,6 +170,7 @@ def test_vhead_update_matches_16x16_head_update(dtype, loss, value_loss, mb):
     for vh in (True, False):
         p = ppo_preset(**kw) if loss == "ppo" else dppo_preset(**kw)
         p.vhead_kernel = vh
+        p.phead_kernel = False    # the value head alone (the policy head: test_phead_update_*)
         eng, model, _, _ = _engine(p)
         assert eng.vhead == vh
         xq = _fill_buffer(eng, model)
@@ -192,6 +193,56 @@ def test_vhead_update_matches_16x16_head_update(dtype, loss, value_loss, mb):
 
 
 @pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
+@pytest.mark.parametrize("loss,mb", [("ppo", None), ("ppo", 1024), ("ppo", 1000), ("dppo_ref", 768)])
+def test_phead_update_matches_16x16_head_update(dtype, loss, mb):
+    """The policy head's update on the 32x32 transposed-chain kernel (csrc/phead.hip: row-major
+    h1p / g1p / g2p, the observation operand of both fc1 layers row-major — x_buf itself for a
+    full batch (mb None), the kernel's gathered rows for a minibatch; dW_mu by MFMA over the
+    LDS-staged h2 / dL/dmu) vs the 16x16 head kernels: the whole gradient, the loss sums and the
+    reference loss's mu_prev; vs autograd for the ppo loss.  Ragged minibatches (1000, 768) leave
+    rows past M in the last workgroup (zero gradient)."""
+    N = 128 * 16
+    kw = dict(device="gpu", env_name="Humanoid-v2", num_envs=128, exploration_size=N, batch_size=mb or N,
+              dtype=dtype, ent_coeff=0.01, loss=loss, update_kernels="heads")
+    bf = dtype == "bf16"
+    res = {}
+    for ph in (True, False):
+        p = ppo_preset(**kw) if loss == "ppo" else dppo_preset(**kw)
+        p.vhead_kernel = ph
+        p.phead_kernel = ph
+        eng, model, _, _ = _engine(p)
+        assert eng.phead == ph and eng.vhead == ph
+        xq = _fill_buffer(eng, model)
+        idx = None if mb is None else torch.randperm(eng.N, generator=torch.Generator().manual_seed(5))[:mb]
+        eng.begin_update()
+        eng.grad(idx)
+        torch.cuda.synchronize()
+        res[ph] = (eng.grad_flat.clone(), eng.last_losses(), eng.mu_prev.clone())
+        if ph:
+            assert eng._x_full == (mb is None)
+        if ph and loss == "ppo":
+            ii = torch.arange(eng.N, device=DEV) if idx is None else idx.to(DEV)
+            g_ref, _ = _torch_grad(model, p, xq, eng, ii)
+            assert (eng.grad_flat - g_ref).norm().item() / g_ref.norm().item() < (6e-2 if bf else 2e-4)
+            for name in ("p_fc1", "p_fc2", "mu"):
+                for part in ("weight", "bias"):
+                    o, n = model.offsets[f"{name}.{part}"]
+                    gr, gk = g_ref[o:o + n], eng.grad_flat[o:o + n]
+                    assert (gk - gr).norm().item() <= (1e-1 if bf else 6e-4) * (gr.norm().item() + 1e-8), (name, part)
+            o, n = model.offsets["log_std"]
+            assert (eng.grad_flat[o:o + n] - g_ref[o:o + n]).norm().item() <= (
+                (1e-1 if bf else 6e-4) * (g_ref[o:o + n].norm().item() + 1e-8))
+    (g1, l1, mp1), (g0, l0, mp0) = res[True], res[False]
+    assert torch.isfinite(g1).all()
+    rel = (g1 - g0).norm().item() / g0.norm().item()
+    assert rel < (2e-2 if bf else 2e-5), rel
+    for k in ("loss_value", "loss_clip", "loss_ent"):
+        assert abs(l1[k] - l0[k]) < (1e-2 if bf else 1e-5) * (1 + abs(l0[k])), (k, l1[k], l0[k])
+    if loss == "dppo_ref":
+        assert (mp1 - mp0).abs().max().item() <= (2e-2 if bf else 2e-5) * (1 + mp0.abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
 def test_wgrad_row_major_operands_bit_identical_to_fragment_major(dtype):
     """The wgrad reading the 32x32 value head's row-major operands (per-lane row DMA into XOR-
     swizzled 128-byte-row images, ds_read_b64_tr_b16) gives the same MFMA operands in the same k
@@ -199,6 +250,7 @@ def test_wgrad_row_major_operands_bit_identical_to_fragment_major(dtype):
     from pytorch_dppo_amd.models.actor_critic import fm_index
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=256, exploration_size=256 * 16,
                     batch_size=256 * 16, dtype=dtype, update_kernels="heads")
+    p.phead_kernel = False   # the value layers' operands only (v_fc1's X stays fragment-major)
     eng, model, _, _ = _engine(p)
     assert eng.vhead
     _fill_buffer(eng, model)
@@ -877,13 +929,14 @@ def test_packed_metrics_match_torch(max_norm):
     assert torch.equal(eng.metrics_buf[:2], eng.ep_sum)
 
 
-@pytest.mark.parametrize("extra", [[], ["--overlap-rollout"], ["--grad-comm", "process_group"]])
+@pytest.mark.parametrize("extra", [[], ["--overlap-rollout", "off"], ["--grad-comm", "process_group"]])
 def test_two_ranks_on_one_gpu_stay_in_sync(extra):
     """bench.py as 2 ranks sharing the box's GPU (RCCL refuses two ranks on one device, so
     --dist-backend gloo): by default the gloo adapter runs the PRODUCTION multi-rank branch (the
     in-stream one an N-GPU RCCL run takes: joint kernels → gather → all-reduce → whole-vector
-    Adam; with --overlap-rollout the side-stream value step); the ranks must end with
-    bit-identical parameters (--verify-sync)."""
+    Adam, and — the world > 1 default, --overlap-rollout auto — the last epoch's value step on
+    the side stream beside the next rollout); the ranks must end with bit-identical parameters
+    (--verify-sync)."""
     import os
     import subprocess
     import sys
@@ -902,7 +955,11 @@ def test_two_ranks_on_one_gpu_stay_in_sync(extra):
     pg = "process_group" in extra
     assert d["config"]["grad_allreduce"] == ("process_group" if pg else "gloo_in_stream")
     assert ("grad_allreduce process_group" if pg else "grad_allreduce in_stream") in r.stderr
-    if "--overlap-rollout" in extra:
+    off = "off" in extra
+    assert d["config"]["overlap_rollout"] is (not off)
+    if off:
+        assert d["config"]["overlap_value_step"] == "none"
+    elif not pg:
         assert d["config"]["overlap_value_step"] == "side_stream"
 
 
@@ -1123,13 +1180,14 @@ def test_bench_geometry_full_batch_gradient_matches_autograd(dtype, tol):
                     batch_size=4096 * 16, dtype=dtype, num_epoch=1)
     eng, model, env, stats = _engine(p)
     stats.observes(env.observe())
-    assert eng.xT_from_rollout and eng.N == 65536
+    # (the 32x32 policy head reads the observation rows from x_buf itself: no x^T at all)
+    assert (eng.xT_from_rollout or eng.phead) and eng.N == 65536
     assert sum(b["tasks_host"].numel() // 8 for b in eng.buckets) >= 200
     eng.rollout()
     eng.values()
     eng.gae()
     eng.begin_update()
-    assert eng._xT_valid
+    assert eng._xT_valid or eng.phead
     eng.grad(None)
     xq = eng.decode(eng.x_buf)[:eng.N, :model.num_inputs]
     model.flat.grad = None
