@@ -131,6 +131,9 @@ def main():
     ap.add_argument("--dist-timeout-s", type=float, default=300.0,
                     help="bound of every wait on peers (collective watchdog; abort + non-zero exit)")
     ap.add_argument("--heartbeat-timeout-s", type=float, default=60.0)
+    ap.add_argument("--t32", default="auto", choices=["auto", "off", "value", "both"],
+                    help="update head kernels: the 32x32 transposed-chain kernels (csrc/vhead.hip, csrc/phead.hip) "
+                         "for none / the value head / both heads; auto = the Params defaults")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -165,6 +168,9 @@ def main():
                         dist_backend=args.dist_backend, grad_comm=args.grad_comm,
                         dist_timeout_s=args.dist_timeout_s,
                         phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
+        if args.t32 != "auto":
+            p.vhead_kernel = args.t32 in ("value", "both")
+            p.phead_kernel = args.t32 == "both"
         w = DPPOWorker(p, ctx)
         m = {}
         for i in range(args.warmup):
@@ -210,6 +216,8 @@ def main():
     if ctx.collective:
         grad_ar = ("process_group" if ctx.native is None else
                    "rccl_in_stream" if ctx.backend == "nccl" else "gloo_in_stream")
+    t32_heads = [k for k, on in (("value", getattr(w.engine, "vhead", False)),
+                                 ("policy", getattr(w.engine, "phead", False))) if on]
     del w
     variants = {}
     for dt in [d for d in args.variants.split(",") if d and d != args.dtype]:
@@ -233,6 +241,7 @@ def main():
                           "rollout_len": T, "num_epoch": args.num_epoch,
                           "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout,
                           "per_head_kernels": heads, "grad_allreduce": grad_ar,
+                          "t32_heads": t32_heads,
                           # --overlap-rollout on the in-stream path: the last value-head all-reduce +
                           # Adam run on a side stream (second communicator) beside the next rollout
                           "overlap_value_step": ("side_stream" if args.overlap_rollout and ctx.native_side is not None

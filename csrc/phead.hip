@@ -52,9 +52,25 @@ DEV int ph_swz(int row) { return ((row >> 1) & 1) << 2; }
 
 // 4 consecutive rows x 16 columns of a row-major bf16 plane, transposed: lane 4 q + p of each
 // 16-lane group addresses row q, columns 4 p .. 4 p + 3; lane i receives column i (rows 0-3)
+// (inline asm, no wait: with the builtin the compiler put an s_waitcnt vmcnt(0) — every in-flight
+// DMA and operand store — in front of these reads; ph_settle waits for them instead)
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 DEV s16x4 tr4(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  s16x4 v;
+  const unsigned addr = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)(p);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+// the LDS reads of a group of fragments have landed (the asm redefines them: no use moves above)
+template <int DT>
+DEV void ph_settle(typename VT<DT>::Frag (&fa)[2], typename VT<DT>::Frag (&fb)[2]) {
+  if constexpr (DT == DT_S3) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(fa[0].h), "+v"(fa[0].l), "+v"(fa[1].h), "+v"(fa[1].l), "+v"(fb[0].h), "+v"(fb[0].l),
+                   "+v"(fb[1].h), "+v"(fb[1].l));
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[0]), "+v"(fa[1]), "+v"(fb[0]), "+v"(fb[1]));
+  }
 }
 DEV bf16x8 cat8(s16x4 a0, s16x4 a1) {
   typedef __attribute__((ext_vector_type(8))) short s16x8;
@@ -111,8 +127,8 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
                                        (__attribute__((address_space(3))) void*)(acts + 64 * k), 4, 0, 0);
     }
   }
-  const float l_adv = a.adv[srow];
-  const float l_lpo = ref_loss ? 0.f : a.logp_old[srow];
+  float l_adv = a.adv[srow];
+  float l_lpo = ref_loss ? 0.f : a.logp_old[srow];
   if (tid < 64) {
     const int j = tid & 31;
     lsd[tid] = tid < 32 ? (j < A ? a.log_std[j] : 0.f) : ((ref_loss && j < A) ? a.log_std_old[j] : 0.f);
@@ -194,6 +210,10 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
   const bool write_x = a.xT_ready == 0;
   const int xst = write_x ? 2 : 0;   // X operand stores per fc1 step
 
+  // the loss inputs (and the action DMAs) land before the stream starts: the asm redefines the
+  // registers, so no compiler-inserted wait for them falls inside the counted stream (where it
+  // would also wait for every in-flight DMA and operand store)
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(l_adv), "+v"(l_lpo)::"memory");
   // ---- prime: X stages 0, 1 and ring stages 0, 1 (the launcher checks ns1 >= 3) ----
   static_assert(PH_S == 3 && PH_XS == 3, "the wait counts below are written for 3-stage rings");
   issue_x(0);
@@ -215,11 +235,25 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
-  // a step past fc1: the previous step issued the refill st + 1 (if any) and `stores` stores
-  auto sync_late = [&](int st, int stores) __attribute__((always_inline)) {
-    sync((st + 1 < ntot ? PH_GL : 0) + stores);
-    if (st + 2 < ntot) issue(st + 2);
+  // from the last two fc1 steps on the counts come from VmTrack, entering with stage ns1 - 2's
+  // batch followed by [its step's X stores,] X(ns1 - 1), R(ns1 - 1) and the previous step's X
+  // stores (ns1 == 3: stage 1's batch is the prologue's, the first step's X stores only)
+  VmTrack vt(ns1 == 3 ? 2 + PH_GL + xst : 2 + PH_GL + 2 * xst, xst);
+  constexpr int SP = S3 ? 2 : 1;   // store instructions per operand fragment
+  auto sync_t = [&](int st) __attribute__((always_inline)) {
+    sync(vt.younger());
+    const bool refill = st + 2 < ntot;
+    if (refill) issue(st + 2);
+    vt.advance(refill ? PH_GL : 0);
+  };
+  auto sync_late = [&](int st) __attribute__((always_inline)) {
+    sync_t(st);
     return ring + (st % PH_S) * PH_SB;
+  };
+  // an operand store, counted
+  auto sto = [&](__amdgpu_buffer_rsrc_t rs, unsigned vrow, unsigned fsoff, const Frag& f) __attribute__((always_inline)) {
+    st_op<DT>(rs, vrow, fsoff, f);
+    vt.add(SP);
   };
   auto fc1 = [&](const char* stg, int st) __attribute__((always_inline)) {
     Frag xb[KPS];
@@ -238,17 +272,16 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
   // steps 0 .. ns1-3 issue X(st + 2) and fc1 stage st + 2 (younger than R(st): X(st+1), R(st+1)
   // and the previous step's X operand stores; step 0: R(1) only)
   for (int st = 0; st < ns1 - 2; ++st) {
-    sync(st == 0 ? PH_GL : 2 + PH_GL + xst);
+    sync(st == 0 ? PH_GL : (st == 1 ? 2 + PH_GL + xst : 2 + PH_GL + 2 * xst));
     issue_x(st + 2);
     issue(st + 2);
     fc1(ring + (st % PH_S) * PH_SB, st);
   }
   // the last two fc1 steps refill with fc2 stages 0, 1 (no more X)
-  sync(2 + PH_GL + xst);
-  issue(ns1);
+  sync_t(ns1 - 2);
   fc1(ring + ((ns1 - 2) % PH_S) * PH_SB, ns1 - 2);
-  sync(PH_GL + xst);
-  issue(ns1 + 1);
+  vt.add(xst);
+  sync_t(ns1 - 1);
   fc1(ring + ((ns1 - 1) % PH_S) * PH_SB, ns1 - 1);
   {
     // h1 = tanh, the bias column (feature n_out[0]) = 1
@@ -267,21 +300,19 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
 
   // ---- fc2: h2^T += W2 . h1^T; stage j takes k-steps KPS j ..; their B operands double as the
   // h1 operand stores (split: the last stage also stores the zero k-step 7) ----
-  int stores = xst;
+  vt.add(xst);
   static_for_vh<0, NS2>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
-    const char* stg = sync_late(ns1 + j, stores);
+    const char* stg = sync_late(ns1 + j);
     Frag b[KPS];
 #pragma unroll
     for (int e = 0; e < KPS; ++e) {
       const int k16 = KPS * j + e;
       b[e] = b_operand<DT>(acc1[k16 >> 1], k16 & 1);
-      st_op<DT>(rs_h1, v128, 16 * k16 * EB, b[e]);
+      sto(rs_h1, v128, 16 * k16 * EB, b[e]);
     }
-    stores = KPS * (S3 ? 2 : 1);
     if constexpr (S3 && j == NS2 - 1) {
-      st_op<DT>(rs_h1, v128, 16 * 7 * EB, b_operand<DT>(acc1[3], 1));
-      stores += 2;
+      sto(rs_h1, v128, 16 * 7 * EB, b_operand<DT>(acc1[3], 1));
     }
     ring_mma<DT, 4 * KPS, (S3 ? 1 : 2)>(stg, lane, [&](int i) { return i; },
                                         [&](int i, const Frag& w) __attribute__((always_inline)) {
@@ -307,7 +338,7 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
   f32x16 mu = f32x16{};
   static_for_vh<0, NS3>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
-    const char* stg = sync_late(e2 + j, j == 0 ? stores : 0);
+    const char* stg = sync_late(e2 + j);
     constexpr int NF = S3 ? 4 : 8;
     Frag b[NF];
 #pragma unroll
@@ -479,22 +510,25 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
             fa[q] = get(Hp, PH_HP, 128, 32 * tt, 2 * k2 + q, true);
             fb[q] = get(Dp, PH_DP, 64, 0, 2 * k2 + q, false);
           }
+          ph_settle<DT>(fa, fb);
 #pragma unroll
           for (int q = 0; q < 2; ++q) dw = V::mma(dw, fb[q], fa[q]);   // A = dL/dmu^T, B = h2: D[dim][feature]
           __builtin_amdgcn_sched_barrier(0);
         }
-        // feature 32 w + (l & 31), dim ph_dim(i, h): dst[part_dw + dim * 128 + feature]
+        // feature 32 w + (l & 31), dim ph_dim(i, h): dst[part_dw + dim * 128 + feature] (all 32
+        // dims: those past A are zero — one store per register, a constant count)
         const unsigned base = (unsigned)((size_t)blockIdx.x * a.npart + a.part_dw + 32 * wave + r) * 4u;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int d = ph_dim(i, h);
-          if (d < A) __builtin_amdgcn_raw_buffer_store_b32(dw[i], rs_part, base + (unsigned)d * 512u, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dw[i]), rs_part, base + (unsigned)d * 512u, 0, 0);
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
+    vt.add(16);   // this wave's dW_mu stores (in its round)
   }
 
   // ---- dgrad mu: g2 = (W3^T dL/dmu) (1 - h2^2) over the 4 h2 tiles ----
@@ -514,7 +548,7 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
   if constexpr (S3) {
     static_for_vh<0, NG3>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      const char* stg = sync_late(e3 + j, 0);
+      const char* stg = sync_late(e3 + j);
       f32x16 gq[2] = {f32x16{}, f32x16{}};
       ring_mma<DT, 4, 2>(stg, lane, [&](int i) { return i; },
                          [&](int i, const Frag& w) __attribute__((always_inline)) {
@@ -524,7 +558,7 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
       g2_ops(2 * j + 1, gq[1]);
     });
   } else {
-    const char* stg = sync_late(e3, 0);
+    const char* stg = sync_late(e3);
     f32x16 ga[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) ga[t] = f32x16{};
@@ -538,20 +572,17 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
 
   // ---- dgrad fc2: g1 = (W2^T g2) (1 - h1^2), two passes of 2 h1 tiles; the g2 operand stores
   // ride along (one k-step per split step / two per bf16 step) ----
-  stores = 0;
   static_for_vh<0, 2>([&](auto pc) __attribute__((always_inline)) {
     constexpr int pass = decltype(pc)::value;
     f32x16 gp[2] = {f32x16{}, f32x16{}};
     static_for_vh<0, NG2 / 2>([&](auto jc) __attribute__((always_inline)) {
       constexpr int jj = decltype(jc)::value, j = pass * (NG2 / 2) + jj;
-      const char* stg = sync_late(eg3 + j, stores);
+      const char* stg = sync_late(eg3 + j);
       if constexpr (S3) {
-        st_op<DT>(rs_g2, v128, 16 * j * EB, j < NGB ? gb[j < NGB ? j : 0] : Frag{});
-        stores = 2;
+        sto(rs_g2, v128, 16 * j * EB, j < NGB ? gb[j < NGB ? j : 0] : Frag{});
       } else {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) st_op<DT>(rs_g2, v128, 16 * (2 * j + e) * EB, gb[2 * j + e]);
-        stores = 2;
+        for (int e = 0; e < 2; ++e) sto(rs_g2, v128, 16 * (2 * j + e) * EB, gb[2 * j + e]);
       }
       // (split: the last stage's k-step 7 is zero: its 2 fragments are not multiplied)
       constexpr int NF = (S3 && jj == NG2 / 2 - 1) ? 2 : 4 * KPS;
@@ -567,14 +598,14 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) g1[i] = gp[tt][i] * __builtin_fmaf(-acc1[t][i], acc1[t][i], 1.f);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) st_op<DT>(rs_g1, v128, (32 * t + 16 * s) * EB, b_operand<DT>(g1, s));
+      for (int s = 0; s < 2; ++s) sto(rs_g1, v128, (32 * t + 16 * s) * EB, b_operand<DT>(g1, s));
     }
-    stores += 4 * (S3 ? 2 : 1);   // (a count past 8 waits longer: safe)
   });
 
   // ---- per-workgroup partials (fixed order over the waves): loss terms (not column 1: the
   // value head's) and dlog_std ----
-  WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
+  // (no DMA is in flight: the last stage's sync waited for all of them; the operand stores may
+  // drain after the waves end)
   float* dst = a.part + (size_t)blockIdx.x * a.npart;
   if (tid < 8 + A && tid != 1) {
     dst[tid] = ((red[tid] + red[PH_RED + tid]) + red[2 * PH_RED + tid]) + red[3 * PH_RED + tid];

@@ -101,20 +101,39 @@ DEV typename VT<DT>::Frag b_operand(const f32x16& x, int s) {
   }
 }
 
-// s_waitcnt vmcnt(n) for a runtime n in [0, 8] (undercounting is safe)
+// s_waitcnt vmcnt(n) for a runtime n (counts past 23 wait for 23: undercounting only waits longer)
 DEV void wait_vm_rt(int n) {
   switch (n) {
-    case 0: WAIT_VMCNT(0); break;
-    case 1: WAIT_VMCNT(1); break;
-    case 2: WAIT_VMCNT(2); break;
-    case 3: WAIT_VMCNT(3); break;
-    case 4: WAIT_VMCNT(4); break;
-    case 5: WAIT_VMCNT(5); break;
-    case 6: WAIT_VMCNT(6); break;
-    case 7: WAIT_VMCNT(7); break;
-    default: WAIT_VMCNT(8); break;
+#define T32_VMC(k) \
+  case k: WAIT_VMCNT(k); break;
+    T32_VMC(0) T32_VMC(1) T32_VMC(2) T32_VMC(3) T32_VMC(4) T32_VMC(5) T32_VMC(6) T32_VMC(7)
+    T32_VMC(8) T32_VMC(9) T32_VMC(10) T32_VMC(11) T32_VMC(12) T32_VMC(13) T32_VMC(14) T32_VMC(15)
+    T32_VMC(16) T32_VMC(17) T32_VMC(18) T32_VMC(19) T32_VMC(20) T32_VMC(21) T32_VMC(22)
+#undef T32_VMC
+    default: WAIT_VMCNT(23); break;
   }
 }
+
+// Counted-wait bookkeeping of a 3-stage ring past its runtime-length prologue: n counts every
+// vector-memory instruction the wave issues (refills, X loads AND operand stores); ma / mb are
+// the counts right after the two pending ring batches (stage st, st + 1).  The sync of stage st
+// waits with exactly the instructions issued after its batch still in flight (vmcnt counts in
+// issue order on gfx9-family parts): a wait that left the younger stores out would wait for them
+// to reach memory, an op left uncounted only makes the wait longer.  In straight-line (unrolled)
+// code every count folds to a constant: one s_waitcnt, no switch.
+struct VmTrack {
+  int n, ma, mb;
+  // entering with stage st's batch `older` instructions back and stage st + 1's `older1`
+  DEV explicit VmTrack(int older, int older1 = 0) : n(0), ma(-older), mb(-older1) {}
+  DEV void add(int k) { n += k; }
+  DEV int younger() const { return n - ma; }
+  // after stage st's sync: the refill (stage st + 2, `k` instructions) or none
+  DEV void advance(int k) {
+    n += k;
+    ma = mb;
+    mb = n;
+  }
+};
 
 template <int B, int E, typename F>
 DEV void static_for_vh(F&& f) {
@@ -159,7 +178,7 @@ DEV void ring_mma(const char* stg, int lane, SLOT&& slot, F&& f) {
 // of each 16-lane group (measured: the bf16 value head's g1 rows, scripts/debug_t32_nan.py), a
 // store-data WAR the compiler did not pad here
 DEV void st_b128(u32x4v v, __amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 2);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
   asm volatile("s_nop 1" ::"v"(v));
 }
 template <int DT>

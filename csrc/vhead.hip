@@ -180,6 +180,10 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
 
   constexpr int NS2 = vh_ns2<DT>(), NSD = TRAIN ? vh_nsd<DT>() : 0;
   const int ntot = ns1 + NS2 + NSD;
+  // the loss inputs land before the stream starts (one load latency per workgroup): the asm
+  // redefines them, so no compiler-inserted wait for them can fall inside the counted stream —
+  // where it would also wait for every in-flight DMA and operand store
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(l_ret), "+v"(l_vold)::"memory");
   // ---- prime: X stages 0, 1 and ring stages 0, 1 (the launcher checks ns1 >= 3) ----
   static_assert(VH_S == 3 && VH_XS == 3, "the wait counts below are written for 3-stage rings");
   VH_STAMP(0);
@@ -195,9 +199,9 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc2[t] = f32x16{};
 
-  // one stream step's sync: this wave's DMAs of ring stage st by count (`younger` = its DMA
-  // instructions issued after that stage's batch may stay in flight; each step issues [X, refill]),
-  // then the barrier: every wave's, and everyone is done with stage st - 1
+  // one stream step's sync: this wave's DMAs of ring stage st by count (`younger` = its vector
+  // memory instructions issued after that stage's batch may stay in flight), then the barrier:
+  // every wave's stage st landed, and everyone is done with stage st - 1
   auto sync = [&](int younger) __attribute__((always_inline)) {
     asm volatile("" ::: "memory");
     wait_vm_rt(younger);
@@ -205,11 +209,24 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
-  // steps past fc1: the previous step issued one refill (VH_GL) if it had a stage to refill
+  // from the last two fc1 steps on: the counts by VmTrack (entering with stage ns1 - 2's batch
+  // X(ns1 - 1) + R(ns1 - 1) back)
+  VmTrack vt(1 + VH_GL);
+  constexpr int SP = DT == DT_S3 ? 2 : 1;   // store instructions per operand fragment
+  auto sync_t = [&](int st) __attribute__((always_inline)) {
+    sync(vt.younger());
+    const bool refill = st + 2 < ntot;
+    if (refill) issue(st + 2);
+    vt.advance(refill ? VH_GL : 0);
+  };
   auto sync_late = [&](int st) __attribute__((always_inline)) {
-    sync(st + 1 < ntot ? VH_GL : 0);
-    if (st + 2 < ntot) issue(st + 2);
+    sync_t(st);
     return ring + (st % VH_S) * VH_SB;
+  };
+  // an operand store, counted
+  auto sto = [&](__amdgpu_buffer_rsrc_t rs, unsigned vrow, unsigned fsoff, const Frag& f) __attribute__((always_inline)) {
+    st_op<DT>(rs, vrow, fsoff, f);
+    vt.add(SP);
   };
   constexpr int G1 = DT == DT_S3 ? 2 : 4;   // fragments per LDS read group (<= 8 reads in flight)
   auto fc1 = [&](const char* stg, int st) __attribute__((always_inline)) {
@@ -230,11 +247,9 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
     fc1(ring + (st % VH_S) * VH_SB, st);
   }
   // the last two fc1 steps refill with fc2 stages 0, 1 (no more X)
-  sync(1 + VH_GL);
-  issue(ns1);
+  sync_t(ns1 - 2);
   fc1(ring + ((ns1 - 2) % VH_S) * VH_SB, ns1 - 2);
-  sync(VH_GL);
-  issue(ns1 + 1);
+  sync_t(ns1 - 1);
   fc1(ring + ((ns1 - 1) % VH_S) * VH_SB, ns1 - 1);
   VH_STAMP(1);
   {
@@ -265,7 +280,7 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
 #pragma unroll
     for (int e = 0; e < 2 * KPS; ++e) {
       b[e] = b_operand<DT>(acc[KPS * j + (e >> 1)], e & 1);
-      if constexpr (TRAIN) st_op<DT>(rs_h1, v512, (256 * q + 32 * (KPS * j + (e >> 1)) + 16 * (e & 1)) * EB, b[e]);
+      if constexpr (TRAIN) sto(rs_h1, v512, (256 * q + 32 * (KPS * j + (e >> 1)) + 16 * (e & 1)) * EB, b[e]);
     }
     const char* stg = sync_late(ns1 + j);
     // (fc2 holds h1 and the fc2 accumulators: one / two fragments per read group)
@@ -377,11 +392,9 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) gb[2 * t + s] = b_operand<DT>(g2, s);
     }
+    // (unconditional stores of a selected fragment: the counted waits stay compile-time constants)
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int qq = 0; qq < 2; ++qq)
-        if (q == qq) st_op<DT>(rs_g2, v128, 16 * (4 * qq + k) * EB, gb[4 * qq + k]);
+    for (int k = 0; k < 4; ++k) sto(rs_g2, v128, 16 * (4 * q + k) * EB, q ? gb[4 + k] : gb[k]);
 
     VH_STAMP(4);
     // ---- dgrad fc2: g1 = (W2^T g2) (1 - h1^2) over this wave's h1 tiles, two per pass ----
@@ -407,13 +420,14 @@ __global__ __launch_bounds__(VH_WAVES * 64, 1) void vhead_kernel(MlpArgs a) {
         for (int i = 0; i < 16; ++i) g1[i] = ga[tt][i] * __builtin_fmaf(-hv[i], hv[i], 1.f);
 #pragma unroll
         for (int s = 0; s < 2; ++s)
-          st_op<DT>(rs_g1, v512, (256 * q + 32 * (2 * ip + tt) + 16 * s) * EB, b_operand<DT>(g1, s));
+          sto(rs_g1, v512, (256 * q + 32 * (2 * ip + tt) + 16 * s) * EB, b_operand<DT>(g1, s));
       }
       if constexpr (ip == 1) VH_STAMP(5);
     });
     VH_STAMP(6);
     // ---- per-workgroup partials (fixed order): the value loss (column 1) and dW_v ----
-    WAIT_VMCNT(0);   // no DMA may outlive the workgroup's LDS
+    // (no DMA is in flight: the last stage's sync waited for all of them; the operand stores may
+    // drain after the waves end)
     float* dst = a.part + (size_t)blockIdx.x * a.npart;
     if (tid < 128) {
       const int k = tid, t = k >> 5, rr2 = k & 31;

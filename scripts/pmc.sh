@@ -6,13 +6,14 @@ OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT/pmc"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 rocprofv3 -L > "$OUT/pmc/counters_list.txt" 2>&1 || true
-REGEX=${REGEX:-'mlp_head|mlp_train|wgrad_kernel|rollout_kernel|mlp_value|gather_adam'}
+REGEX=${REGEX:-'mlp_head|mlp_train|wgrad_kernel|rollout_kernel|mlp_value|gather_adam|vhead|phead'}
 i=0
-for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
-         "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU" \
-         "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
-         "TCC_HIT_sum TCC_MISS_sum" \
-         "FETCH_SIZE"; do
+for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
+         "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_INSTS_SALU" \
+         "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+         "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum" \
+         "FETCH_SIZE" \
+         "WRITE_SIZE"; do
   i=$((i+1))
   echo "== pass $i: $P"
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $P --kernel-include-regex "$REGEX" -d "$OUT/pmc/p$i" -o run \

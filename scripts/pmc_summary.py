@@ -34,4 +34,7 @@ for k in agg:
           f"active {g('SQ_ACTIVE_INST_ANY') / tot:.2f}")
     print(f"   insts/dispatch: MFMA {g('SQ_INSTS_MFMA'):.3g} VALU {g('SQ_INSTS_VALU'):.3g} LDS {g('SQ_INSTS_LDS'):.3g}; "
           f"LDS bank-conflict/active {g('SQ_LDS_BANK_CONFLICT') / max(g('SQ_LDS_IDX_ACTIVE'), 1):.2f}")
-    print(f"   L2 hit {g('TCC_HIT_sum') / (g('TCC_HIT_sum') + g('TCC_MISS_sum')):.2f}; FETCH_SIZE {g('FETCH_SIZE') / 1024:.1f} MB")
+    print(f"   L2 hit {g('TCC_HIT_sum') / (g('TCC_HIT_sum') + g('TCC_MISS_sum')):.2f}; FETCH_SIZE {g('FETCH_SIZE') / 1024:.1f} MB"
+          f"; WRITE_SIZE {g('WRITE_SIZE') / 1024:.1f} MB")
+    print(f"   SQ_BUSY_CYCLES {g('SQ_BUSY_CYCLES'):.3g}; SALU {g('SQ_INSTS_SALU'):.3g}; VMEM rd {g('SQ_INSTS_VMEM_RD'):.3g} "
+          f"wr {g('SQ_INSTS_VMEM_WR'):.3g}; wait_inst_lds/wave-cycles {g('SQ_WAIT_INST_LDS') / tot:.3f}")
