@@ -131,7 +131,7 @@ def main():
     ap.add_argument("--dist-timeout-s", type=float, default=300.0,
                     help="bound of every wait on peers (collective watchdog; abort + non-zero exit)")
     ap.add_argument("--heartbeat-timeout-s", type=float, default=60.0)
-    ap.add_argument("--t32", default="auto", choices=["auto", "off", "value", "both"],
+    ap.add_argument("--t32", default="auto", choices=["auto", "off", "value", "policy", "both"],
                     help="update head kernels: the 32x32 transposed-chain kernels (csrc/vhead.hip, csrc/phead.hip) "
                          "for none / the value head / both heads; auto = the Params defaults")
     ap.add_argument("--verbose", action="store_true")
@@ -170,7 +170,7 @@ def main():
                         phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
         if args.t32 != "auto":
             p.vhead_kernel = args.t32 in ("value", "both")
-            p.phead_kernel = args.t32 == "both"
+            p.phead_kernel = args.t32 in ("policy", "both")
         w = DPPOWorker(p, ctx)
         m = {}
         for i in range(args.warmup):

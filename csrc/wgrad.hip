@@ -47,27 +47,31 @@ constexpr size_t wgrad_lds_bytes() { return (size_t)S * WG_SLOTS * wgrad_frag_by
 // half's transposed reads that share banks) get distinct chunk pairs — conflict-free
 __host__ __device__ inline int wgrad_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
 
-// an MFMA operand (lane l: feature 16 s + (l & 15) of the quadrant, rows 8 (l >> 4) .. + 7) from a
-// row-major quadrant image at qb: two ds_read_b64_tr_b16 of 4 rows each (lane 4 q' + p' of a 16-lane
-// group addresses row q', columns 4 p' .. 4 p' + 3; lane i receives column i) per precision part
-template <int DT>
-DEV typename Prec<DT>::Frag rm_frag(const char* qb, int s, int lane) {
-  typedef __attribute__((ext_vector_type(4))) short s16x4;
+// Row-major operands: lane l's MFMA operand (feature 16 s + (l & 15) of a quadrant, rows 8 (l >> 4)
+// .. + 7) is two ds_read_b64_tr_b16 of 4 rows each (lane 4 q' + p' of a 16-lane group addresses row
+// q', columns 4 p' .. 4 p' + 3; lane i receives column i) per precision part.  rm_off: the byte
+// offset (within a stage) of read `sub` of slot f (quadrant slots f & ~3 .. + 3, s = f & 3)
+DEV unsigned rm_off(int f, int sub, int lane, int FB) {
   const int li = lane & 15, g = lane >> 4;
-  auto rd = [&](const char* base, int sub) __attribute__((always_inline)) {
-    const int row = 8 * g + 4 * sub + (li >> 2), col = 16 * s + 4 * (li & 3);
-    const char* p = base + row * 128 + (((col >> 3) ^ wgrad_swz(row)) << 4) + (col & 7) * 2;
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  const int row = 8 * g + 4 * sub + (li >> 2), col = 16 * (f & 3) + 4 * (li & 3);
+  return (unsigned)((f & ~3) * FB + row * 128 + (((col >> 3) ^ wgrad_swz(row)) << 4) + (col & 7) * 2);
+}
+// the operand from its two precomputed read offsets (split: the lo image 4 KiB on)
+template <int DT>
+DEV typename Prec<DT>::Frag rm_frag_at(const char* st, const unsigned (&o)[2]) {
+  typedef __attribute__((ext_vector_type(4))) short s16x4;
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  auto rd = [&](unsigned off) __attribute__((always_inline)) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(st + off));
   };
   auto cat = [&](s16x4 a0, s16x4 a1) __attribute__((always_inline)) {
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
     const s16x8 v{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
     return *reinterpret_cast<const bf16x8*>(&v);
   };
   if constexpr (IsSplit<DT>::value) {
-    return S3Frag{cat(rd(qb, 0), rd(qb, 1)), cat(rd(qb + 4096, 0), rd(qb + 4096, 1))};
+    return S3Frag{cat(rd(o[0]), rd(o[1])), cat(rd(o[0] + 4096), rd(o[1] + 4096))};
   } else {
-    return cat(rd(qb, 0), rd(qb, 1));
+    return cat(rd(o[0]), rd(o[1]));
   }
 }
 
@@ -142,6 +146,24 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   constexpr bool RMOK = DT == DT_S3 || DT == DT_BF16;   // (fp32 / e4m3 operands are fragment-major only)
   const bool g_rm = RMOK && a.g_rm[tk.layer] != 0, x_rm = RMOK && a.x_rm[tk.layer] != 0;
   const int wn = wave / tk.kq, wk = wave - (wave / tk.kq) * tk.kq;
+  // per-lane byte offsets (within a stage) of the wave's 4 dY and 4 X fragments: fragment-major
+  // [0] = the lane's 16 bytes; row-major [0] / [1] = the two 4-row transposed reads (rm_off)
+  unsigned oa[4][2], ob[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    auto fill = [&](unsigned (&o)[2], int f, bool rm) {
+      if (RMOK && rm) {
+        o[0] = rm_off(f, 0, lane, FB);
+        o[1] = rm_off(f, 1, lane, FB);
+      } else {
+        o[0] = IsSplit<DT>::value ? (unsigned)(f * FB + (lane >> 5) * 1024 + (lane & 31) * 16)
+                                  : (unsigned)(f * FB + lane * 8 * (int)sizeof(T));
+        o[1] = 0;
+      }
+    };
+    fill(oa[i], wn * 4 + i, g_rm);
+    fill(ob[i], NF + wk * 4 + i, x_rm);
+  }
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -186,20 +208,21 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
             acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8[i], b8[j], acc[i][j], 0, 0, 0, 127, 0, 127);
         continue;
       }
-      auto lds_frag = [&](int f, bool rm) {
+      // (lane offsets precomputed per task: the loop adds the stage base only)
+      auto lds_frag = [&](int i, bool rm, const unsigned (&o)[4][2]) {
         if constexpr (DT == DT_S3 || DT == DT_BF16)
-          if (rm) return rm_frag<DT>(st + (f & ~3) * FB, f & 3, lane);
+          if (rm) return rm_frag_at<DT>(st, o[i]);
         if constexpr (IsSplit<DT>::value) {
-          const char* b = st + f * FB + (lane >> 5) * 1024 + (lane & 31) * 16;
+          const char* b = st + o[i][0];
           return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + 512)};
         } else {
-          return P::load(reinterpret_cast<const T*>(st + f * FB) + lane * 8);
+          return P::load(reinterpret_cast<const T*>(st + o[i][0]));
         }
       };
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        af[i] = lds_frag(wn * 4 + i, g_rm);
-        bf[i] = lds_frag(NF + wk * 4 + i, x_rm);
+        af[i] = lds_frag(i, g_rm, oa);
+        bf[i] = lds_frag(i, x_rm, ob);
       }
       if constexpr (LATE) issue(k + S - 1);
 #pragma unroll

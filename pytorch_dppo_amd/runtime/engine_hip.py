@@ -168,7 +168,7 @@ class HipEngine:
         # g2p row-major, and the observation operand of p_fc1 AND v_fc1 row-major — x_buf itself
         # for a full-batch step (no x^T anywhere: the rollout skips writing it), the kernel's
         # gathered rows in xT for a minibatch
-        self.phead = (self.vhead and bool(params.phead_kernel)
+        self.phead = (self.heads and not self.fp8 and bool(params.phead_kernel)
                       and bool(self.ext.phead_train_applies(self.dt, self.layout, A)))
         # the gradient-amax ring: 3 slots x 4 tensors x 64 sub-slot lines of 32 dwords (csrc/kernels.h)
         self.q8_amax = torch.zeros(3 * 4 * Q8_SUB * 32, dtype=torch.int32, device=device)

@@ -20,7 +20,7 @@ from pytorch_dppo_amd.parallel.dist import init_single_rank_collective  # noqa: 
 from pytorch_dppo_amd.runtime.launcher import free_port  # noqa: E402
 from pytorch_dppo_amd.runtime.worker import DPPOWorker  # noqa: E402
 
-ARMS = {"h16": (False, False), "v32": (True, False), "pv32": (True, True)}
+ARMS = {"h16": (False, False), "v32": (True, False), "p32": (False, True), "pv32": (True, True)}
 
 
 def main():

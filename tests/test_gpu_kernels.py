@@ -193,8 +193,9 @@ def test_vhead_update_matches_16x16_head_update(dtype, loss, value_loss, mb):
 
 
 @pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
-@pytest.mark.parametrize("loss,mb", [("ppo", None), ("ppo", 1024), ("ppo", 1000), ("dppo_ref", 768)])
-def test_phead_update_matches_16x16_head_update(dtype, loss, mb):
+@pytest.mark.parametrize("loss,mb,vh", [("ppo", None, True), ("ppo", 1024, True), ("ppo", 1000, False),
+                                        ("dppo_ref", 768, True), ("ppo", None, False)])
+def test_phead_update_matches_16x16_head_update(dtype, loss, mb, vh):
     """The policy head's update on the 32x32 transposed-chain kernel (csrc/phead.hip: row-major
     h1p / g1p / g2p, the observation operand of both fc1 layers row-major — x_buf itself for a
     full batch (mb None), the kernel's gathered rows for a minibatch; dW_mu by MFMA over the
@@ -208,10 +209,10 @@ def test_phead_update_matches_16x16_head_update(dtype, loss, mb):
     res = {}
     for ph in (True, False):
         p = ppo_preset(**kw) if loss == "ppo" else dppo_preset(**kw)
-        p.vhead_kernel = ph
+        p.vhead_kernel = ph and vh     # (vh False: the policy kernel beside the 16x16 value head)
         p.phead_kernel = ph
         eng, model, _, _ = _engine(p)
-        assert eng.phead == ph and eng.vhead == ph
+        assert eng.phead == ph and eng.vhead == (ph and vh)
         xq = _fill_buffer(eng, model)
         idx = None if mb is None else torch.randperm(eng.N, generator=torch.Generator().manual_seed(5))[:mb]
         eng.begin_update()
@@ -251,6 +252,7 @@ def test_wgrad_row_major_operands_bit_identical_to_fragment_major(dtype):
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=256, exploration_size=256 * 16,
                     batch_size=256 * 16, dtype=dtype, update_kernels="heads")
     p.phead_kernel = False   # the value layers' operands only (v_fc1's X stays fragment-major)
+    p.vhead_kernel = True
     eng, model, _, _ = _engine(p)
     assert eng.vhead
     _fill_buffer(eng, model)
@@ -278,7 +280,7 @@ def test_wgrad_row_major_operands_bit_identical_to_fragment_major(dtype):
     b["slab"].zero_()
     eng.ext.wgrad(eng._wgrad_dt(), wg_g, wg_x, eng.g_rows, eng.x_rows, eng.ldT, b["tasks"],
                   b["tasks_host"], b["slab"], *eng._q8_args(), [0] * 12)
-    assert torch.equal(slab_rm, b["slab"])
+    assert torch.equal(slab_rm, b["slab"]), (slab_rm - b["slab"]).abs().max().item()
 
 
 def _torch_rollout(params, model, seed_state_from):
