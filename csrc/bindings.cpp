@@ -172,7 +172,7 @@ RolloutArgs rollout_args(int64_t dt, int64_t rows, torch::Tensor state, torch::T
   }
   a.epstat = epstat.data_ptr<float>();
   if (g_roll_tstamp != nullptr) {
-    TORCH_CHECK(g_roll_tstamp_numel >= (int64_t)nblk * 8 * 8, "rollout tstamp buffer too small");
+    TORCH_CHECK(g_roll_tstamp_numel >= (int64_t)nblk * 8 * 16, "rollout tstamp buffer too small ([blk][8 waves][16])");
     a.tstamp = g_roll_tstamp;
   }
   return a;

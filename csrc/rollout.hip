@@ -254,7 +254,8 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   using GT = std::conditional_t<SPLIT, float, typename PX::T>;
   // phase timeline (diagnostics, a.tstamp != null): per-wave shader-clock cycles summed over
   // the steps for each phase, written by lane 0 of every wave of every workgroup
-  unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // (slots 7-10: the per-step filter's moments / reduce / gather / barrier, SN only)
+  unsigned long long ph_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long ph_t = a.tstamp ? __builtin_amdgcn_s_memtime() : 0ull;
 #define PH(i)                                                     \
   do {                                                            \
@@ -352,14 +353,18 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
         };
         if (a.kind == 1) moments(std::integral_constant<int, 1>{});
         else moments(std::integral_constant<int, 0>{});
+        PH(7);
         // features blk + nblk * (w + NW j) on wave w: the features of this workgroup are merged
         // by its waves concurrently
         bool okr = true;
         for (int dfeat = (int)blockIdx.x + (int)gridDim.x * wave; okr && dfeat < O; dfeat += (int)gridDim.x * NW)
           okr = sn_reduce(a, dfeat, (int)gridDim.x, step, lane, shs);
         if (!okr && lane == 0) *sn_fail = 1;
+        PH(8);
         if (wave == 0 && !sn_gather(a, step, lane, nm, ninv) && lane == 0) *sn_fail = 1;
+        PH(9);
         __syncthreads();
+        PH(10);
         if (*sn_fail) {   // a peer never published: give up (the host raises)
           if (tid == 0) __hip_atomic_store(a.sn_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           return;
@@ -573,7 +578,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   __syncthreads();
   if (a.tstamp != nullptr && lane == 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a.tstamp[((size_t)blockIdx.x * NW + wave) * 8 + i] = ph_acc[i];
+    for (int i = 0; i < 11; ++i) a.tstamp[((size_t)blockIdx.x * NW + wave) * 16 + i] = ph_acc[i];
   }
 #undef PH
   // ---- write back env state, episode trackers, partial moments / episode stats ----

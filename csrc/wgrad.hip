@@ -56,9 +56,21 @@ DEV unsigned rm_off(int f, int sub, int lane, int FB) {
   const int row = 8 * g + 4 * sub + (li >> 2), col = 16 * (f & 3) + 4 * (li & 3);
   return (unsigned)((f & ~3) * FB + row * 128 + (((col >> 3) ^ wgrad_swz(row)) << 4) + (col & 7) * 2);
 }
-// the operand from its two precomputed read offsets (split: the lo image 4 KiB on)
+// Split-bf16 row-major quadrants keep the memory's [8 hi | 8 lo] groups: a row's 64 features are 256
+// contiguous bytes, DMA'd 4 rows per instruction (16 lanes x 16 B per row: whole 256-byte row
+// segments, not 16-byte pieces at a 32-byte stride), the 16 chunks of a row XOR-swizzled by
+// wgrad_swz16(row) so the 16 rows of a transposed read meet each 16-byte bank group at most twice
+// (the 2-cycle minimum of a 512-byte read)
+__host__ __device__ inline int wgrad_swz16(int row) { return ((row & 3) << 2) | ((row >> 3) & 3); }
+DEV unsigned rm_off_s3(int f, int sub, int part, int lane, int FB) {
+  const int li = lane & 15, g = lane >> 4;
+  const int row = 8 * g + 4 * sub + (li >> 2), col = 16 * (f & 3) + 4 * (li & 3);
+  const int pos = ((col >> 3) * 2 + part) ^ wgrad_swz16(row);
+  return (unsigned)((f & ~3) * FB + row * 256 + pos * 16 + (col & 7) * 2);
+}
+// the operand from its precomputed read offsets (split: hi reads o[0], o[1], lo reads o[2], o[3])
 template <int DT>
-DEV typename Prec<DT>::Frag rm_frag_at(const char* st, const unsigned (&o)[2]) {
+DEV typename Prec<DT>::Frag rm_frag_at(const char* st, const unsigned (&o)[4]) {
   typedef __attribute__((ext_vector_type(4))) short s16x4;
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   auto rd = [&](unsigned off) __attribute__((always_inline)) {
@@ -69,7 +81,7 @@ DEV typename Prec<DT>::Frag rm_frag_at(const char* st, const unsigned (&o)[2]) {
     return *reinterpret_cast<const bf16x8*>(&v);
   };
   if constexpr (IsSplit<DT>::value) {
-    return S3Frag{cat(rd(o[0]), rd(o[1])), cat(rd(o[0] + 4096), rd(o[1] + 4096))};
+    return S3Frag{cat(rd(o[0]), rd(o[1])), cat(rd(o[2]), rd(o[3]))};
   } else {
     return cat(rd(o[0]), rd(o[1]));
   }
@@ -94,9 +106,10 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   // k0/16 + f - NF.  Wave w DMAs slots C*w .. C*w + C-1 (a slot >= F re-loads fragment f mod F).
   // FM operands: a fragment is contiguous (FB bytes per k-step).  Row-major operands (RM: the
   // transposed-chain value head's h1 / g1 / g2, csrc/vhead.hip; row length a.g_rm / a.x_rm): a
-  // quadrant's 4 slots hold its [32 rows][64 features] image per k-step (split: hi 4 KiB | lo 4 KiB),
-  // 128-byte rows with the 16-byte chunks XOR-swizzled by wgrad_swz(row), DMA'd row by row (8 rows
-  // per instruction) and read back transposed (ds_read_b64_tr_b16).
+  // quadrant's 4 slots hold its [32 rows][64 features] image per k-step — bf16: 128-byte rows, the
+  // 16-byte chunks XOR-swizzled by wgrad_swz(row), 8 rows per DMA instruction; split-bf16: the
+  // memory's 256-byte [8 hi | 8 lo] rows, wgrad_swz16, 4 rows per instruction — read back
+  // transposed (ds_read_b64_tr_b16).
   const char* srcp[C][NI];
   size_t kstride[C];
   int dst[C];
@@ -121,10 +134,15 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
 #pragma unroll
       for (int hh = 0; hh < NI; ++hh) {
         const int n = NI * sq + hh;                   // 1 KiB DMA instruction of the quadrant image
-        const int part = IsSplit<DT>::value ? n >> 2 : 0, rb = IsSplit<DT>::value ? (n & 3) : n;
-        const int row = 8 * rb + (lane >> 3);
-        const int c = (lane & 7) ^ wgrad_swz(row);
-        srcp[q][hh] = ob + ((size_t)(tk.m0 + row) * rm + f0 + 8 * c) * sizeof(T) + 16 * part;
+        if constexpr (IsSplit<DT>::value) {           // rows 4 n .. 4 n + 3, 256 bytes each
+          const int row = 4 * n + (lane >> 4);
+          const int c = (lane & 15) ^ wgrad_swz16(row);
+          srcp[q][hh] = ob + ((size_t)(tk.m0 + row) * rm + f0) * sizeof(T) + 16 * c;
+        } else {                                      // rows 8 n .. 8 n + 7, 128 bytes each
+          const int row = 8 * n + (lane >> 3);
+          const int c = (lane & 7) ^ wgrad_swz(row);
+          srcp[q][hh] = ob + ((size_t)(tk.m0 + row) * rm + f0 + 8 * c) * sizeof(T);
+        }
       }
       kstride[q] = (size_t)32 * rm * sizeof(T);
     }
@@ -148,17 +166,21 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   const int wn = wave / tk.kq, wk = wave - (wave / tk.kq) * tk.kq;
   // per-lane byte offsets (within a stage) of the wave's 4 dY and 4 X fragments: fragment-major
   // [0] = the lane's 16 bytes; row-major [0] / [1] = the two 4-row transposed reads (rm_off)
-  unsigned oa[4][2], ob[4][2];
+  unsigned oa[4][4], ob[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    auto fill = [&](unsigned (&o)[2], int f, bool rm) {
+    auto fill = [&](unsigned (&o)[4], int f, bool rm) {
+      o[1] = o[2] = o[3] = 0;
       if (RMOK && rm) {
-        o[0] = rm_off(f, 0, lane, FB);
-        o[1] = rm_off(f, 1, lane, FB);
+        if constexpr (IsSplit<DT>::value) {
+          for (int j = 0; j < 4; ++j) o[j] = rm_off_s3(f, j & 1, j >> 1, lane, FB);
+        } else {
+          o[0] = rm_off(f, 0, lane, FB);
+          o[1] = rm_off(f, 1, lane, FB);
+        }
       } else {
         o[0] = IsSplit<DT>::value ? (unsigned)(f * FB + (lane >> 5) * 1024 + (lane & 31) * 16)
                                   : (unsigned)(f * FB + lane * 8 * (int)sizeof(T));
-        o[1] = 0;
       }
     };
     fill(oa[i], wn * 4 + i, g_rm);
@@ -209,7 +231,7 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
         continue;
       }
       // (lane offsets precomputed per task: the loop adds the stage base only)
-      auto lds_frag = [&](int i, bool rm, const unsigned (&o)[4][2]) {
+      auto lds_frag = [&](int i, bool rm, const unsigned (&o)[4][4]) {
         if constexpr (DT == DT_S3 || DT == DT_BF16)
           if (rm) return rm_frag_at<DT>(st, o[i]);
         if constexpr (IsSplit<DT>::value) {

@@ -245,7 +245,12 @@ class HipEngine:
             if self.ldT <= self.x_buf.shape[0]:
                 xb = self.x_buf.view(-1)
                 self.wg_x_full = [xb, self.h1pT, self.h2pT, xb, self.h1vT, self.h2vT]
-        self._x_full = False   # the current step's X operand: x_buf (full batch, phead) or xT
+        # X side of p_fc1 / v_fc1 per step under the 32x32 policy head: "fm" = the rollout's
+        # fragment-major x^T (full batch), "buf" = x_buf's rows (full batch without it), "mb" = the
+        # rows the policy kernel gathered into xT (minibatch); rm_xfm = the flags of "fm"
+        self.rm_xfm = list(self.rm)
+        self.rm_xfm[6 + 0] = self.rm_xfm[6 + 3] = 0
+        self._x_mode = "fm"
         for buf, r in bias_rows:
             if self.q8:       # e4m3 bytes of the activation scale (Q8_SH = 256: exact)
                 storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), Q8_SH, 2)
@@ -301,7 +306,8 @@ class HipEngine:
         # the rollout can emit the full-batch x^T operand when the update is one full-batch step
         # (Q8: the policy kernel writes the e4m3 x^T in the first full-batch step instead)
         self.xT_from_rollout = (self.mb == self.N and self.ldT == self.N and E % 16 == 0 and self.N % 32 == 0
-                                and params.obs_norm_update == "rollout" and not self.q8 and not self.phead)
+                                and params.obs_norm_update == "rollout" and not self.q8
+                                and not (self.phead and self.wg_x_full is not self.wg_x))
         self._xT_valid = False   # True once a rollout wrote x^T for the current buffer contents
         self.s12 = torch.zeros(2, O, dtype=torch.float64, **dev)
         stats.device_merge = self._device_merge
@@ -437,9 +443,10 @@ class HipEngine:
 
     def _wgrad(self, b: Dict) -> None:
         """one wgrad launch over bucket b's tasks (Q8: e4m3 operands, the step's scales)"""
-        wg_x = self.wg_x_full if self._x_full else self.wg_x
+        wg_x = self.wg_x_full if (self.phead and self._x_mode == "buf") else self.wg_x
+        rm = self.rm_xfm if (not self.phead or self._x_mode == "fm") else self.rm
         self.ext.wgrad(self._wgrad_dt(), self.wg_g, wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
-                       b["tasks_host"], b["slab"], *self._q8_args(), self.rm)
+                       b["tasks_host"], b["slab"], *self._q8_args(), rm)
 
     def _w8(self):
         """fp8 mode: (e4m3 image, per-layer scales) for the value head's e4m3 fc1; else off"""
@@ -1005,10 +1012,19 @@ class HipEngine:
                 1 if p.std_convention == "var" else 0, 1 if first else 0, part.shape[1], h, part_dw,
                 1 if t32 else 0]
         if h == 0 and self.phead:
-            # full batch: the wgrad reads x_buf (no X rows written); a minibatch: the kernel
-            # gathers its observation rows into xT (row-major)
-            self._x_full = idx_t is self.empty and self.wg_x_full is not self.wg_x
-            xt_ready = self._x_full
+            # full batch: the rollout's fragment-major x^T if it wrote one (read by the wgrad as
+            # before), else x_buf's rows; a minibatch: the kernel gathers its observation rows
+            # into xT (row-major).  The kernel writes X rows only in the last case.
+            # (measured: the fragment-major x^T beside the row-major policy operands made the
+            # wgrad slower than x_buf's rows — 4.378 vs 4.214 ms per bf16x3 iteration, profiles/r5 —
+            # so x_buf's rows come first and the rollout writes no x^T when they can serve)
+            full = idx_t is self.empty
+            if full and self.wg_x_full is not self.wg_x:
+                self._x_mode, xt_ready = "buf", True
+            elif full and xt_ready:
+                self._x_mode = "fm"
+            else:
+                self._x_mode, xt_ready = "mb", False
 
         # fp8: the value head's fc1 on the e4m3 image; the policy's GEMMs only with fp8_policy_gemms
         w8 = self._w8() if (h == 1 or p.fp8_policy_gemms) else (self.no_u8, self.no_q)
@@ -1026,7 +1042,7 @@ class HipEngine:
             launch(-1)
             self._q8_cal[h] = True
         launch(self._q8_step)
-        if h == 0 and idx_t is self.empty:
+        if h == 0 and idx_t is self.empty and not self.phead:
             self._xT_valid = True   # the policy kernel wrote x^T of this buffer (full batch)
         if h == 0 and p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])   # train.py:164, before Adam moves it

@@ -46,7 +46,7 @@ def main():
     eng.begin_update()
     eng.grad(idx)
     torch.cuda.synchronize()
-    print("x_full", eng._x_full, flush=True)
+    print("x_mode", eng._x_mode, flush=True)
     ii = torch.arange(eng.N, device=DEV) if idx is None else idx.to(DEV)
     M = ii.numel()
     x = xq[ii].clone()

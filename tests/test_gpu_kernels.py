@@ -219,8 +219,8 @@ def test_phead_update_matches_16x16_head_update(dtype, loss, mb, vh):
         eng.grad(idx)
         torch.cuda.synchronize()
         res[ph] = (eng.grad_flat.clone(), eng.last_losses(), eng.mu_prev.clone())
-        if ph:
-            assert eng._x_full == (mb is None)
+        if ph:   # (no rollout wrote x^T: a full batch reads x_buf's rows)
+            assert eng._x_mode == ("buf" if mb is None else "mb")
         if ph and loss == "ppo":
             ii = torch.arange(eng.N, device=DEV) if idx is None else idx.to(DEV)
             g_ref, _ = _torch_grad(model, p, xq, eng, ii)
@@ -1188,7 +1188,7 @@ def test_bench_geometry_full_batch_gradient_matches_autograd(dtype, tol):
                     batch_size=4096 * 16, dtype=dtype, num_epoch=1)
     eng, model, env, stats = _engine(p)
     stats.observes(env.observe())
-    # (the 32x32 policy head reads the observation rows from x_buf itself: no x^T at all)
+    # (the 32x32 policy head reads the observation rows from x_buf: the rollout writes no x^T)
     assert (eng.xT_from_rollout or eng.phead) and eng.N == 65536
     assert sum(b["tasks_host"].numel() // 8 for b in eng.buckets) >= 200
     eng.rollout()
@@ -1197,6 +1197,7 @@ def test_bench_geometry_full_batch_gradient_matches_autograd(dtype, tol):
     eng.begin_update()
     assert eng._xT_valid or eng.phead
     eng.grad(None)
+    assert not eng.phead or eng._x_mode == "buf"
     xq = eng.decode(eng.x_buf)[:eng.N, :model.num_inputs]
     model.flat.grad = None
     mu, ls, v = model(xq)
