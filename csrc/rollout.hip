@@ -59,7 +59,29 @@ DEV float sn_val(u64 x) { return __uint_as_float((unsigned)x); }
 // formulas — and published as the (mean, 1/std) granules.  The values of a poll pass whose tags
 // all match are the values (no second read).  Returns false on a timeout.
 constexpr int SN_CHUNKS = 4;                 // workgroups per reducer lane: the grid is <= 256
-DEV bool sn_reduce(const RolloutArgs& a, int d, int nblk, int step, int lane, const float* shs) {
+// fp64 sum over the wave into lane 63 in a fixed order: an inclusive DPP scan (row_shr 1, 2, 4, 8
+// within each row of 16, then row_bcast 15 / 31 across the rows) — 12 DPP moves and 6 adds, not
+// 12 ds_bpermute round trips on the hand-off's critical path
+template <int CTRL, int ROWMASK>
+DEV double sn_dpp64(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const unsigned l2 = __builtin_amdgcn_update_dpp(0u, lo, CTRL, ROWMASK, 0xf, true);
+  const unsigned h2 = __builtin_amdgcn_update_dpp(0u, hi, CTRL, ROWMASK, 0xf, true);
+  return __hiloint2double((int)h2, (int)l2);
+}
+DEV double sn_wave_sum63(double v) {
+  v += sn_dpp64<0x111, 0xf>(v);   // row_shr:1
+  v += sn_dpp64<0x112, 0xf>(v);   // row_shr:2
+  v += sn_dpp64<0x114, 0xf>(v);   // row_shr:4
+  v += sn_dpp64<0x118, 0xf>(v);   // row_shr:8
+  v += sn_dpp64<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
+  v += sn_dpp64<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3
+  return v;
+}
+// (pf: feature d's running (mean, M2), loaded by lane 63 at the start of the step — off the
+// hand-off's critical path — or, pf == false, loaded here)
+DEV bool sn_reduce(const RolloutArgs& a, int d, int nblk, int step, int lane, const float* shs, bool pf,
+                   double pmean, double pm2) {
   const int O = a.O;
   const unsigned tag = a.sn_epoch0 + (unsigned)step;
   const u64* g1 = a.sn_g1;
@@ -87,22 +109,19 @@ DEV bool sn_reduce(const RolloutArgs& a, int d, int nblk, int step, int lane, co
     p1 += (double)v1[c];
     p2 += (double)v2[c];
   }
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    p1 += __shfl_xor(p1, o, 64);
-    p2 += __shfl_xor(p2, o, 64);
-  }
-  if (lane == 0) {
+  p1 = sn_wave_sum63(p1);
+  p2 = sn_wave_sum63(p2);
+  if (lane == 63) {
     const double count = (double)a.E, n_a = a.sn_n0 + (double)step * count;
     const double bmean_d = p1 / count;
     const double bmean = (double)shs[d] + bmean_d;
     double bm2 = p2 - p1 * bmean_d;
     if (bm2 < 0.0) bm2 = 0.0;
     const double n = n_a + count;
-    const double mean0 = a.sn_mean[d];
+    const double mean0 = pf ? pmean : a.sn_mean[d];
     const double delta = bmean - mean0;
     const double mu = mean0 + delta * (count / n);
-    const double M2 = a.sn_m2[d] + bm2 + delta * delta * (n_a * count / n);
+    const double M2 = (pf ? pm2 : a.sn_m2[d]) + bm2 + delta * delta * (n_a * count / n);
     double var = M2 / n;
     if (var < a.sn_var_floor) var = a.sn_var_floor;
     const float muf = (float)mu, inv = (float)(1.0 / sqrt(var));
@@ -116,19 +135,21 @@ DEV bool sn_reduce(const RolloutArgs& a, int d, int nblk, int step, int lane, co
   return true;
 }
 
-// Wave 0: gather every feature's (mean, 1/std) of this step into LDS (the values of the poll pass
-// whose tags all match; O <= 384 features (Humanoid: 376): 2 O granules in 12 registers per lane)
-constexpr int SN_GATHER = 12;
-DEV bool sn_gather(const RolloutArgs& a, int step, int lane, float* nm, float* ninv) {
+// Every wave: gather its share of the step's (mean, 1/std) granules into LDS (granules tid,
+// tid + NTHR, ... of the 2 O; the values of the poll pass whose tags all match; O <= SN_MAX_O)
+constexpr int SN_MAX_O = 384;
+template <int NTHR>
+DEV bool sn_gather(const RolloutArgs& a, int step, int tid, float* nm, float* ninv) {
+  constexpr int GU = (2 * SN_MAX_O + NTHR - 1) / NTHR;
   const int O = a.O;
   const unsigned tag = a.sn_epoch0 + (unsigned)step;
-  float v[SN_GATHER];
+  float v[GU];
   for (unsigned spins = 0;; ++spins) {
     bool ok = true;
 #pragma unroll
-    for (int u = 0; u < SN_GATHER; ++u) {
-      const int i = 64 * u + lane;
-      if (64 * u < 2 * O && i < 2 * O) {
+    for (int u = 0; u < GU; ++u) {
+      const int i = tid + NTHR * u;
+      if (i < 2 * O) {
         const u64 x = sn_get(a.sn_g2 + i);
         ok &= (unsigned)(x >> 32) == tag;
         v[u] = sn_val(x);
@@ -139,12 +160,10 @@ DEV bool sn_gather(const RolloutArgs& a, int step, int lane, float* nm, float* n
     if (spins > 8) __builtin_amdgcn_s_sleep(1);
   }
 #pragma unroll
-  for (int u = 0; u < SN_GATHER; ++u) {
-    const int i = 64 * u + lane;
-    if (64 * u < 2 * O && i < 2 * O) {
-      if (i < O) nm[i] = v[u];
-      else ninv[i - O] = v[u];
-    }
+  for (int u = 0; u < GU; ++u) {
+    const int i = tid + NTHR * u;
+    if (i < O) nm[i] = v[u];
+    else if (i < 2 * O) ninv[i - O] = v[u];
   }
   return true;
 }
@@ -330,7 +349,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
       if (!last) {
         // this step's batch moments about the iteration shift -> the iteration's moments (as in
         // rollout mode) and this workgroup's granules; its waves merge the features it owns
-        // (sn_reduce), wave 0 gathers the new stats of every feature (sn_gather)
+        // (sn_reduce), every wave gathers its share of the new stats of every feature (sn_gather)
         const unsigned tag = a.sn_epoch0 + (unsigned)step;
         auto moments = [&](auto kind_tag) {
           constexpr int KIND = decltype(kind_tag)::value;
@@ -351,17 +370,24 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
             sn_put(g + O + d, tag, ls2);
           }
         };
+        // the running (mean, M2) of this wave's first feature, loaded now: consumed after the
+        // hand-off (features blk + nblk * (w + NW j) on wave w; the first: j = 0)
+        const int dfirst = (int)blockIdx.x + (int)gridDim.x * wave;
+        double pmean = 0.0, pm2 = 0.0;
+        if (dfirst < O && lane == 63) {
+          pmean = a.sn_mean[dfirst];
+          pm2 = a.sn_m2[dfirst];
+        }
         if (a.kind == 1) moments(std::integral_constant<int, 1>{});
         else moments(std::integral_constant<int, 0>{});
         PH(7);
-        // features blk + nblk * (w + NW j) on wave w: the features of this workgroup are merged
-        // by its waves concurrently
+        // the features of this workgroup are merged by its waves concurrently
         bool okr = true;
-        for (int dfeat = (int)blockIdx.x + (int)gridDim.x * wave; okr && dfeat < O; dfeat += (int)gridDim.x * NW)
-          okr = sn_reduce(a, dfeat, (int)gridDim.x, step, lane, shs);
+        for (int dfeat = dfirst; okr && dfeat < O; dfeat += (int)gridDim.x * NW)
+          okr = sn_reduce(a, dfeat, (int)gridDim.x, step, lane, shs, dfeat == dfirst, pmean, pm2);
         if (!okr && lane == 0) *sn_fail = 1;
         PH(8);
-        if (wave == 0 && !sn_gather(a, step, lane, nm, ninv) && lane == 0) *sn_fail = 1;
+        if (!sn_gather<NTHR>(a, step, tid, nm, ninv) && lane == 0) *sn_fail = 1;
         PH(9);
         __syncthreads();
         PH(10);
@@ -644,7 +670,7 @@ void launch_nw(const RolloutArgs& a, hipStream_t s) {
     return;
   }
   const int cap = ncu * (per_cu > 1 ? per_cu - 1 : per_cu);
-  if (nblk > cap || nblk > SN_MAX_BLOCKS || a.O > 64 * SN_GATHER / 2) {
+  if (nblk > cap || nblk > SN_MAX_BLOCKS || a.O > SN_MAX_O) {
     dppo_note_error(hipErrorCooperativeLaunchTooLarge, __FILE__, __LINE__);
     return;
   }
@@ -666,7 +692,7 @@ int stepnorm_cap(const RolloutArgs& a) {
       hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  if (a.O > 64 * SN_GATHER / 2) return 0;   // the gather holds 2 O granules in registers
+  if (a.O > SN_MAX_O) return 0;   // the gather holds 2 O granules in registers
   const int cap = ncu * (per_cu > 1 ? per_cu - 1 : per_cu);
   return cap < SN_MAX_BLOCKS ? cap : SN_MAX_BLOCKS;
 }
