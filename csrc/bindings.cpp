@@ -413,8 +413,8 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   TORCH_CHECK(!(w8.defined() && w8.numel() > 0) || (dt == 1 && head >= 0), "w8: the fp8 mode's per-head bf16 update only");
   set_w8(a, w8, qscale, L);
   if (t32) {   // the row-major operand rows the kernels write are whole padded widths
-    const int64_t wid[11] = {head == 0 && !xT_ready ? L.d_in[0] : 0, head == 0 ? 128 : 0, 0, head == 1 ? 512 : 0, 0,
-                             head == 0 ? 128 : 0, head == 0 ? 128 : 0, 0, head == 1 ? 512 : 0, head == 1 ? 128 : 0, 0};
+    const int64_t wid[11] = {head == 0 && !xT_ready ? L.d_in[0] : 0, 0, 0, head == 1 ? 512 : 0, 0,
+                             head == 0 ? 128 : 0, 0, 0, head == 1 ? 512 : 0, head == 1 ? 128 : 0, 0};
     for (int i = 0; i < 11; ++i)
       TORCH_CHECK(tbufs[i].numel() >= wid[i] * ldT, "t32 head: row-major operand buffer ", i, " too small");
   }
@@ -425,6 +425,7 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
     launch_vhead_train((int)dt, a, cur_stream());
   } else if (t32) {
     TORCH_CHECK(head == 0 && !q8 && a.W8 == nullptr && phead_shape_ok(a), "phead: the policy head at bf16x3 / bf16");
+    TORCH_CHECK(part_dw + 32 * 128 + 128 * 128 <= npart, "phead: the dW_mu and dW_p2 blocks must fit the partial row");
     const int64_t eb = dt == 3 ? 4 : 2;
     TORCH_CHECK(ldT * std::max<int64_t>(L.d_in[0], 128) * eb < (int64_t(1) << 31), "phead: row-major operands beyond 2 GiB");
     TORCH_CHECK((int64_t)nblk * npart * 4 < (int64_t(1) << 31), "phead: partial buffer beyond 2 GiB");

@@ -15,13 +15,15 @@
 // Observation rows: a per-wave 3-slot X ring (2 KiB per k-step stage).
 //
 // Outputs (TRAIN only — the rollout kernel computes the policy forward):
-//   * the row-major wgrad operands h1 [ldT][128], g1 [ldT][128], g2 [ldT][128] (csrc/wgrad.hip RM
-//     reads) and, for a minibatch (idx != null, !xT_ready), the observation rows [ldT][d0]
+//   * the row-major wgrad operand g1 [ldT][128] (csrc/wgrad.hip RM reads) and, for a minibatch
+//     (idx != null, !xT_ready), the observation rows [ldT][d0]
 //     (full-batch calls: the wgrad reads x_buf itself — no x^T copy anywhere);
-//   * per-workgroup partials: loss terms (columns 0, 2-7), dlog_std (8 + j), and the mu layer's
-//     weight gradient dW_mu [32][128] at part_dw (bias = column 100), summed over the workgroup's
-//     128 rows by MFMA with the batch as K: the rows' h2 / dL/dmu are staged row-major in LDS
-//     and read back transposed (ds_read_b64_tr_b16), each of 4 waves one 32-feature tile.
+//   * per-workgroup partials: loss terms (columns 0, 2-7), dlog_std (8 + j), the mu layer's weight
+//     gradient dW_mu [32][128] at part_dw (bias = column 100) and p_fc2's dW_p2 [128][128] right
+//     after it (bias = column 100), each summed over the workgroup's 128 rows by MFMA with the
+//     batch as K: the operands are staged row-major in LDS and read back transposed
+//     (ds_read_b64_tr_b16).  So only p_fc1's operands (g1 and the observation rows) go through
+//     HBM to the wgrad.
 #include "t32.h"
 
 namespace {
@@ -203,9 +205,7 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
 
   // row-major operand stores of this lane's row (the launcher checks ldT * max(d0, 128) * EB < 2^31)
   const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(a.xT, (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_h1 = __builtin_amdgcn_make_buffer_rsrc(a.h1pT, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_g1 = __builtin_amdgcn_make_buffer_rsrc(a.g1pT, (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_g2 = __builtin_amdgcn_make_buffer_rsrc(a.g2pT, (short)0, 0x7fffffff, 0x00020000);
   const unsigned vx = (unsigned)(mr * d0 + 8 * h) * EB, v128 = (unsigned)(mr * 128 + 8 * h) * EB;
   const bool write_x = a.xT_ready == 0;
   const int xst = write_x ? 2 : 0;   // X operand stores per fc1 step
@@ -309,10 +309,6 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
     for (int e = 0; e < KPS; ++e) {
       const int k16 = KPS * j + e;
       b[e] = b_operand<DT>(acc1[k16 >> 1], k16 & 1);
-      sto(rs_h1, v128, 16 * k16 * EB, b[e]);
-    }
-    if constexpr (S3 && j == NS2 - 1) {
-      sto(rs_h1, v128, 16 * 7 * EB, b_operand<DT>(acc1[3], 1));
     }
     ring_mma<DT, 4 * KPS, (S3 ? 1 : 2)>(stg, lane, [&](int i) { return i; },
                                         [&](int i, const Frag& w) __attribute__((always_inline)) {
@@ -453,36 +449,42 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
   // ---- dW_mu^T [128 features][32 dims] = h2^T . dL/dmu over the workgroup's 128 rows: two
   // rounds of the h2 half [128][64] + dL/dmu [128][32] staged row-major (hi | lo planes); wave w
   // takes feature tile w in round w / 2 (K = all 128 rows: the whole workgroup sum, fixed order) ----
+  const int row = 32 * wave + r;   // this lane's row of the workgroup's 128
+  // row-major staging of 16-byte operand chunks (hi | lo planes) and the transposed fragment
+  // (lane: column c0 + (l & 31), rows 16 kk + 8 (l >> 5) ..) of a staged plane
+  auto put = [&](char* plane, int rowb, int chunk, const Frag& f, int pstride) __attribute__((always_inline)) {
+    if constexpr (S3) {
+      *reinterpret_cast<bf16x8*>(plane + rowb + 16 * chunk) = f.h;
+      *reinterpret_cast<bf16x8*>(plane + pstride + rowb + 16 * chunk) = f.l;
+    } else {
+      *reinterpret_cast<bf16x8*>(plane + rowb + 16 * chunk) = f;
+    }
+  };
+  auto get = [&](const char* plane, int pstride, int rowbytes, int c0, int kk, bool swz) __attribute__((always_inline)) -> Frag {
+    const int li = lane & 15, g = lane >> 4;
+    const int col = c0 + 16 * (g & 1) + 4 * (li & 3);
+    auto rd = [&](const char* base, int sub) __attribute__((always_inline)) {
+      const int rw2 = 16 * kk + 8 * (g >> 1) + 4 * sub + (li >> 2);
+      const int ch = (col >> 3) ^ (swz ? ph_swz(rw2) : 0);
+      return tr4(base + rw2 * rowbytes + 16 * ch + 2 * (col & 7));
+    };
+    if constexpr (S3) {
+      return Frag{cat8(rd(plane, 0), rd(plane, 1)), cat8(rd(plane + pstride, 0), rd(plane + pstride, 1))};
+    } else {
+      return cat8(rd(plane, 0), rd(plane, 1));
+    }
+  };
+  auto bar = [&]() __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  const __amdgpu_buffer_rsrc_t rs_part = __builtin_amdgcn_make_buffer_rsrc(a.part, (short)0, 0x7fffffff, 0x00020000);
   {
     char* Hp = scr;                     // [2 planes][128 rows][128 B]
     char* Dp = scr + 2 * PH_HP;         // [2 planes][128 rows][64 B]
-    const int row = 32 * wave + r;
-    auto put = [&](char* plane, int rowb, int chunk, const Frag& f, int pstride) __attribute__((always_inline)) {
-      if constexpr (S3) {
-        *reinterpret_cast<bf16x8*>(plane + rowb + 16 * chunk) = f.h;
-        *reinterpret_cast<bf16x8*>(plane + pstride + rowb + 16 * chunk) = f.l;
-      } else {
-        *reinterpret_cast<bf16x8*>(plane + rowb + 16 * chunk) = f;
-      }
-    };
-    // the transposed fragment (lane: column c0 + (l & 31), rows 16 kk + 8 (l >> 5) ..) of a plane
-    auto get = [&](const char* plane, int pstride, int rowbytes, int c0, int kk, bool swz) __attribute__((always_inline)) -> Frag {
-      const int li = lane & 15, g = lane >> 4;
-      const int col = c0 + 16 * (g & 1) + 4 * (li & 3);
-      auto rd = [&](const char* base, int sub) __attribute__((always_inline)) {
-        const int rw2 = 16 * kk + 8 * (g >> 1) + 4 * sub + (li >> 2);
-        const int ch = (col >> 3) ^ (swz ? ph_swz(rw2) : 0);
-        return tr4(base + rw2 * rowbytes + 16 * ch + 2 * (col & 7));
-      };
-      if constexpr (S3) {
-        return Frag{cat8(rd(plane, 0), rd(plane, 1)), cat8(rd(plane + pstride, 0), rd(plane + pstride, 1))};
-      } else {
-        return cat8(rd(plane, 0), rd(plane, 1));
-      }
-    };
 #pragma unroll
     for (int s = 0; s < 2; ++s) put(Dp, row * 64, 2 * s + h, db[s], PH_DP);
-    const __amdgpu_buffer_rsrc_t rs_part = __builtin_amdgcn_make_buffer_rsrc(a.part, (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int round = 0; round < 2; ++round) {
       // the h2 tiles 2 round, 2 round + 1 of this wave's rows (pinned here: not converted early
@@ -578,12 +580,6 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
     static_for_vh<0, NG2 / 2>([&](auto jc) __attribute__((always_inline)) {
       constexpr int jj = decltype(jc)::value, j = pass * (NG2 / 2) + jj;
       const char* stg = sync_late(eg3 + j);
-      if constexpr (S3) {
-        sto(rs_g2, v128, 16 * j * EB, j < NGB ? gb[j < NGB ? j : 0] : Frag{});
-      } else {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) sto(rs_g2, v128, 16 * (2 * j + e) * EB, gb[2 * j + e]);
-      }
       // (split: the last stage's k-step 7 is zero: its 2 fragments are not multiplied)
       constexpr int NF = (S3 && jj == NG2 / 2 - 1) ? 2 : 4 * KPS;
       ring_mma<DT, NF, (S3 ? 1 : 2)>(stg, lane, [&](int i) { return i; },
@@ -601,6 +597,72 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
       for (int s = 0; s < 2; ++s) sto(rs_g1, v128, (32 * t + 16 * s) * EB, b_operand<DT>(g1, s));
     }
   });
+
+  // ---- dW_p2^T [out 128][in 128] = g2^T . h1b over the workgroup's 128 rows (h1b: h1 with its
+  // bias column), fused like dW_mu (train.py:166's p_fc2 gradient without the g2 / h1 operand
+  // round trip through HBM and the wgrad): four rounds of an out-half of g2 and an in-half of h1
+  // staged row-major in the freed ring + scratch (2 x 32 KiB), wave w taking the round's tile
+  // (out 64 go + 32 (w >> 1), in 64 ih + 32 (w & 1)) with K = all 128 rows (fixed order) ----
+  {
+    static_assert(2 * 2 * PH_HP <= PH_S * PH_SB + PH_SCR, "two staged halves fit the ring + scratch");
+    char* Gs = smem;                  // g2 out-half [2 planes][128 rows][128 B]
+    char* Hs = smem + 2 * PH_HP;      // h1 in-half  [2 planes][128 rows][128 B]
+    bar();   // every wave is done with the ring's last stage and the scratch
+    auto stage_g = [&](int go) __attribute__((always_inline)) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int k16 = 4 * go + kk;   // g2 features 16 k16 + 8 h ..: the half's chunk 2 kk + h
+        put(Gs, row * 128, (2 * kk + h) ^ ph_swz(row), k16 < NGB ? gb[k16 < NGB ? k16 : 0] : Frag{}, PH_HP);
+      }
+    };
+    auto stage_h = [&](int ih) __attribute__((always_inline)) {
+      // (pinned here: the conversions are not hoisted above the barriers and held)
+      asm volatile("" : "+v"(acc1[2 * ih]), "+v"(acc1[2 * ih + 1]));
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          put(Hs, row * 128, (4 * tt + 2 * s + h) ^ ph_swz(row), b_operand<DT>(acc1[2 * ih + tt], s), PH_HP);
+    };
+    const unsigned base = (unsigned)((size_t)blockIdx.x * a.npart + a.part_dw + 32 * 128 + 32 * (wave & 1) + r) * 4u;
+    // rounds (go, ih) = (0, 0), (0, 1), (1, 1), (1, 0): one half restaged per round after the first
+    static_for_vh<0, 4>([&](auto rc) __attribute__((always_inline)) {
+      constexpr int rd = decltype(rc)::value;
+      constexpr int go = rd >> 1, ih = (rd == 1 || rd == 2) ? 1 : 0;
+      if constexpr (rd == 0) {
+        stage_g(0);
+        stage_h(0);
+      } else if constexpr (rd == 2) {
+        stage_g(1);
+      } else {
+        stage_h(ih);
+      }
+      bar();
+      f32x16 dw = f32x16{};
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) {
+        Frag fa[2], fb[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          fa[q] = get(Gs, PH_HP, 128, 32 * (wave >> 1), 2 * k2 + q, true);
+          fb[q] = get(Hs, PH_HP, 128, 32 * (wave & 1), 2 * k2 + q, true);
+        }
+        ph_settle<DT>(fa, fb);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) dw = V::mma(dw, fa[q], fb[q]);   // A = g2^T (out), B = h1b (in)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // out feature 64 go + 32 (w >> 1) + ph_dim(i, h) (registers), in feature 64 ih + 32 (w & 1)
+      // + (l & 31) (lanes): dst[part_dw + 4096 + out * 128 + in]
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const unsigned o = (unsigned)(64 * go + 32 * (wave >> 1) + ph_dim(i, h));
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dw[i]), rs_part, base + (o * 128u + 64u * ih) * 4u, 0,
+                                              0);
+      }
+      bar();
+    });
+  }
 
   // ---- per-workgroup partials (fixed order over the waves): loss terms (not column 1: the
   // value head's) and dlog_std ----

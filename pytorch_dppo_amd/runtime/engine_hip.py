@@ -190,7 +190,9 @@ class HipEngine:
         # the wgrad
         self.nhead_blk = self.ldT // 128
         self.part_dw = [_r(8 + A, 4), 8]
-        np_pol = self.part_dw[0] + 32 * 128
+        # (the 32x32 policy head also sums p_fc2's weight gradient [128][128] right after dW_mu:
+        # p_fc2 leaves the wgrad, and h1p / g2p their HBM round trip)
+        np_pol = self.part_dw[0] + 32 * 128 + (128 * 128 if self.phead else 0)
         self.part_h = [torch.zeros(self.nhead_blk, np_pol, **f32), torch.zeros(self.nhead_blk, 8 + 128, **f32)]
         # world size 1: both head kernels write ONE partial buffer (policy its columns, value
         # column 1 and its dW_v after the policy's block) and one wgrad + gather/Adam launch
@@ -339,12 +341,14 @@ class HipEngine:
                           if self.device.type == "cuda" else 256)
         ls = self.L.layers
         names = [l.name for l in ls]
+        # (the 32x32 policy head sums p_fc2's weight gradient itself)
+        pol = ("p_fc1",) if getattr(self, "phead", False) else ("p_fc1", "p_fc2")
         if self.heads and joint:
-            groups = [[names.index(n) for n in ("p_fc1", "p_fc2", "v_fc1", "v_fc2")]]
+            groups = [[names.index(n) for n in pol + ("v_fc1", "v_fc2")]]
             ranges = [(self.A, model.num_params)]
             partials = [True]
         elif self.heads:
-            groups = [[names.index(n) for n in ("p_fc1", "p_fc2")], [names.index(n) for n in ("v_fc1", "v_fc2")]]
+            groups = [[names.index(n) for n in pol], [names.index(n) for n in ("v_fc1", "v_fc2")]]
             (_, phi), (vlo, vhi) = self.head_range
             ranges = [(self.A, phi), (vlo, vhi)]
             partials = [True, False]
@@ -511,6 +515,8 @@ class HipEngine:
                 for j in range(A):
                     add(kind, 8 + j, j)
                 narrow(kind, "mu", dwp, 0)
+                if self.phead:
+                    narrow(kind, "p_fc2", dwp + 32 * 128, 0)
             if dwv is not None:
                 add(kind, 1, -2)
                 narrow(kind, "v", dwv, vbase)

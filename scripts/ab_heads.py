@@ -33,10 +33,14 @@ def main():
     ctx = init_single_rank_collective(dev, port=free_port())
     workers = {}
     for a in arms:
-        vh, ph = ARMS[a]
+        # "<arm>:w<N>": the same arm with Params.wgrad_wgs = N (wgrad tasks per launch)
+        base, _, wg = a.partition(":w")
+        vh, ph = ARMS[base]
         p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536,
                         batch_size=65536, dtype=dtype, seed=1, phase_timing=0)
         p.vhead_kernel, p.phead_kernel = vh, ph
+        if wg:
+            p.wgrad_wgs = int(wg)
         w = DPPOWorker(p, ctx)
         assert w.engine.vhead == vh and w.engine.phead == ph, a
         for _ in range(2):

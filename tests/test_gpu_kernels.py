@@ -873,8 +873,14 @@ def test_head_kernels_match_one_kernel_update(env_name, mb, dtype, loss, monkeyp
             c = torch.arange(mb, device=DEV).repeat(nfeat)
             return eng.decode(buf).reshape(-1)[fm_index(r, c, eng.ldT)].view(nfeat, mb)
 
-        ph = bool(getattr(eng, "phead", False))   # (the 32x32 policy head: h1p and X rows row-major)
-        res[heads] = (eng.grad_flat.clone(), eng.last_losses(), rowmajor(eng.h1pT, n1p, ph),
+        # (the 32x32 policy head: X rows row-major; h1p is not stored — p_fc2's weight gradient is
+        # summed in the kernel — so both arms compare h1v instead)
+        ph = bool(getattr(eng, "phead", False))
+        if heads == "1":
+            use_h1v = ph
+        h1 = (rowmajor(eng.h1vT, model.layer("v_fc2").fan_in, bool(getattr(eng, "vhead", False))) if use_h1v
+              else rowmajor(eng.h1pT, n1p))
+        res[heads] = (eng.grad_flat.clone(), eng.last_losses(), h1,
                       rowmajor(eng.g1vT, n1v, bool(getattr(eng, "vhead", False))),
                       rowmajor(eng.xT, model.num_inputs, ph), eng.mu_prev.clone(), eng.v_prev.clone())
         if heads == "1" and loss == "ppo":
