@@ -274,7 +274,9 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   // phase timeline (diagnostics, a.tstamp != null): per-wave shader-clock cycles summed over
   // the steps for each phase, written by lane 0 of every wave of every workgroup
   // (slots 7-10: the per-step filter's moments / reduce / gather / barrier, SN only)
-  unsigned long long ph_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // (slots 11-14: absolute s_memrealtime of step 8's filter entry / moments published / reduce
+  // done / gather done — the cross-workgroup skew of the hand-offs)
+  unsigned long long ph_acc[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long ph_t = a.tstamp ? __builtin_amdgcn_s_memtime() : 0ull;
 #define PH(i)                                                     \
   do {                                                            \
@@ -283,6 +285,10 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
       ph_acc[i] += t_ - ph_t;                                     \
       ph_t = t_;                                                  \
     }                                                             \
+  } while (0)
+#define PH_ABS(i)                                                                  \
+  do {                                                                             \
+    if (a.tstamp != nullptr && step == 8) ph_acc[i] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
   for (int step = 0; step <= a.T; ++step) {
     const int tb = a.t_base + step;
@@ -378,17 +384,21 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
           pmean = a.sn_mean[dfirst];
           pm2 = a.sn_m2[dfirst];
         }
+        PH_ABS(11);
         if (a.kind == 1) moments(std::integral_constant<int, 1>{});
         else moments(std::integral_constant<int, 0>{});
         PH(7);
+        PH_ABS(12);
         // the features of this workgroup are merged by its waves concurrently
         bool okr = true;
         for (int dfeat = dfirst; okr && dfeat < O; dfeat += (int)gridDim.x * NW)
           okr = sn_reduce(a, dfeat, (int)gridDim.x, step, lane, shs, dfeat == dfirst, pmean, pm2);
         if (!okr && lane == 0) *sn_fail = 1;
         PH(8);
+        PH_ABS(13);
         if (!sn_gather<NTHR>(a, step, tid, nm, ninv) && lane == 0) *sn_fail = 1;
         PH(9);
+        PH_ABS(14);
         __syncthreads();
         PH(10);
         if (*sn_fail) {   // a peer never published: give up (the host raises)
@@ -604,9 +614,10 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   __syncthreads();
   if (a.tstamp != nullptr && lane == 0) {
 #pragma unroll
-    for (int i = 0; i < 11; ++i) a.tstamp[((size_t)blockIdx.x * NW + wave) * 16 + i] = ph_acc[i];
+    for (int i = 0; i < 15; ++i) a.tstamp[((size_t)blockIdx.x * NW + wave) * 16 + i] = ph_acc[i];
   }
 #undef PH
+#undef PH_ABS
   // ---- write back env state, episode trackers, partial moments / episode stats ----
   for (int i = tid; i < nvalid * S; i += NTHR) a.state[(size_t)e0 * S + i] = st[i];
   if (tid < nvalid) {

@@ -2,7 +2,8 @@
 """Per-step phase split of the one-launch per-step observation filter (obs_norm_update='step',
 csrc/rollout.hip SN path) at the bench geometry: s_memtime cycles per step (median over workgroups of
 the max over waves) for the filter's moments / reduce (first hand-off) / gather (second hand-off) /
-barrier, and the rest of the step; plus the rollout time without stamps.
+barrier, and the rest of the step; plus the rollout time without stamps, and the cross-workgroup
+spread of step 8's hand-offs (absolute 100 MHz stamps: min / median / max over workgroups).
 
     python scripts/probe_filter_phases.py [reps]
 """
@@ -50,8 +51,18 @@ def main():
     eng.ext.set_rollout_tstamp(torch.empty(0, dtype=torch.int64, device=dev))
     t = buf.view(nblk, 8, 16)[:, :, :11].double() / eng.T
     per = {n: float(t[:, :, i].max(dim=1).values.median()) for i, n in enumerate(NAMES)}
+    # step 8's absolute 100 MHz stamps (slots 11-14): per workgroup the latest wave; relative to
+    # the earliest filter entry, in microseconds
+    ab = buf.view(nblk, 8, 16)[:, :, 11:15].double()
+    t0 = ab[:, :, 0][ab[:, :, 0] > 0].min()
+    us = (ab - t0) / 100.0
+    wg = us.amax(dim=1)                    # [nblk, 4]: entry, moments published, reduce done, gather done
+    red = us[:, 0, 2]                      # wave 0 of every workgroup is a reducer (features < nblk)
+    q = lambda v: [round(float(v.min()), 2), round(float(v.median()), 2), round(float(v.max()), 2)]
+    skew = {"entry": q(wg[:, 0]), "moments published": q(wg[:, 1]), "reducers done (wave 0)": q(red),
+            "gather done": q(wg[:, 3])}
     print(json.dumps({"rollout_ms": round(ms, 4), "cycles_per_step(median blk, max wave)": per,
-                      "sum": sum(per.values())}, indent=1), flush=True)
+                      "sum": sum(per.values()), "step8_us_min_median_max": skew}, indent=1), flush=True)
 
 
 if __name__ == "__main__":
