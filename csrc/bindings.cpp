@@ -212,7 +212,7 @@ void rollout_stepnorm(int64_t dt, int64_t rows, torch::Tensor state, torch::Tens
   check(sn[0], "sn mean", at::kDouble, a.O);
   check(sn[1], "sn m2", at::kDouble, a.O);
   TORCH_CHECK(sn[2].data_ptr() != shift.data_ptr(), "the shift must not alias the stats being merged into");
-  check(g1, "g1", at::kLong, (int64_t)nblk * 2 * a.O);
+  check(g1, "g1", at::kLong, (int64_t)sn_g1_elems(nblk, a.O));
   check(g2, "g2", at::kLong, 2 * (int64_t)a.O);
   check(err, "err", at::kInt, 1);
   TORCH_CHECK(epoch0 >= 1 && epoch0 + a.T < (int64_t)UINT32_MAX, "epoch0");

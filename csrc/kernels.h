@@ -46,7 +46,7 @@ struct RolloutArgs {
   // filter that absorbs every observation before normalising it, model.py:68 / train.py:84-85);
   // sn_g1 == null: off (mean / inv_std above are fixed for the launch).  Step t, all workgroups
   // co-resident (cooperative launch): each publishes its batch moments about `shift` as 8-byte
-  // {tag, fp32} granules (sn_g1[blk][2O]); workgroup b sums features b, b + nblk, ... over all
+  // {tag, fp32} granules (sn_g1, sn_g1_index); workgroup b sums the 4-feature units b, b + nblk, ... over all
   // workgroups in a fixed order (fp64), Chan-merges them into the fp64 running stats (sn_mean,
   // sn_m2: each feature owned by ONE workgroup for the whole launch) and publishes the new fp32
   // (mean, 1/std) as granules (sn_g2[2O]); every workgroup gathers those and normalises.  Tags
@@ -55,13 +55,24 @@ struct RolloutArgs {
   double* sn_m2;             // [O] running sum of squared deviations (fp64, in place)
   float* sn_mean_f32;        // [O] fp32 images after the last step (host-visible)
   float* sn_inv_std;         // [O]
-  unsigned long long* sn_g1; // [nblk][2O] partial-moment granules
+  unsigned long long* sn_g1; // sn_g1_elems(nblk, O) partial-moment granules (sn_g1_index)
   unsigned long long* sn_g2; // [2O] stats granules
   unsigned* sn_err;          // nonzero: a spin timed out (the launch gave up; the host raises)
   double sn_n0;              // running count before step 0 (each step adds E)
   unsigned sn_epoch0;        // tag of step 0's granules (>= 1)
   double sn_var_floor;
 };
+
+// The per-step filter's partial-moment granules (RolloutArgs::sn_g1), line-blocked: a 128-byte
+// line holds moment m of features 4 fu .. 4 fu + 3 of workgroups 4 wb .. 4 wb + 3 (granule
+// 4 (w & 3) + (d & 3)); lines ordered [m][fu][wb].
+inline __host__ __device__ size_t sn_g1_index(int m, int d, int w, int O, int nblk) {
+  const int nfu = (O + 3) >> 2, nwb = (nblk + 3) >> 2;
+  return ((size_t)(m * nfu + (d >> 2)) * nwb + (w >> 2)) * 16 + (size_t)(w & 3) * 4 + (d & 3);
+}
+inline __host__ __device__ size_t sn_g1_elems(int nblk, int O) {
+  return (size_t)2 * ((O + 3) >> 2) * ((nblk + 3) >> 2) * 16;
+}
 
 // fp8 mode's gradient-amax ring (csrc/common.h Q8): [3 slots][4 tensors][Q8_SUB sub-slots][Q8_LINE]
 constexpr int Q8_SUB = 64, Q8_LINE = 32;

@@ -43,7 +43,7 @@ DEV float env_obs(const float* st, int S, int r, int d) {
 // leaving waves that never finish.
 typedef unsigned long long u64;
 constexpr unsigned SN_SPIN_MAX = 1u << 21;   // >= ~1 s of polling per hand-off
-constexpr int SN_MAX_BLOCKS = 256;           // grid cap of the per-step normalisation launch (SN_CHUNKS lanes' worth)
+constexpr int SN_MAX_BLOCKS = 256;           // grid cap of the per-step normalisation launch
 DEV void sn_put(u64* g, unsigned tag, float v) {
   __hip_atomic_store(g, ((u64)tag << 32) | (u64)__float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -52,94 +52,98 @@ DEV u64 sn_get(const u64* g) {
 }
 DEV float sn_val(u64 x) { return __uint_as_float((unsigned)x); }
 
-// Waves 0 .. NW-1 of workgroup `blk`: the step's Chan merge of the features it owns (feature
-// blk + nblk * w on wave w): the fp32 partials of all nblk workgroups summed in fp64 in a fixed
-// order (lane l holds workgroups l, l + 64, ... in that order; then an xor butterfly, which leaves
-// the same bits in every lane), merged into the running (mean, M2) — csrc/obs.hip obs_merge's
-// formulas — and published as the (mean, 1/std) granules.  The values of a poll pass whose tags
-// all match are the values (no second read).  Returns false on a timeout.
-constexpr int SN_CHUNKS = 4;                 // workgroups per reducer lane: the grid is <= 256
-// fp64 sum over the wave into lane 63 in a fixed order: an inclusive DPP scan (row_shr 1, 2, 4, 8
-// within each row of 16, then row_bcast 15 / 31 across the rows) — 12 DPP moves and 6 adds, not
-// 12 ds_bpermute round trips on the hand-off's critical path
-template <int CTRL, int ROWMASK>
-DEV double sn_dpp64(double v) {
-  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
-  const unsigned l2 = __builtin_amdgcn_update_dpp(0u, lo, CTRL, ROWMASK, 0xf, true);
-  const unsigned h2 = __builtin_amdgcn_update_dpp(0u, hi, CTRL, ROWMASK, 0xf, true);
-  return __hiloint2double((int)h2, (int)l2);
-}
-DEV double sn_wave_sum63(double v) {
-  v += sn_dpp64<0x111, 0xf>(v);   // row_shr:1
-  v += sn_dpp64<0x112, 0xf>(v);   // row_shr:2
-  v += sn_dpp64<0x114, 0xf>(v);   // row_shr:4
-  v += sn_dpp64<0x118, 0xf>(v);   // row_shr:8
-  v += sn_dpp64<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
-  v += sn_dpp64<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3
-  return v;
-}
-// (pf: feature d's running (mean, M2), loaded by lane 63 at the start of the step — off the
-// hand-off's critical path — or, pf == false, loaded here)
-DEV bool sn_reduce(const RolloutArgs& a, int d, int nblk, int step, int lane, const float* shs, bool pf,
-                   double pmean, double pm2) {
-  const int O = a.O;
+// Workgroup `blk`: the step's Chan merge of the 4-feature units u = blk, blk + nblk, ...
+// sn_g1 is line-blocked (kernels.h sn_g1_index): a 128-byte line holds one moment of 4 features x
+// 4 workgroups, so a publisher writes 2 O / 4 partial lines and a unit is 2 nblk / 4 lines.
+// (One reducer wave per feature over a workgroup-major layout polled one line per workgroup —
+// 512 per feature, shared with 15 other features' reducers — and took 3-8 us per hand-off at 256
+// workgroups; the idle cross-XCD hop is 0.41 us, scripts/probes/xcd_latency.hip.)  All NW waves
+// poll a unit: wave w moment w & 1, line rows 4 ((w >> 1) RL + i) + (l >> 4), i < RL; lane
+// l holds granule l & 15 (workgroup offset (l >> 2) & 3, feature fi = l & 3) and sums its rows
+// in fp64 in order, then an xor butterfly over the lanes of one fi (the same bits in every lane:
+// a fixed order) leaves the wave's partial in lanes 0-3; wave 0 adds the NW / 2 parts of each
+// moment (fixed order), merges into the running (mean, M2) — csrc/obs.hip obs_merge's formulas —
+// and publishes the (mean, 1/std) granules.  The values of a poll pass whose tags all match are
+// the values.  (pf: the first unit's running (mean, M2), loaded by wave 0's lanes 0-3 at the
+// start of the step — off the hand-off's critical path.)  Returns false on a timeout (after the
+// workgroup's barriers).
+template <int NW>
+DEV bool sn_reduce(const RolloutArgs& a, int nblk, int step, int wave, int lane, const float* shs,
+                   double* red, double pmean, double pm2, unsigned& npoll) {
+  const int O = a.O, nfu = (O + 3) >> 2, nwb = (nblk + 3) >> 2;
   const unsigned tag = a.sn_epoch0 + (unsigned)step;
-  const u64* g1 = a.sn_g1;
-  float v1[SN_CHUNKS], v2[SN_CHUNKS];
-  for (unsigned spins = 0;; ++spins) {
-    bool ok = true;
+  const int gp = lane & 15, fi = lane & 3, wi = (lane >> 2) & 3, lq = lane >> 4;
+  constexpr int RL = SN_MAX_BLOCKS / 4 / 4 / (NW / 2);   // line rows per lane (64 rows in NW / 2 parts)
+  const int m = wave & 1, part = wave >> 1;
+  bool fail = false;
+  for (int u = (int)blockIdx.x; u < nfu; u += nblk) {
+    const int d = 4 * u + fi;
+    {
+      const u64* g = a.sn_g1 + (size_t)(m * nfu + u) * nwb * 16 + gp;
+      float v[RL];
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
 #pragma unroll
-    for (int c = 0; c < SN_CHUNKS; ++c) {
-      const int w = 64 * c + lane;
-      v1[c] = v2[c] = 0.f;
-      if (w < nblk) {
-        const u64 x1 = sn_get(g1 + (size_t)w * 2 * O + d), x2 = sn_get(g1 + (size_t)w * 2 * O + O + d);
-        ok &= (unsigned)(x1 >> 32) == tag && (unsigned)(x2 >> 32) == tag;
-        v1[c] = sn_val(x1);
-        v2[c] = sn_val(x2);
+        for (int i = 0; i < RL; ++i) {
+          const int wb = lq + 4 * (RL * part + i);
+          v[i] = 0.f;
+          if (wb < nwb && 4 * wb + wi < nblk && d < O) {
+            const u64 x = sn_get(g + (size_t)wb * 16);
+            ok &= (unsigned)(x >> 32) == tag;
+            v[i] = sn_val(x);
+          }
+        }
+        npoll = spins + 1;
+        if (__all(ok)) break;
+        if (spins > SN_SPIN_MAX) { fail = true; break; }
+        if (spins > 8) __builtin_amdgcn_s_sleep(1);
       }
-    }
-    if (__all(ok)) break;
-    if (spins > SN_SPIN_MAX) return false;
-    if (spins > 8) __builtin_amdgcn_s_sleep(1);
-  }
-  double p1 = 0.0, p2 = 0.0;
+      double p = 0.0;
 #pragma unroll
-  for (int c = 0; c < SN_CHUNKS; ++c) {
-    p1 += (double)v1[c];
-    p2 += (double)v2[c];
+      for (int i = 0; i < RL; ++i) p += (double)v[i];
+#pragma unroll
+      for (int x = 4; x < 64; x <<= 1) p += __shfl_xor(p, x);
+      if (lane < 4) red[4 * wave + lane] = p;
+    }
+    __syncthreads();
+    if (wave == 0 && lane < 4 && d < O) {
+      double p1 = 0.0, p2 = 0.0;
+#pragma unroll
+      for (int q = 0; q < NW / 2; ++q) {
+        p1 += red[8 * q + lane];
+        p2 += red[8 * q + 4 + lane];
+      }
+      const bool pf = u == (int)blockIdx.x;
+      const double count = (double)a.E, n_a = a.sn_n0 + (double)step * count;
+      const double bmean_d = p1 / count;
+      const double bmean = (double)shs[d] + bmean_d;
+      double bm2 = p2 - p1 * bmean_d;
+      if (bm2 < 0.0) bm2 = 0.0;
+      const double n = n_a + count;
+      const double mean0 = pf ? pmean : a.sn_mean[d];
+      const double delta = bmean - mean0;
+      const double mu = mean0 + delta * (count / n);
+      const double M2 = (pf ? pm2 : a.sn_m2[d]) + bm2 + delta * delta * (n_a * count / n);
+      double var = M2 / n;
+      if (var < a.sn_var_floor) var = a.sn_var_floor;
+      const float muf = (float)mu, inv = (float)(1.0 / sqrt(var));
+      a.sn_mean[d] = mu;
+      a.sn_m2[d] = M2;
+      a.sn_mean_f32[d] = muf;
+      a.sn_inv_std[d] = inv;
+      sn_put(a.sn_g2 + d, tag, muf);
+      sn_put(a.sn_g2 + O + d, tag, inv);
+    }
+    if (u + nblk < nfu) __syncthreads();   // (red is reused by the next unit)
   }
-  p1 = sn_wave_sum63(p1);
-  p2 = sn_wave_sum63(p2);
-  if (lane == 63) {
-    const double count = (double)a.E, n_a = a.sn_n0 + (double)step * count;
-    const double bmean_d = p1 / count;
-    const double bmean = (double)shs[d] + bmean_d;
-    double bm2 = p2 - p1 * bmean_d;
-    if (bm2 < 0.0) bm2 = 0.0;
-    const double n = n_a + count;
-    const double mean0 = pf ? pmean : a.sn_mean[d];
-    const double delta = bmean - mean0;
-    const double mu = mean0 + delta * (count / n);
-    const double M2 = (pf ? pm2 : a.sn_m2[d]) + bm2 + delta * delta * (n_a * count / n);
-    double var = M2 / n;
-    if (var < a.sn_var_floor) var = a.sn_var_floor;
-    const float muf = (float)mu, inv = (float)(1.0 / sqrt(var));
-    a.sn_mean[d] = mu;
-    a.sn_m2[d] = M2;
-    a.sn_mean_f32[d] = muf;
-    a.sn_inv_std[d] = inv;
-    sn_put(a.sn_g2 + d, tag, muf);
-    sn_put(a.sn_g2 + O + d, tag, inv);
-  }
-  return true;
+  return !fail;
 }
 
 // Every wave: gather its share of the step's (mean, 1/std) granules into LDS (granules tid,
 // tid + NTHR, ... of the 2 O; the values of the poll pass whose tags all match; O <= SN_MAX_O)
 constexpr int SN_MAX_O = 384;
 template <int NTHR>
-DEV bool sn_gather(const RolloutArgs& a, int step, int tid, float* nm, float* ninv) {
+DEV bool sn_gather(const RolloutArgs& a, int step, int tid, float* nm, float* ninv, unsigned& npoll) {
   constexpr int GU = (2 * SN_MAX_O + NTHR - 1) / NTHR;
   const int O = a.O;
   const unsigned tag = a.sn_epoch0 + (unsigned)step;
@@ -155,6 +159,7 @@ DEV bool sn_gather(const RolloutArgs& a, int step, int tid, float* nm, float* ni
         v[u] = sn_val(x);
       }
     }
+    npoll = spins + 1;
     if (__all(ok)) break;
     if (spins > SN_SPIN_MAX) return false;
     if (spins > 8) __builtin_amdgcn_s_sleep(1);
@@ -178,6 +183,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   using T = typename P::T;
   constexpr int NTHR = 64 * NW;
   static_assert(ROWS % 4 == 0 && NTHR % ROWS == 0 && (NTHR / ROWS) <= 64, "rollout tiling");
+  static_assert(!SN || NW >= 4, "the per-step filter's reduce polls with waves 0-3");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int e0 = blockIdx.x * ROWS;
   const int nvalid = min(ROWS, a.E - e0);
@@ -208,6 +214,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   float* nm = SN ? cv.take<float>(O) : nullptr;
   float* ninv = SN ? cv.take<float>(O) : nullptr;
   int* sn_fail = SN ? cv.take<int>(1) : nullptr;
+  double* sn_red = SN ? cv.take<double>(32) : nullptr;   // the reduce's per-wave partials
   // fp8: the MFMA tile is e4m3 but the buffer rows are bf16 — a bf16 staging tile lets them
   // leave as 16-byte row chunks (element stores strided by the row length were 2.6x the bf16
   // kernel's time)
@@ -276,7 +283,8 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   // (slots 7-10: the per-step filter's moments / reduce / gather / barrier, SN only)
   // (slots 11-14: absolute s_memrealtime of step 8's filter entry / moments published / reduce
   // done / gather done — the cross-workgroup skew of the hand-offs)
-  unsigned long long ph_acc[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // (slot 15: step 8's poll passes, gather << 32 | reduce)
+  unsigned long long ph_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long ph_t = a.tstamp ? __builtin_amdgcn_s_memtime() : 0ull;
 #define PH(i)                                                     \
   do {                                                            \
@@ -362,25 +370,26 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
           for (int d = tid; d < O; d += NTHR) {
             const float sh = shs[d];
             float ls1 = 0.f, ls2 = 0.f;
+            // every row read unconditionally (st holds ROWS rows), the invalid ones masked: a
+            // per-row branch kept the compiler from batching the LDS reads (one round trip each)
 #pragma unroll
-            for (int r = 0; r < ROWS; ++r)
-              if (r < nvalid) {
-                const float dd = env_obs<KIND>(st, S, r, d) - sh;
-                ls1 += dd;
-                ls2 += dd * dd;
-              }
+            for (int r = 0; r < ROWS; ++r) {
+              const float o = env_obs<KIND>(st, S, r, d);
+              const float dd = r < nvalid ? o - sh : 0.f;
+              ls1 += dd;
+              ls2 += dd * dd;
+            }
             s1[d] += ls1;
             s2[d] += ls2;
-            u64* g = a.sn_g1 + (size_t)blockIdx.x * 2 * O;
-            sn_put(g + d, tag, ls1);
-            sn_put(g + O + d, tag, ls2);
+            sn_put(a.sn_g1 + sn_g1_index(0, d, (int)blockIdx.x, O, (int)gridDim.x), tag, ls1);
+            sn_put(a.sn_g1 + sn_g1_index(1, d, (int)blockIdx.x, O, (int)gridDim.x), tag, ls2);
           }
         };
-        // the running (mean, M2) of this wave's first feature, loaded now: consumed after the
-        // hand-off (features blk + nblk * (w + NW j) on wave w; the first: j = 0)
-        const int dfirst = (int)blockIdx.x + (int)gridDim.x * wave;
+        // the running (mean, M2) of this workgroup's first unit (4 features), loaded now:
+        // consumed after the hand-off (wave 0, lanes 0-3)
+        const int dfirst = 4 * (int)blockIdx.x + lane;
         double pmean = 0.0, pm2 = 0.0;
-        if (dfirst < O && lane == 63) {
+        if (wave == 0 && lane < 4 && dfirst < O) {
           pmean = a.sn_mean[dfirst];
           pm2 = a.sn_m2[dfirst];
         }
@@ -389,16 +398,18 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
         else moments(std::integral_constant<int, 0>{});
         PH(7);
         PH_ABS(12);
-        // the features of this workgroup are merged by its waves concurrently
-        bool okr = true;
-        for (int dfeat = dfirst; okr && dfeat < O; dfeat += (int)gridDim.x * NW)
-          okr = sn_reduce(a, dfeat, (int)gridDim.x, step, lane, shs, dfeat == dfirst, pmean, pm2);
-        if (!okr && lane == 0) *sn_fail = 1;
+        unsigned npr = 0, npg = 0;
+        if (!sn_reduce<NW>(a, (int)gridDim.x, step, wave, lane, shs, sn_red, pmean, pm2, npr) && lane == 0)
+          *sn_fail = 1;
         PH(8);
         PH_ABS(13);
-        if (!sn_gather<NTHR>(a, step, tid, nm, ninv) && lane == 0) *sn_fail = 1;
+        // the gather polls start once this workgroup's reducers are done: polling from the
+        // other waves during the reduce queued ahead of the reducers' own loads on the CU
+        __syncthreads();
+        if (!sn_gather<NTHR>(a, step, tid, nm, ninv, npg) && lane == 0) *sn_fail = 1;
         PH(9);
         PH_ABS(14);
+        if (a.tstamp != nullptr && step == 8) ph_acc[15] = ((unsigned long long)npg << 32) | npr;
         __syncthreads();
         PH(10);
         if (*sn_fail) {   // a peer never published: give up (the host raises)
@@ -614,7 +625,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_kernel(RolloutArgs a) {
   __syncthreads();
   if (a.tstamp != nullptr && lane == 0) {
 #pragma unroll
-    for (int i = 0; i < 15; ++i) a.tstamp[((size_t)blockIdx.x * NW + wave) * 16 + i] = ph_acc[i];
+    for (int i = 0; i < 16; ++i) a.tstamp[((size_t)blockIdx.x * NW + wave) * 16 + i] = ph_acc[i];
   }
 #undef PH
 #undef PH_ABS
@@ -649,7 +660,7 @@ size_t rollout_lds(const RolloutArgs& a) {
   b += al(sizeof(uint32_t) * 3 * ROWS);
   b += al(sizeof(float) * a.S) + al(sizeof(int) * a.S);
   b += al(sizeof(float) * 2 * a.A);
-  if (a.sn_g1 != nullptr) b += 3 * al(sizeof(float) * a.O) + al(sizeof(int));
+  if (a.sn_g1 != nullptr) b += 3 * al(sizeof(float) * a.O) + al(sizeof(int)) + al(sizeof(double) * 32);
   if (DT == DT_FP8) b += al(sizeof(__bf16) * ROWS * a.d1);   // bf16 staging tile of the buffer rows
   return b;
 }

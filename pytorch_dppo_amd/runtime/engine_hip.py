@@ -631,7 +631,9 @@ class HipEngine:
         into ``ls`` (in place, fp64) before normalising it (csrc/rollout.hip sn_step)."""
         if self._sn_bufs is None:
             nroll = self.mom.shape[0]
-            self._sn_bufs = (torch.zeros(nroll * 2 * self.O, dtype=torch.int64, device=self.device),
+            # (csrc/kernels.h sn_g1_elems: 4-feature x 4-workgroup line blocks)
+            g1n = 2 * (-(-self.O // 4)) * (-(-nroll // 4)) * 16
+            self._sn_bufs = (torch.zeros(g1n, dtype=torch.int64, device=self.device),
                              torch.zeros(2 * self.O, dtype=torch.int64, device=self.device),
                              torch.zeros(1, dtype=torch.int32, device=self.device),
                              torch.zeros(1, dtype=torch.int32, pin_memory=True))

@@ -57,10 +57,14 @@ def main():
     t0 = ab[:, :, 0][ab[:, :, 0] > 0].min()
     us = (ab - t0) / 100.0
     wg = us.amax(dim=1)                    # [nblk, 4]: entry, moments published, reduce done, gather done
-    red = us[:, 0, 2]                      # wave 0 of every workgroup is a reducer (features < nblk)
+    nred = min(nblk, (eng.O + 3) // 4)     # workgroups whose wave 0 reduces a 4-feature unit
+    red = us[:nred, 0, 2]
     q = lambda v: [round(float(v.min()), 2), round(float(v.median()), 2), round(float(v.max()), 2)]
     skew = {"entry": q(wg[:, 0]), "moments published": q(wg[:, 1]), "reducers done (wave 0)": q(red),
             "gather done": q(wg[:, 3])}
+    npl = buf.view(nblk, 8, 16)[:, :, 15]
+    skew["reduce polls (reducers, wave 0)"] = q((npl[:nred, 0] & 0xFFFFFFFF).double())
+    skew["gather polls (wave 7)"] = q((npl[:, 7] >> 32).double())
     print(json.dumps({"rollout_ms": round(ms, 4), "cycles_per_step(median blk, max wave)": per,
                       "sum": sum(per.values()), "step8_us_min_median_max": skew}, indent=1), flush=True)
 
