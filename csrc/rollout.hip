@@ -66,7 +66,10 @@ DEV float sn_val(u64 x) { return __uint_as_float((unsigned)x); }
 // and publishes the (mean, 1/std) granules.  The values of a poll pass whose tags all match are
 // the values.  (pf: the first unit's running (mean, M2), loaded by wave 0's lanes 0-3 at the
 // start of the step — off the hand-off's critical path.)  Returns false on a timeout (after the
-// workgroup's barriers).
+// workgroup's barriers).  Measured per rollout at 4,096 envs (profiles/r5/filter_probe_*): one
+// reducer wave per feature 0.50 ms; one workgroup per 16-feature line block 0.60 ms (4 us per poll
+// pass of 512 lines); 4x4 lines on waves 0-3 0.449 ms; on all 8 waves 0.415 ms; 2 features x 8
+// workgroups per line 0.425 ms — the pass time follows each wave's outstanding line loads.
 template <int NW>
 DEV bool sn_reduce(const RolloutArgs& a, int nblk, int step, int wave, int lane, const float* shs,
                    double* red, double pmean, double pm2, unsigned& npoll) {
