@@ -653,12 +653,16 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
       // out feature 64 go + 32 (w >> 1) + ph_dim(i, h) (registers), in feature 64 ih + 32 (w & 1)
-      // + (l & 31) (lanes): dst[part_dw + 4096 + out * 128 + in]
+      // + (l & 31) (lanes): dst[part_dw + 4096 + out * 128 + in]; only the entries the gather
+      // reads (out < n2, in <= n1: the bias column) — the kernel's tail is its stores (no vector
+      // memory instruction follows them, so no counted wait sees the difference)
+      const bool in_ok = 64 * ih + 32 * (wave & 1) + r <= a.n_out[0];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const unsigned o = (unsigned)(64 * go + 32 * (wave >> 1) + ph_dim(i, h));
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dw[i]), rs_part, base + (o * 128u + 64u * ih) * 4u, 0,
-                                              0);
+        if (in_ok && o < (unsigned)a.n_out[1])
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dw[i]), rs_part, base + (o * 128u + 64u * ih) * 4u,
+                                                0, 0);
       }
       bar();
     });
