@@ -298,11 +298,24 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
     }
     float tot = 0.f;
     int j;
+    // the item's optimizer state, loaded before the column sums (its latency overlaps theirs)
+    const int jj = ITEM_IPB * (int)blockIdx.x + (int)threadIdx.x;
+    int d = -1, wi = 0, wti = 0;
+    float mi = 0.f, vi = 0.f, pv = 0.f;
+    if ((int)threadIdx.x < ITEM_IPB && jj < nitems) {
+      d = red_dst[jj];
+      if (d >= 0) {
+        mi = m[d];
+        vi = v[d];
+        pv = p[d];
+        wi = w_map[d];
+        wti = wt_map[d];
+      }
+    }
     if (item_reduce(part, npblk, npart, red_col, nitems, blockIdx.x, red, tot, j)) {
-      const int d = red_dst[j];
       if (d >= 0) {
         const float gi = tot * scale;
-        update(d, gi, m[d], v[d], p[d], w_map[d], wt_map[d]);
+        update(d, gi, mi, vi, pv, wi, wti);
         ss = gi * gi;
       } else {
         loss_out[-1 - d] = tot;
