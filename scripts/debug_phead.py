@@ -75,8 +75,10 @@ def main():
     if mode != "full":
         report("x", dec(eng.xT)[:, :model.num_inputs], x, 1e-3)
     # the per-workgroup dW_mu blocks [32][128] (bias column 100) vs torch's sum over each block's rows
-    part = eng.part_joint
-    c0 = eng.part_dw_joint[0]
+    # (the joint world-1 path's partial rows, or the per-head path's)
+    joint = bool(eng.part_joint.abs().sum() > 0)
+    part = eng.part_joint if joint else eng.part_h[0]
+    c0 = eng.part_dw_joint[0] if joint else eng.part_dw[0]
     blk = part[: (M + 127) // 128, c0:c0 + 32 * 128].view(-1, 32, 128)
     A = model.num_outputs
     h2b = torch.cat([h2, torch.ones(M, 1, device=DEV)], 1)
