@@ -5,7 +5,7 @@ the max over waves) for the filter's moments / reduce (first hand-off) / gather 
 barrier, and the rest of the step; plus the rollout time without stamps, and the cross-workgroup
 spread of step 8's hand-offs (absolute 100 MHz stamps: min / median / max over workgroups).
 
-    python scripts/probe_filter_phases.py [reps]
+    python scripts/probe_filter_phases.py [reps] [step|rollout]
 """
 import json
 import os
@@ -26,11 +26,12 @@ NAMES = ["observe", "fc1", "fc2", "fc3", "sample", "logp/reward", "env", "sn mom
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    mode = sys.argv[2] if len(sys.argv) > 2 else "step"   # obs_norm_update: step | rollout
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     ctx = init_single_rank_collective(dev, port=free_port())
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536, batch_size=65536,
-                    dtype="bf16x3", seed=1, obs_norm_update="step")
+                    dtype="bf16x3", seed=1, obs_norm_update=mode)
     w = DPPOWorker(p, ctx)
     eng = w.engine
     for _ in range(2):
@@ -51,6 +52,10 @@ def main():
     eng.ext.set_rollout_tstamp(torch.empty(0, dtype=torch.int64, device=dev))
     t = buf.view(nblk, 8, 16)[:, :, :11].double() / eng.T
     per = {n: float(t[:, :, i].max(dim=1).values.median()) for i, n in enumerate(NAMES)}
+    if mode != "step":
+        print(json.dumps({"rollout_ms": round(ms, 4), "cycles_per_step(median blk, max wave)": per}, indent=1),
+              flush=True)
+        return
     # step 8's absolute 100 MHz stamps (slots 11-14): per workgroup the latest wave; relative to
     # the earliest filter entry, in microseconds
     ab = buf.view(nblk, 8, 16)[:, :, 11:15].double()
