@@ -314,7 +314,8 @@ __device__ __forceinline__ float slab_sum(const float* __restrict__ p, int nch, 
 // Column sums of the per-workgroup partial rows (the reduce items of the gather kernels): the
 // 256 threads of a block take items j = IPB b + (tid % IPB) (consecutive items are consecutive
 // columns: one 128-byte segment per row) in RG = 256 / IPB row groups; row group g sums rows
-// g, g + RG, ... in order (32 loads in flight: 512 partial rows are 2 dependent batches), then
+// g, g + RG, ... in order (16 loads in flight: 512 partial rows are 4 dependent batches; 32 in
+// flight took the gather kernel from 80 to 113 VGPRs, 6 to 4 waves per SIMD: fewer than its grid), then
 // thread tid < IPB adds the RG groups in order — fixed order, deterministic.  Returns true on the
 // threads that own an item (tid < IPB, j < nitems) with its sum in `out`.
 // red_dst[j] >= 0: flat gradient index (of the gathered slice); -1 - q: loss_out[q].
@@ -327,12 +328,12 @@ __device__ __forceinline__ bool item_reduce(const float* __restrict__ part, int 
   float s = 0.f;
   if (j < nitems && tid < 256) {   // (a 512-thread block: threads 256+ add zeros; red holds blockDim floats)
     const float* p = part + red_col[j];
-    for (int r0 = rg; r0 < nprow; r0 += 32 * RG) {
-      float x[32];
+    for (int r0 = rg; r0 < nprow; r0 += 16 * RG) {
+      float x[16];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) x[u] = (r0 + RG * u < nprow) ? p[(size_t)(r0 + RG * u) * npart] : 0.f;
+      for (int u = 0; u < 16; ++u) x[u] = (r0 + RG * u < nprow) ? p[(size_t)(r0 + RG * u) * npart] : 0.f;
 #pragma unroll
-      for (int u = 0; u < 32; ++u)
+      for (int u = 0; u < 16; ++u)
         if (r0 + RG * u < nprow) s += x[u];
     }
   }
