@@ -339,7 +339,9 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   // ROW-MAJOR ([ldT][512] / [ldT][512] / [ldT][128]); policy (csrc/phead.hip): h1p / g1p / g2p
   // ([ldT][128]) and, unless xT_ready, the observation rows into xT ([ldT][d0]).  The engine's
   // wgrad must read them so (its rm flags)
+  // (policy: opts[7] == 1 also sums p_fc2's weight gradient in the kernel, 2 stores h1p / g2p)
   const bool t32 = opts.size() == 8 && opts[7] != 0;
+  const bool p2 = t32 && head == 0 && opts[7] == 1;
   TORCH_CHECK(head >= -1 && head <= 1, "head: -1 (both heads, one kernel), 0 policy, 1 value");
   TORCH_CHECK(fopts.size() == 2, "fopts: clip, ent_coeff");
   TORCH_CHECK(tbufs.size() == 11, "11 transposed buffers");
@@ -413,8 +415,9 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   TORCH_CHECK(!(w8.defined() && w8.numel() > 0) || (dt == 1 && head >= 0), "w8: the fp8 mode's per-head bf16 update only");
   set_w8(a, w8, qscale, L);
   if (t32) {   // the row-major operand rows the kernels write are whole padded widths
-    const int64_t wid[11] = {head == 0 && !xT_ready ? L.d_in[0] : 0, 0, 0, head == 1 ? 512 : 0, 0,
-                             head == 0 ? 128 : 0, 0, 0, head == 1 ? 512 : 0, head == 1 ? 128 : 0, 0};
+    const int64_t pn = head == 0 && !p2 ? 128 : 0;   // h1p / g2p
+    const int64_t wid[11] = {head == 0 && !xT_ready ? L.d_in[0] : 0, pn, 0, head == 1 ? 512 : 0, 0,
+                             head == 0 ? 128 : 0, pn, 0, head == 1 ? 512 : 0, head == 1 ? 128 : 0, 0};
     for (int i = 0; i < 11; ++i)
       TORCH_CHECK(tbufs[i].numel() >= wid[i] * ldT, "t32 head: row-major operand buffer ", i, " too small");
   }
@@ -425,13 +428,14 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
     launch_vhead_train((int)dt, a, cur_stream());
   } else if (t32) {
     TORCH_CHECK(head == 0 && !q8 && a.W8 == nullptr && phead_shape_ok(a), "phead: the policy head at bf16x3 / bf16");
-    TORCH_CHECK(part_dw + 32 * 128 + 128 * 128 <= npart, "phead: the dW_mu and dW_p2 blocks must fit the partial row");
+    TORCH_CHECK(part_dw + 32 * 128 + (p2 ? 128 * 128 : 0) <= npart,
+                "phead: the dW_mu (and dW_p2) blocks must fit the partial row");
     const int64_t eb = dt == 3 ? 4 : 2;
     TORCH_CHECK(ldT * std::max<int64_t>(L.d_in[0], 128) * eb < (int64_t(1) << 31), "phead: row-major operands beyond 2 GiB");
     TORCH_CHECK((int64_t)nblk * npart * 4 < (int64_t(1) << 31), "phead: partial buffer beyond 2 GiB");
     TORCH_CHECK(ldT % phead_rows() == 0 && Mpad <= ldT && (L.d_in[0] >> 4) / (dt == 3 ? 1 : 2) >= 3,
                 "phead: ldT covers whole workgroups; fc1 has >= 3 stages");
-    launch_phead_train((int)dt, a, cur_stream());
+    launch_phead_train((int)dt, a, p2 ? 1 : 0, cur_stream());
   } else if (head >= 0) {
     launch_mlp_head((int)dt, (int)head, a, cur_stream());
   } else {

@@ -155,7 +155,8 @@ extern "C" void set_vhead(int enable);
 extern "C" int phead_applies(const MlpArgs& a);   // set_phead flag and shapes
 extern "C" int phead_shape_ok(const MlpArgs& a);
 extern "C" int phead_rows();
-extern "C" void launch_phead_train(int dt, const MlpArgs& a, hipStream_t s);
+// p2: p_fc2's weight gradient summed in the kernel (else h1p / g2p stored row-major for the wgrad)
+extern "C" void launch_phead_train(int dt, const MlpArgs& a, int p2, hipStream_t s);
 extern "C" void set_phead(int enable);
 
 // fp8 mode: the Adam kernels also refresh the e4m3 image the update's fc1 reads (csrc/mlp_head.hip

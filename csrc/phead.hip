@@ -83,7 +83,11 @@ DEV bf16x8 cat8(s16x4 a0, s16x4 a1) {
 // dimension of accumulator register i of a 32x32 tile on lane half h (t32.h layout)
 DEV int ph_dim(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-template <int DT>
+// P2: sum p_fc2's weight gradient in the kernel (dW_p2 partial blocks; h1 / g2 stay on chip) —
+// the bf16x3 path (4.26 -> 4.15 ms per iteration, same box); at bf16 the operands' HBM round trip
+// is half as many bytes and the kernel stores h1 / g2 row-major for the wgrad instead (2.27 vs
+// 2.36 ms with P2; profiles/r5/ab_p2_by_dtype.log)
+template <int DT, bool P2>
 __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
   using V = VT<DT>;
   using Frag = typename V::Frag;
@@ -206,6 +210,11 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
   // row-major operand stores of this lane's row (the launcher checks ldT * max(d0, 128) * EB < 2^31)
   const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(a.xT, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_g1 = __builtin_amdgcn_make_buffer_rsrc(a.g1pT, (short)0, 0x7fffffff, 0x00020000);
+  // (!P2: h1 and g2 row-major for the wgrad's p_fc2 tiles)
+  const __amdgpu_buffer_rsrc_t rs_h1 =
+      __builtin_amdgcn_make_buffer_rsrc(P2 ? a.g1pT : a.h1pT, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_g2 =
+      __builtin_amdgcn_make_buffer_rsrc(P2 ? a.g1pT : a.g2pT, (short)0, 0x7fffffff, 0x00020000);
   const unsigned vx = (unsigned)(mr * d0 + 8 * h) * EB, v128 = (unsigned)(mr * 128 + 8 * h) * EB;
   const bool write_x = a.xT_ready == 0;
   const int xst = write_x ? 2 : 0;   // X operand stores per fc1 step
@@ -309,6 +318,10 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
     for (int e = 0; e < KPS; ++e) {
       const int k16 = KPS * j + e;
       b[e] = b_operand<DT>(acc1[k16 >> 1], k16 & 1);
+      if constexpr (!P2) sto(rs_h1, v128, 16 * k16 * EB, b[e]);
+    }
+    if constexpr (!P2 && S3 && j == NS2 - 1) {
+      sto(rs_h1, v128, 16 * 7 * EB, b_operand<DT>(acc1[3], 1));
     }
     ring_mma<DT, 4 * KPS, (S3 ? 1 : 2)>(stg, lane, [&](int i) { return i; },
                                         [&](int i, const Frag& w) __attribute__((always_inline)) {
@@ -580,6 +593,14 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
     static_for_vh<0, NG2 / 2>([&](auto jc) __attribute__((always_inline)) {
       constexpr int jj = decltype(jc)::value, j = pass * (NG2 / 2) + jj;
       const char* stg = sync_late(eg3 + j);
+      if constexpr (!P2) {
+        if constexpr (S3) {
+          sto(rs_g2, v128, 16 * j * EB, j < NGB ? gb[j < NGB ? j : 0] : Frag{});
+        } else {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) sto(rs_g2, v128, 16 * (2 * j + e) * EB, gb[2 * j + e]);
+        }
+      }
       // (split: the last stage's k-step 7 is zero: its 2 fragments are not multiplied)
       constexpr int NF = (S3 && jj == NG2 / 2 - 1) ? 2 : 4 * KPS;
       ring_mma<DT, NF, (S3 ? 1 : 2)>(stg, lane, [&](int i) { return i; },
@@ -603,7 +624,7 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
   // round trip through HBM and the wgrad): four rounds of an out-half of g2 and an in-half of h1
   // staged row-major in the freed ring + scratch (2 x 32 KiB), wave w taking the round's tile
   // (out 64 go + 32 (w >> 1), in 64 ih + 32 (w & 1)) with K = all 128 rows (fixed order) ----
-  {
+  if constexpr (P2) {
     static_assert(2 * 2 * PH_HP <= PH_S * PH_SB + PH_SCR, "two staged halves fit the ring + scratch");
     char* Gs = smem;                  // g2 out-half [2 planes][128 rows][128 B]
     char* Hs = smem + 2 * PH_HP;      // h1 in-half  [2 planes][128 rows][128 B]
@@ -694,14 +715,20 @@ extern "C" int phead_applies(const MlpArgs& a) { return g_phead && phead_shape_o
 
 extern "C" int phead_rows() { return PH_ROWS; }
 
-extern "C" void launch_phead_train(int dt, const MlpArgs& a, hipStream_t s) {
+template <int DT, bool P2>
+void launch_ph(const MlpArgs& a, int nblk, hipStream_t s) {
+  set_max_lds_once<phead_kernel<DT, P2>>(ph_lds_bytes());
+  hipLaunchKernelGGL((phead_kernel<DT, P2>), dim3(nblk), dim3(PH_WAVES * 64), ph_lds_bytes(), s, a);
+}
+
+extern "C" void launch_phead_train(int dt, const MlpArgs& a, int p2, hipStream_t s) {
   const int nblk = (a.M + PH_ROWS - 1) / PH_ROWS;
   if (dt == DT_S3) {
-    set_max_lds_once<phead_kernel<DT_S3>>(ph_lds_bytes());
-    hipLaunchKernelGGL((phead_kernel<DT_S3>), dim3(nblk), dim3(PH_WAVES * 64), ph_lds_bytes(), s, a);
+    if (p2) launch_ph<DT_S3, true>(a, nblk, s);
+    else launch_ph<DT_S3, false>(a, nblk, s);
   } else {
-    set_max_lds_once<phead_kernel<DT_BF16>>(ph_lds_bytes());
-    hipLaunchKernelGGL((phead_kernel<DT_BF16>), dim3(nblk), dim3(PH_WAVES * 64), ph_lds_bytes(), s, a);
+    if (p2) launch_ph<DT_BF16, true>(a, nblk, s);
+    else launch_ph<DT_BF16, false>(a, nblk, s);
   }
   HIP_CHECK_LAUNCH();
 }

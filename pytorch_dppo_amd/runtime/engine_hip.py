@@ -170,6 +170,10 @@ class HipEngine:
         # gathered rows in xT for a minibatch
         self.phead = (self.heads and not self.fp8 and bool(params.phead_kernel)
                       and bool(self.ext.phead_train_applies(self.dt, self.layout, A)))
+        # ... summing p_fc2's weight gradient itself at bf16x3 (h1p / g2p never reach HBM: 4.26 ->
+        # 4.15 ms per iteration); at bf16 their round trip is half the bytes and storing them for
+        # the wgrad is faster (2.27 vs 2.36 ms; same box, profiles/r5/ab_p2_by_dtype.log)
+        self.phead_p2 = self.phead and self.dt == native.DT_CODE["bf16x3"]
         # the gradient-amax ring: 3 slots x 4 tensors x 64 sub-slot lines of 32 dwords (csrc/kernels.h)
         self.q8_amax = torch.zeros(3 * 4 * Q8_SUB * 32, dtype=torch.int32, device=device)
         self._q8_next = 0          # step counter of the amax ring
@@ -190,9 +194,9 @@ class HipEngine:
         # the wgrad
         self.nhead_blk = self.ldT // 128
         self.part_dw = [_r(8 + A, 4), 8]
-        # (the 32x32 policy head also sums p_fc2's weight gradient [128][128] right after dW_mu:
-        # p_fc2 leaves the wgrad, and h1p / g2p their HBM round trip)
-        np_pol = self.part_dw[0] + 32 * 128 + (128 * 128 if self.phead else 0)
+        # (the 32x32 policy head at bf16x3 also sums p_fc2's weight gradient [128][128] right after
+        # dW_mu: p_fc2 leaves the wgrad, and h1p / g2p their HBM round trip)
+        np_pol = self.part_dw[0] + 32 * 128 + (128 * 128 if self.phead_p2 else 0)
         self.part_h = [torch.zeros(self.nhead_blk, np_pol, **f32), torch.zeros(self.nhead_blk, 8 + 128, **f32)]
         # world size 1: both head kernels write ONE partial buffer (policy its columns, value
         # column 1 and its dW_v after the policy's block) and one wgrad + gather/Adam launch
@@ -341,8 +345,8 @@ class HipEngine:
                           if self.device.type == "cuda" else 256)
         ls = self.L.layers
         names = [l.name for l in ls]
-        # (the 32x32 policy head sums p_fc2's weight gradient itself)
-        pol = ("p_fc1",) if getattr(self, "phead", False) else ("p_fc1", "p_fc2")
+        # (the 32x32 policy head at bf16x3 sums p_fc2's weight gradient itself)
+        pol = ("p_fc1",) if getattr(self, "phead_p2", False) else ("p_fc1", "p_fc2")
         if self.heads and joint:
             groups = [[names.index(n) for n in pol + ("v_fc1", "v_fc2")]]
             ranges = [(self.A, model.num_params)]
@@ -515,7 +519,7 @@ class HipEngine:
                 for j in range(A):
                     add(kind, 8 + j, j)
                 narrow(kind, "mu", dwp, 0)
-                if self.phead:
+                if self.phead_p2:
                     narrow(kind, "p_fc2", dwp + 32 * 128, 0)
             if dwv is not None:
                 add(kind, 1, -2)
@@ -1018,7 +1022,7 @@ class HipEngine:
         t32 = (h == 1 and self.vhead) or (h == 0 and self.phead)
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
                 1 if p.std_convention == "var" else 0, 1 if first else 0, part.shape[1], h, part_dw,
-                1 if t32 else 0]
+                (2 if h == 0 and not self.phead_p2 else 1) if t32 else 0]
         if h == 0 and self.phead:
             # full batch: the rollout's fragment-major x^T if it wrote one (read by the wgrad as
             # before), else x_buf's rows; a minibatch: the kernel gathers its observation rows

@@ -92,10 +92,13 @@ def main():
     print("   block0 nonzero entries", nz.shape[0], nz[:8].tolist(), flush=True)
     # the per-workgroup dW_p2 blocks [128 out][128 in] (bias column 100; only out < 100, in <= 100
     # are written) vs torch's sum over each block's rows
-    b2 = part[: (M + 127) // 128, c0 + 32 * 128:c0 + 32 * 128 + 128 * 128].view(-1, 128, 128)[:, :100, :101]
-    h1b = torch.cat([h1, torch.ones(M, 1, device=DEV)], 1)
-    ref2 = torch.stack([g2[128 * b_:128 * (b_ + 1)].t() @ h1b[128 * b_:128 * (b_ + 1)] for b_ in range(b2.shape[0])])
-    print("dW_p2 blocks: max err", (b2 - ref2).abs().max().item(), "ref absmax", ref2.abs().max().item(), flush=True)
+    if eng.phead_p2:   # (bf16: h1p / g2p go to the wgrad instead)
+        b2 = part[: (M + 127) // 128, c0 + 32 * 128:c0 + 32 * 128 + 128 * 128].view(-1, 128, 128)[:, :100, :101]
+        h1b = torch.cat([h1, torch.ones(M, 1, device=DEV)], 1)
+        ref2 = torch.stack([g2[128 * b_:128 * (b_ + 1)].t() @ h1b[128 * b_:128 * (b_ + 1)]
+                            for b_ in range(b2.shape[0])])
+        print("dW_p2 blocks: max err", (b2 - ref2).abs().max().item(), "ref absmax", ref2.abs().max().item(),
+              flush=True)
     g = eng.grad_flat
     for k_ in ("log_std", "p_fc1.weight", "p_fc1.bias", "p_fc2.weight", "p_fc2.bias", "mu.weight", "mu.bias",
                "v_fc1.weight", "v_fc2.weight", "v.weight"):

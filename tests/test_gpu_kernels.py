@@ -199,7 +199,7 @@ def test_phead_update_matches_16x16_head_update(dtype, loss, mb, vh):
     """The policy head's update on the 32x32 transposed-chain kernel (csrc/phead.hip: row-major
     h1p / g1p / g2p, the observation operand of both fc1 layers row-major — x_buf itself for a
     full batch (mb None), the kernel's gathered rows for a minibatch; dW_mu by MFMA over the
-    LDS-staged h2 / dL/dmu) vs the 16x16 head kernels: the whole gradient, the loss sums and the
+    LDS-staged h2 / dL/dmu; at bf16x3 dW_p2 too) vs the 16x16 head kernels: the whole gradient, the loss sums and the
     reference loss's mu_prev; vs autograd for the ppo loss.  Ragged minibatches (1000, 768) leave
     rows past M in the last workgroup (zero gradient)."""
     N = 128 * 16
@@ -213,6 +213,8 @@ def test_phead_update_matches_16x16_head_update(dtype, loss, mb, vh):
         p.phead_kernel = ph
         eng, model, _, _ = _engine(p)
         assert eng.phead == ph and eng.vhead == (ph and vh)
+        # (bf16x3: p_fc2's weight gradient summed in the kernel; bf16: h1p / g2p row-major for the wgrad)
+        assert eng.phead_p2 == (ph and not bf)
         xq = _fill_buffer(eng, model)
         idx = None if mb is None else torch.randperm(eng.N, generator=torch.Generator().manual_seed(5))[:mb]
         eng.begin_update()
