@@ -116,6 +116,9 @@ def main():
     ap.add_argument("--overlap-rollout", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
                     help="the last value-head all-reduce + Adam overlap the next rollout on a side stream (exact: "
                          "the rollout reads only the policy); auto = on when the world has more than one rank")
+    ap.add_argument("--overlap-value", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
+                    help="every epoch's value-head all-reduce + Adam on a side stream, joined before the next value "
+                         "kernel (exact); auto = the measured default (docs/ARCHITECTURE.md §13: off)")
     ap.add_argument("--force-collectives", action="store_true",
                     help="diagnostics: run the hot-path RCCL collectives even at world size 1")
     ap.add_argument("--phase-timing", type=int, default=0,
@@ -147,6 +150,7 @@ def main():
     # the north-star configuration at N > 1: the last epoch's value all-reduce + Adam beside the
     # next rollout (bit-identical to stream order: test_head_chains_through_rccl_bit_identical_to_fused)
     args.overlap_rollout = args.overlap_rollout == "on" or (args.overlap_rollout == "auto" and world > 1)
+    args.overlap_value = args.overlap_value == "on"
     if world > 1:
         ctx = init_distributed("gpu", timeout_s=args.dist_timeout_s, backend=args.dist_backend,
                                grad_comm=args.grad_comm)
@@ -165,6 +169,7 @@ def main():
         p = dppo_preset(device="gpu", env_name=args.env_name, num_envs=E, exploration_size=rows,
                         batch_size=args.batch_size or rows, num_epoch=args.num_epoch, dtype=dtype,
                         num_processes=ctx.world_size, seed=1, overlap_rollout=args.overlap_rollout,
+                        overlap_value_epochs=args.overlap_value,
                         dist_backend=args.dist_backend, grad_comm=args.grad_comm,
                         dist_timeout_s=args.dist_timeout_s,
                         phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
@@ -218,6 +223,11 @@ def main():
                    "rccl_in_stream" if ctx.backend == "nccl" else "gloo_in_stream")
     t32_heads = [k for k, on in (("value", getattr(w.engine, "vhead", False)),
                                  ("policy", getattr(w.engine, "phead", False))) if on]
+    # what the engine DID with the value-head steps (not what the flags asked for): run on the side
+    # stream (a second communicator), left pending on a process-group all-reduce, or in stream order
+    n_iter = args.warmup + args.steps
+    side_steps, pend_steps = int(getattr(w.engine, "side_steps", 0)), int(getattr(w.engine, "pending_steps", 0))
+    overlap_value_step = "side_stream" if side_steps else ("pending_work" if pend_steps else "none")
     del w
     variants = {}
     for dt in [d for d in args.variants.split(",") if d and d != args.dtype]:
@@ -242,11 +252,11 @@ def main():
                           "minibatch_rows": p.minibatch_rows(), "overlap_rollout": args.overlap_rollout,
                           "per_head_kernels": heads, "grad_allreduce": grad_ar,
                           "t32_heads": t32_heads,
-                          # --overlap-rollout on the in-stream path: the last value-head all-reduce +
-                          # Adam run on a side stream (second communicator) beside the next rollout
-                          "overlap_value_step": ("side_stream" if args.overlap_rollout and ctx.native_side is not None
-                                                 else "pending_work" if args.overlap_rollout and ctx.collective
-                                                 else "none"),
+                          # counted by the engine: value-head all-reduce + Adam steps that ran on the
+                          # side stream (--overlap-rollout: the last epoch's, beside the next rollout;
+                          # --overlap-value: every epoch's) or pending on a process-group all-reduce
+                          "overlap_value_step": overlap_value_step,
+                          "overlapped_value_steps_per_iter": (side_steps + pend_steps) / max(n_iter, 1),
                           "note": ("value = total env steps/s of all n_gpus workers (one DPPO worker per GPU); "
                                    "the 8-worker node figure of the metric is the n_gpus=8 run; vs_baseline "
                                    "divides by the reference's derived 8-worker CPU node estimate (BASELINE.md)"),

@@ -496,6 +496,9 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
   {
     char* Hp = scr;                     // [2 planes][128 rows][128 B]
     char* Dp = scr + 2 * PH_HP;         // [2 planes][128 rows][64 B]
+    // every wave's loss has read its actions (acts, in the scratch the staging below overwrites:
+    // Dp covers wave 2's, the split Hp lo plane waves 0 / 1's) before any wave stages
+    bar();
 #pragma unroll
     for (int s = 0; s < 2; ++s) put(Dp, row * 64, 2 * s + h, db[s], PH_DP);
 #pragma unroll
@@ -703,10 +706,11 @@ int g_phead = 1;
 
 }  // namespace
 
-// the shapes the kernel covers: the reference policy (d0 -> 100 -> 100 -> A <= 32; any observation
-// width <= 384 that is a multiple of 32)
+// the shapes the kernel covers: the reference policy (d0 -> 100 -> 100 -> A <= 32; observation
+// widths 128, 256, 384: the wgrad reads the observation operand as row-major rows of the operand
+// width, d0 rounded up to its 128-row tile, so x_buf's rows serve only when d0 is that width)
 extern "C" int phead_shape_ok(const MlpArgs& a) {
-  return a.d_in[0] % 32 == 0 && a.d_in[0] >= 64 && a.d_in[0] <= 384 && a.d_out[0] == 128 && a.n_out[0] < 128 &&
+  return a.d_in[0] % 128 == 0 && a.d_in[0] >= 128 && a.d_in[0] <= 384 && a.d_out[0] == 128 && a.n_out[0] < 128 &&
          a.n_out[0] >= 97 && a.d_in[1] == 128 && a.d_out[1] == 128 && a.n_out[1] < 128 && a.n_out[1] >= 97 &&
          a.d_in[2] == 128 && a.d_out[2] == 32 && a.A >= 1 && a.A <= 32 && a.n_out[2] <= 32;
 }

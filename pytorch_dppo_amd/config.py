@@ -73,6 +73,12 @@ class Params:
     # head's last step stays pending until after the next rollout (which reads only the policy:
     # exact); CPU engine: the whole last step (option b, a 1-update policy lag)
     overlap_rollout: bool = False
+    # GPU engine, in-stream communicator (the default at N > 1): EVERY epoch's value-head all-reduce
+    # + Adam on a side stream (second communicator), joined just before the next value kernel, so
+    # it runs beside the next epoch's policy Adam + policy kernel (chief.py:13-20's sum -> Adam ->
+    # release off the critical path, once per epoch).  Exact (the policy chain reads no value
+    # parameter).  False: stream order (only the last epoch's, with overlap_rollout)
+    overlap_value_epochs: bool = False
     dist_timeout_s: float = 300.0
     verify_sync_every: int = 0           # debug param-checksum all-reduce period
     adam_betas: tuple = (0.9, 0.999)

@@ -295,6 +295,8 @@ class HipEngine:
         # process-group chains, or ("side", None, step, mean) when it runs on the side stream
         self._pending_value = None
         self._side: Optional[torch.cuda.Stream] = None   # the side stream of the overlapped value step
+        self.side_steps = 0          # value steps run on the side stream (bench / tests report it)
+        self.pending_steps = 0       # value steps left pending on a process-group all-reduce
         # world-size-1 fast path: grad_gather + no-clip Adam in one launch (fused_apply=False: off)
         self.fused_apply = bool(params.fused_apply)
         self.idx_dev = torch.zeros(self.ldT, dtype=torch.int32, **dev)
@@ -449,10 +451,11 @@ class HipEngine:
             return (self.q8_amax, self._q8_step, [0, 1, -1, 2, 3, -1], [Q8_SX, Q8_SH, 1.0, Q8_SX, Q8_SH, 1.0])
         return (self.empty, 0, [-1] * 6, [1.0] * 6)
 
-    def _wgrad(self, b: Dict) -> None:
-        """one wgrad launch over bucket b's tasks (Q8: e4m3 operands, the step's scales)"""
-        wg_x = self.wg_x_full if (self.phead and self._x_mode == "buf") else self.wg_x
-        rm = self.rm_xfm if (not self.phead or self._x_mode == "fm") else self.rm
+    def _wgrad(self, b: Dict, xmode: str) -> None:
+        """one wgrad launch over bucket b's tasks (Q8: e4m3 operands, the step's scales); ``xmode``
+        = where the minibatch's observation operand is (_minibatch: "fm" / "buf" / "mb")"""
+        wg_x = self.wg_x_full if (self.phead and xmode == "buf") else self.wg_x
+        rm = self.rm_xfm if (not self.phead or xmode == "fm") else self.rm
         self.ext.wgrad(self._wgrad_dt(), self.wg_g, wg_x, self.g_rows, self.x_rows, self.ldT, b["tasks"],
                        b["tasks_host"], b["slab"], *self._q8_args(), rm)
 
@@ -867,7 +870,13 @@ class HipEngine:
 
     # ------------------------------------------------------------------------------------------
     def _minibatch(self, idx: Optional[torch.Tensor]):
-        """(index tensor, row0, first-step flag, x^T-ready flag) of one minibatch call"""
+        """(index tensor, first-step flag, x^T-ready flag, x-mode) of one minibatch call.
+
+        x-mode: where the observation operand of p_fc1 / v_fc1's weight gradient is — "fm" the
+        rollout's fragment-major x^T (full batch), "buf" x_buf's own rows (full batch under the
+        32x32 policy head: no x^T written), "mb" the rows the policy kernel gathers into xT
+        (minibatch).  Decided here, from the minibatch alone, and passed to both the head
+        kernels and the wgrad (no engine state couples them)."""
         M = self.mb
         if idx is None:
             assert M == self.N, "full-batch call needs minibatch == buffer"
@@ -882,10 +891,21 @@ class HipEngine:
             self.idx_dev[:M].copy_(idx.to(torch.int32), non_blocking=True)
             idx_t = self.idx_dev
         first, xt_ready = bool(self._first_step), bool(idx is None and self._xT_valid)
+        xmode = "fm"
+        if self.phead:
+            # (measured: the fragment-major x^T beside the row-major policy operands made the
+            # wgrad slower than x_buf's rows — 4.378 vs 4.214 ms per bf16x3 iteration, profiles/r5 —
+            # so x_buf's rows come first and the rollout writes no x^T when they can serve)
+            full = idx is None
+            if full and self.wg_x_full is not self.wg_x:
+                xmode, xt_ready = "buf", True
+            elif not (full and xt_ready):
+                xmode, xt_ready = "mb", False
+        self._x_mode = xmode      # (diagnostics / tests only)
         self._first_step = False
         self._q8_step, self._q8_next = self._q8_next, self._q8_next + 1
         self._loss_dev = self.loss_sums
-        return idx_t, first, xt_ready
+        return idx_t, first, xt_ready, xmode
 
     def can_fuse_apply(self, extra_grad: float = 0.0) -> bool:
         """the one-kernel path's grad(idx, apply=True): one gradient range, no clipping (the Adam
@@ -905,9 +925,11 @@ class HipEngine:
         size 1.  In-stream communicators (``allreduce.in_stream``: the native RCCL one — the
         default on an RCCL group — or the gloo adapter) reduce in stream order and do the mean
         themselves: joint kernels (one wgrad, one gather) → all-reduce → whole-vector Adam.
-        With ``last`` (the iteration's final step) under --overlap-rollout and a side
-        communicator, the value head's all-reduce + Adam go to a side stream instead and overlap
-        the next rollout, which reads only the policy (exact; joined in rollout()/values()).
+        With a side communicator, the value head's all-reduce + Adam go to a side stream instead:
+        every epoch's under ``overlap_value_epochs`` (joined right before the next value kernel,
+        so they overlap the policy Adam and the next policy kernel), and the iteration's last
+        (``last``) under --overlap-rollout (overlapping the next rollout, which reads only the
+        policy; joined in rollout()/values()).  Exact either way.
 
         Process-group collectives (``allreduce(t)`` returns an async work handle): per-head
         chains.  The policy range's all-reduce is issued as soon as it is gathered and runs while
@@ -923,16 +945,18 @@ class HipEngine:
             self.grad(idx, apply=True)          # world size 1: gather + Adam in one launch
             return
         if getattr(allreduce, "in_stream", False):
-            self._flush_value()
             if self.heads:
-                idx_t, first, xt_ready = self._minibatch(idx)
-                self._joint_grad(idx_t, first, xt_ready)
+                # (a value step of the previous epoch still on the side stream is joined inside,
+                # right before the value kernel: it ran beside this epoch's policy kernel)
+                self._joint_grad(*self._minibatch(idx))
             else:
+                self._flush_value()
                 self.grad(idx)
-            if (last and p.overlap_rollout and self.heads and getattr(allreduce, "side", False)
-                    and not clip and not extra_grad):
+            if (self.heads and getattr(allreduce, "side", False) and not clip and not extra_grad
+                    and (p.overlap_value_epochs or (last and p.overlap_rollout))):
                 self._split_step_side(allreduce)
                 return
+            self._flush_value()
             allreduce(self.grad_flat)           # sum / mean in stream order: no host-side scaling
             self.apply(extra_grad)
             return
@@ -942,10 +966,10 @@ class HipEngine:
                 self._reduce_wait(allreduce(self.grad_flat), self.grad_flat, mean)
             self.apply(extra_grad)
             return
-        idx_t, first, xt_ready = self._minibatch(idx)
+        mbt = self._minibatch(idx)
         if clip or extra_grad:
             self._flush_value()
-            self._heads_grad(idx_t, first, xt_ready)
+            self._heads_grad(*mbt)
             if allreduce is not None:
                 self._reduce_wait(allreduce(self.grad_flat), self.grad_flat, mean)
             self.apply(extra_grad)
@@ -954,24 +978,26 @@ class HipEngine:
             allreduce = lambda t: None          # noqa: E731
         step_no = self.adam_step + 1
         (plo, phi), (vlo, vhi) = self.head_range
-        self._head_chain(0, idx_t, first, xt_ready)
+        self._head_chain(0, *mbt)
         wp = allreduce(self.grad_flat[plo:phi])
         self._flush_value()
-        self._head_chain(1, idx_t, first, xt_ready)
+        self._head_chain(1, *mbt)
         self._pending_value = ("work", allreduce(self.grad_flat[vlo:vhi]), step_no, mean)
+        self.pending_steps += 1
         self._reduce_wait(wp, self.grad_flat[plo:phi], mean)
         self._head_adam(0, step_no)
         self.adam_step += 1
         self._norm_n = self.norm_regions[1][1]
 
     def _split_step_side(self, allreduce) -> None:
-        """the joint gradient is gathered: policy all-reduce + Adam in stream order, then the
-        value range's all-reduce (the side communicator) + Adam on the side stream, fenced by the
-        stream dependency; rollout() / values() / finish_steps() join it (_flush_value)."""
+        """the joint gradient is gathered: the value range's all-reduce (the side communicator) +
+        Adam are forked to the side stream right away, then the policy range's all-reduce + Adam
+        run in stream order (the two collectives on two communicators may run concurrently).  The
+        next value kernel (_joint_heads), rollout() / values() / finish_steps() join it
+        (_flush_value): it overlaps the policy Adam and the next epoch's policy kernel, or the next
+        rollout after the last epoch."""
         (plo, phi), (vlo, vhi) = self.head_range
         step_no = self.adam_step + 1
-        allreduce(self.grad_flat[plo:phi])
-        self._head_adam(0, step_no)
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.device)
         side = self._side
@@ -979,7 +1005,10 @@ class HipEngine:
         with torch.cuda.stream(side):
             allreduce(self.grad_flat[vlo:vhi], stream=side)
             self._head_adam(1, step_no)
+        allreduce(self.grad_flat[plo:phi])
+        self._head_adam(0, step_no)
         self._pending_value = ("side", None, step_no, False)
+        self.side_steps += 1
         self.adam_step += 1
         self._norm_n = self.norm_regions[1][1]
 
@@ -1013,9 +1042,9 @@ class HipEngine:
         if mean:
             t.mul_(1.0 / torch.distributed.get_world_size())
 
-    def _heads_grad(self, idx_t, first: bool, xt_ready: bool) -> None:
+    def _heads_grad(self, idx_t, first: bool, xt_ready: bool, xmode: str) -> None:
         for h in (0, 1):
-            self._head_chain(h, idx_t, first, xt_ready)
+            self._head_chain(h, idx_t, first, xt_ready, xmode)
 
     def _head_kernel(self, h: int, idx_t, first: bool, xt_ready: bool, part: torch.Tensor, part_dw: int) -> None:
         p, M = self.p, self.mb
@@ -1023,21 +1052,8 @@ class HipEngine:
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
                 1 if p.std_convention == "var" else 0, 1 if first else 0, part.shape[1], h, part_dw,
                 (2 if h == 0 and not self.phead_p2 else 1) if t32 else 0]
-        if h == 0 and self.phead:
-            # full batch: the rollout's fragment-major x^T if it wrote one (read by the wgrad as
-            # before), else x_buf's rows; a minibatch: the kernel gathers its observation rows
-            # into xT (row-major).  The kernel writes X rows only in the last case.
-            # (measured: the fragment-major x^T beside the row-major policy operands made the
-            # wgrad slower than x_buf's rows — 4.378 vs 4.214 ms per bf16x3 iteration, profiles/r5 —
-            # so x_buf's rows come first and the rollout writes no x^T when they can serve)
-            full = idx_t is self.empty
-            if full and self.wg_x_full is not self.wg_x:
-                self._x_mode, xt_ready = "buf", True
-            elif full and xt_ready:
-                self._x_mode = "fm"
-            else:
-                self._x_mode, xt_ready = "mb", False
-
+        # (the 32x32 policy kernel: xt_ready as _minibatch resolved it — it writes X rows into xT
+        # only for x-mode "mb", a minibatch)
         # fp8: the value head's fc1 on the e4m3 image; the policy's GEMMs only with fp8_policy_gemms
         w8 = self._w8() if (h == 1 or p.fp8_policy_gemms) else (self.no_u8, self.no_q)
 
@@ -1059,32 +1075,34 @@ class HipEngine:
         if h == 0 and p.loss == "dppo_ref":
             self.log_std_old.copy_(self.model.flat.data[:self.A])   # train.py:164, before Adam moves it
 
-    def _joint_heads(self, idx_t, first: bool, xt_ready: bool) -> None:
+    def _joint_heads(self, idx_t, first: bool, xt_ready: bool, xmode: str) -> None:
         """both head kernels into the shared partial buffer (disjoint columns and operands), in
         stream order.  (Measured: the policy kernel on a side stream concurrent with the value
         kernel, joined before the wgrad: 4.57 vs 4.39 ms per iteration, same box — each kernel
         fills a CU's LDS, so they only time-slice the CUs and the stream hand-offs are extra.)"""
         for h in self.head_order:
+            if h == 1:
+                self._flush_value()   # the previous step's value Adam (side stream) lands first
             self._head_kernel(h, idx_t, first, xt_ready, self.part_joint, self.part_dw_joint[h])
 
-    def _joint_grad(self, idx_t, first: bool, xt_ready: bool) -> None:
+    def _joint_grad(self, idx_t, first: bool, xt_ready: bool, xmode: str) -> None:
         """both head kernels (one shared partial buffer), ONE wgrad over both heads' layers, ONE
         gather of the whole gradient into grad_flat (no optimizer step)"""
-        self._joint_heads(idx_t, first, xt_ready)
+        self._joint_heads(idx_t, first, xt_ready, xmode)
         b = self.joint_bucket
-        self._wgrad(b)
+        self._wgrad(b, xmode)
         src_off, src_meta = self.joint_src
         rc, rd = self.items["joint"]
         self.ext.grad_gather(b["slab"], src_off, src_meta, self.part_joint, self.nhead_blk, self.part_joint.shape[1],
                              rc, rd, 1.0 / self.mb, self.grad_flat, self.loss_sums, b["runs"])
 
-    def _joint_step(self, idx_t, first: bool, xt_ready: bool) -> None:
+    def _joint_step(self, idx_t, first: bool, xt_ready: bool, xmode: str) -> None:
         """world size 1: policy kernel, value kernel (one shared partial buffer), ONE wgrad over
         both heads' layers, ONE gather + Adam launch over the whole flat vector"""
         p, M = self.p, self.mb
-        self._joint_heads(idx_t, first, xt_ready)
+        self._joint_heads(idx_t, first, xt_ready, xmode)
         b = self.joint_bucket
-        self._wgrad(b)
+        self._wgrad(b, xmode)
         b1, b2 = p.adam_betas
         src_off, src_meta = self.joint_src
         rc, rd = self.items["joint"]
@@ -1096,12 +1114,12 @@ class HipEngine:
         self.adam_step += 1
         self._norm_n = self.norm_n_whole
 
-    def _head_chain(self, h: int, idx_t, first: bool, xt_ready: bool) -> None:
+    def _head_chain(self, h: int, idx_t, first: bool, xt_ready: bool, xmode: str) -> None:
         """head h's kernel -> its wgrad -> its gather into its flat range of grad_flat"""
         M = self.mb
         self._head_kernel(h, idx_t, first, xt_ready, self.part_h[h], self.part_dw[h])
         b = self.buckets[h]
-        self._wgrad(b)
+        self._wgrad(b, xmode)
         lo, hi = self.head_range[h]
         part = self.part_h[h]
         rc, rd = self.items["policy" if h == 0 else "value"]
@@ -1126,14 +1144,14 @@ class HipEngine:
         Adam step run as ONE launch — the same update as grad() then apply()."""
         if self.heads:
             self._flush_value()
-            idx_t, first, xt_ready = self._minibatch(idx)
+            mbt = self._minibatch(idx)
             if apply:
                 assert self.can_fuse_apply(), "fused gather + Adam is not available here"
-                self._joint_step(idx_t, first, xt_ready)
+                self._joint_step(*mbt)
             else:
-                self._heads_grad(idx_t, first, xt_ready)
+                self._heads_grad(*mbt)
             return None
-        idx_t, first, xt_ready = self._minibatch(idx)
+        idx_t, first, xt_ready, xmode = self._minibatch(idx)
         if apply:
             assert self.can_fuse_apply(), "fused gather + Adam is not available here"
             self._launch_grad(idx_t, first, xt_ready, fused_apply=True)
@@ -1153,7 +1171,7 @@ class HipEngine:
                            self.ret, self.values_buf, self.mu_prev, self.v_prev, opts, fopts, self.tbufs,
                            self.ldT, self.part, False, xt_ready, self.no_u8, self.no_q, self.empty, 0)
         b = self.buckets[0]
-        self._wgrad(b)
+        self._wgrad(b, "fm")
         if fused_apply:
             if p.loss == "dppo_ref":   # train.py:164: the pre-update log_std, before Adam moves it
                 self.log_std_old.copy_(self.model.flat.data[:self.A])

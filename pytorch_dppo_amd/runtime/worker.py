@@ -68,7 +68,7 @@ class DPPOWorker:
         if ctx.collective and hasattr(self.engine, "ext"):
             # in-stream communicator (collective: every rank); --overlap-rollout also gets the
             # side-stream one its deferred value step uses
-            ctx.init_native_comm(self.engine.ext, side=bool(params.overlap_rollout))
+            ctx.init_native_comm(self.engine.ext, side=bool(params.overlap_rollout or params.overlap_value_epochs))
         self.iteration = 0
         self.env_steps = 0            # global (all ranks)
         self.updates = 0

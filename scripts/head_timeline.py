@@ -46,17 +46,17 @@ def main():
     ext = eng.ext
     nblk = eng.nhead_blk
     out = {}
-    idx_t, first, xt_ready = eng._minibatch(None)
+    mbt = eng._minibatch(None)
     for h in (0, 1):
         nw = int(ext.head_waves(h))
         buf = torch.zeros(((nblk + EVERY - 1) // EVERY) * nw * 16, dtype=torch.int64, device=dev)
         for _ in range(3):
-            eng._head_chain(h, idx_t, first, xt_ready)
+            eng._head_chain(h, *mbt)
         torch.cuda.synchronize()
         ext.set_train_tstamp(buf, EVERY)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
-        eng._head_chain(h, idx_t, first, xt_ready)
+        eng._head_chain(h, *mbt)
         ev[1].record()
         torch.cuda.synchronize()
         ext.set_train_tstamp(torch.empty(0, dtype=torch.int64, device=dev), 1)

@@ -245,6 +245,26 @@ def test_phead_update_matches_16x16_head_update(dtype, loss, mb, vh):
         assert (mp1 - mp0).abs().max().item() <= (2e-2 if bf else 2e-5) * (1 + mp0.abs().max().item())
 
 
+@pytest.mark.parametrize("env_name", ["Synthetic-64x8", "Ant-v2"])
+def test_phead_gate_on_observation_width(env_name):
+    """the 32x32 policy kernel's wgrad reads the observation operand as rows of
+    the operand width (d0 rounded up to the 128-row wgrad tile), so x_buf's rows serve only when d0
+    is a multiple of 128.  d0 = 96 (Synthetic-64x8) must fall back to the 16x16 policy head (it
+    used to raise at construction), d0 = 128 (Ant-v2) takes the 32x32 kernel; both full-batch
+    gradients match autograd at fp32 tolerance."""
+    N = 256 * 16
+    p = ppo_preset(device="gpu", env_name=env_name, num_envs=256, exploration_size=N, batch_size=N,
+                   dtype="bf16x3", ent_coeff=0.01, update_kernels="heads")
+    eng, model, _, _ = _engine(p)
+    assert eng.heads and eng.phead == (eng.d0 % 128 == 0), (eng.d0, eng.phead)
+    xq = _fill_buffer(eng, model)
+    eng.begin_update()
+    eng.grad(None)
+    torch.cuda.synchronize()
+    g_ref, _ = _torch_grad(model, p, xq, eng, torch.arange(eng.N, device=DEV))
+    assert (eng.grad_flat - g_ref).norm().item() / g_ref.norm().item() < 2e-4
+
+
 @pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
 def test_wgrad_row_major_operands_match_fragment_major(dtype):
     """The wgrad reading the 32x32 value head's row-major operands (per-lane row DMA into XOR-
@@ -785,7 +805,7 @@ def test_native_comm_failure_falls_back_to_process_group(monkeypatch):
         ctx.destroy()
 
 
-@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("overlap", [False, True, "every"])
 @pytest.mark.parametrize("native", [False, True])
 def test_head_chains_through_rccl_bit_identical_to_fused(overlap, native, monkeypatch):
     """The collective paths through the real RCCL call at world size 1.  Process-group RCCL
@@ -796,13 +816,18 @@ def test_head_chains_through_rccl_bit_identical_to_fused(overlap, native, monkey
     summation-order tolerance.  Native in-stream RCCL (csrc/comm.cpp): the joint kernels, the
     gather, the all-reduce and the whole-vector Adam == the joint world-size-1 path, bit for bit;
     with --overlap-rollout the last step's value all-reduce + Adam on the side stream (second
-    communicator) beside the next rollout, still bit for bit."""
+    communicator) beside the next rollout, still bit for bit; with overlap_value_epochs ("every")
+    every epoch's value all-reduce + Adam on the side stream, joined before the next value kernel
+    (the policy Adam and the next policy kernel run beside it), bit for bit."""
     from pytorch_dppo_amd.parallel.dist import DistContext, init_single_rank_collective
     from pytorch_dppo_amd.runtime.launcher import free_port
     from pytorch_dppo_amd.runtime.worker import DPPOWorker
+    if overlap == "every" and not native:
+        pytest.skip("the process-group chains overlap every value step already")
     gc = "native" if native else "process_group"
     kw = dict(device="gpu", env_name="Humanoid-v2", num_envs=64, exploration_size=64 * 8, batch_size=64 * 8,
-              num_epoch=3, dtype="bf16x3", seed=3, overlap_rollout=overlap, update_kernels="heads", grad_comm=gc)
+              num_epoch=3, dtype="bf16x3", seed=3, overlap_rollout=overlap is True,
+              overlap_value_epochs=overlap == "every", update_kernels="heads", grad_comm=gc)
     wj = DPPOWorker(dppo_preset(**kw), DistContext(device=DEV))     # joint world-1 path
     for _ in range(2):
         wj.iteration_step()
@@ -822,10 +847,12 @@ def test_head_chains_through_rccl_bit_identical_to_fused(overlap, native, monkey
     try:
         w2 = DPPOWorker(dppo_preset(**kw), ctx)
         assert (ctx.native is not None) == native
-        assert (ctx.native_side is not None) == (native and overlap)
+        assert (ctx.native_side is not None) == (native and bool(overlap))
         for _ in range(2):
             m = w2.iteration_step()
-        if overlap:
+        if overlap == "every":
+            assert w2.engine.side_steps == 6    # every step of the 2 iterations x 3 epochs
+        elif overlap:
             # the last value step waits for the rollout: on the side stream (native) or as the
             # process group's pending work
             assert w2.engine._pending_value is not None
@@ -945,14 +972,17 @@ def test_packed_metrics_match_torch(max_norm):
     assert torch.equal(eng.metrics_buf[:2], eng.ep_sum)
 
 
-@pytest.mark.parametrize("extra", [[], ["--overlap-rollout", "off"], ["--grad-comm", "process_group"]])
+@pytest.mark.parametrize("extra", [[], ["--overlap-rollout", "off"], ["--grad-comm", "process_group"],
+                                   ["--overlap-value", "on"]])
 def test_two_ranks_on_one_gpu_stay_in_sync(extra):
     """bench.py as 2 ranks sharing the box's GPU (RCCL refuses two ranks on one device, so
     --dist-backend gloo): by default the gloo adapter runs the PRODUCTION multi-rank branch (the
     in-stream one an N-GPU RCCL run takes: joint kernels → gather → all-reduce → whole-vector
     Adam, and — the world > 1 default, --overlap-rollout auto — the last epoch's value step on
-    the side stream beside the next rollout); the ranks must end with bit-identical parameters
-    (--verify-sync)."""
+    the side stream beside the next rollout; --overlap-value: every epoch's); the ranks must end
+    with bit-identical parameters (--verify-sync).  2,048 envs x 16 steps = 32,768 rows per rank:
+    the per-head path the bench geometry takes (>= 128 rows x the CUs), so the side-stream counts
+    the JSON reports (from the engine, not the flags) are the head path's."""
     import os
     import subprocess
     import sys
@@ -960,7 +990,7 @@ def test_two_ranks_on_one_gpu_stay_in_sync(extra):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--num-envs", "512", "--verify-sync", "--variants", "bf16,fp8",
+           "--steps", "2", "--warmup", "1", "--num-envs", "2048", "--verify-sync", "--variants", "bf16,fp8",
            "--dist-backend", "gloo"] + extra
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -971,12 +1001,19 @@ def test_two_ranks_on_one_gpu_stay_in_sync(extra):
     pg = "process_group" in extra
     assert d["config"]["grad_allreduce"] == ("process_group" if pg else "gloo_in_stream")
     assert ("grad_allreduce process_group" if pg else "grad_allreduce in_stream") in r.stderr
+    assert d["config"]["per_head_kernels"] is True
     off = "off" in extra
     assert d["config"]["overlap_rollout"] is (not off)
+    # value steps per iteration the engine overlapped: the last epoch's (overlap-rollout), every
+    # epoch's (overlap-value, 10), the per-head process-group chains' pending ones (10), none
+    n = d["config"]["overlapped_value_steps_per_iter"]
     if off:
-        assert d["config"]["overlap_value_step"] == "none"
-    elif not pg:
+        assert d["config"]["overlap_value_step"] == "none" and n == 0
+    elif pg:
+        assert d["config"]["overlap_value_step"] == "pending_work" and n == 10
+    else:
         assert d["config"]["overlap_value_step"] == "side_stream"
+        assert n == (10 if "--overlap-value" in extra else 1), n
 
 
 def _two_rank_child(rank, world, port, out_dir):
@@ -1000,9 +1037,10 @@ def _two_rank_child(rank, world, port, out_dir):
                   batch_size=256 * 8, num_epoch=3, seed=3, num_processes=world, dist_backend="gloo",
                   verify_sync_every=1, update_kernels="heads")
     for dtype in ("bf16x3", "bf16", "fp8"):
-        for gc, ov in (("auto", False), ("auto", True), ("process_group", False)):
+        for gc, ov in (("auto", False), ("auto", True), ("auto", "every"), ("process_group", False)):
             ctx = ctx_for(gc)
-            w = DPPOWorker(dppo_preset(**common, dtype=dtype, overlap_rollout=ov, grad_comm=gc), ctx)
+            w = DPPOWorker(dppo_preset(**common, dtype=dtype, overlap_rollout=ov is True,
+                                       overlap_value_epochs=ov == "every", grad_comm=gc), ctx)
             for _ in range(2):
                 m = w.iteration_step()
             w.flush_pending()
@@ -1058,12 +1096,13 @@ def test_two_rank_engine_paths_bit_identical_and_mean_scaled_once(tmp_path):
     r1 = torch.load(tmp_path / "two1.pt", weights_only=True)
     for dtype in ("bf16x3", "bf16", "fp8"):
         ref = r0[f"{dtype}/process_group/False"][0]
-        for key in (f"{dtype}/auto/False", f"{dtype}/auto/True", f"{dtype}/process_group/False"):
+        for key in (f"{dtype}/auto/False", f"{dtype}/auto/True", f"{dtype}/auto/every",
+                    f"{dtype}/process_group/False"):
             (f0, s0, n0, side0), (f1, s1, _, _) = r0[key], r1[key]
             assert s0 and s1, key
             assert torch.equal(f0, f1), key                      # replicas bit-identical
             assert n0 == ("auto" in key), key                    # the adapter ran the in-stream branch
-            assert side0 == key.endswith("auto/True"), key
+            assert side0 == (key.endswith("auto/True") or key.endswith("auto/every")), key
             assert torch.equal(f0, ref), (key, (f0 - ref).abs().max().item())
     for dtype in ("fp32", "bf16x3"):
         for gc in ("auto", "process_group"):
