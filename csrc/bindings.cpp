@@ -406,7 +406,8 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
               "xT_ready needs a full-batch call");
   a.xT_ready = xT_ready ? 1 : 0;
   if (g_tstamp != nullptr) {
-    const int64_t nw = head >= 0 ? mlp_head_waves(head) : mlp_train_waves((int)dt, a);
+    // (the 32x32 value head: 4 waves, csrc/vhead.hip; the policy: 4 too, but it takes no stamps)
+    const int64_t nw = (t32 && head == 1) ? 4 : (head >= 0 ? mlp_head_waves(head) : mlp_train_waves((int)dt, a));
     TORCH_CHECK(g_tstamp_numel >= ((nblk + g_tstamp_every - 1) / g_tstamp_every) * nw * 16, "tstamp buffer too small");
     a.tstamp = g_tstamp;
     a.tstamp_every = g_tstamp_every;
@@ -537,15 +538,17 @@ WgradArgs wgrad_args(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torc
     a.xT[i] = xT[i].data_ptr();
   }
   a.ld = (int)ld;
-  // rm: 12 flags (dY side of layers 0-5, then X side): row-major operands of row length g_rows /
-  // x_rows (csrc/vhead.hip); split-bf16 / bf16 only, 64-feature quadrants inside the row
+  // rm: 12 flags (dY side of layers 0-5, then X side): 1 = row-major operands of row length g_rows /
+  // x_rows (csrc/phead.hip, x_buf), 2 = the k16-blocked row-major layout [len / 16][ld][16]
+  // (csrc/vhead.hip); split-bf16 / bf16 only, 64-feature quadrants inside the row
   TORCH_CHECK(rm.empty() || rm.size() == 12, "rm: 12 row-major flags");
   for (size_t i = 0; i < rm.size(); ++i) {
     if (!rm[i]) continue;
     TORCH_CHECK(dt == 1 || dt == 3, "row-major wgrad operands: split-bf16 / bf16 only");
+    TORCH_CHECK(rm[i] == 1 || rm[i] == 2, "rm flag: 0 fragment-major, 1 row-major, 2 k16-blocked row-major");
     const int64_t len = i < 6 ? g_rows[i] : x_rows[i - 6];
     TORCH_CHECK(len % 64 == 0 && ld * len * (dt == 3 ? 4 : 2) < (int64_t(1) << 40), "row-major operand rows");
-    (i < 6 ? a.g_rm[i] : a.x_rm[i - 6]) = (int)len;
+    (i < 6 ? a.g_rm[i] : a.x_rm[i - 6]) = rm[i] == 2 ? -(int)len : (int)len;
   }
   a.tasks = reinterpret_cast<const WgradTask*>(tasks.data_ptr<int>());
   a.ntasks = ntasks;
@@ -704,6 +707,16 @@ void metrics_pack(torch::Tensor ep, torch::Tensor loss8, torch::Tensor norm_part
   check(out, "out", at::kDouble, 11);
   launch_metrics_pack(ep.data_ptr<double>(), loss8.data_ptr<float>(), norm_part.data_ptr<float>(),
                       (int)norm_part.numel(), out.data_ptr<double>(), cur_stream());
+  after_launch(__func__);
+}
+
+// diagnostics (scripts/probe_side_kernel.py): an RCCL-footprint stand-in on the current stream
+void probe_spin(int64_t nblk, int64_t nthreads, int64_t lds, double us, torch::Tensor sink) {
+  TORCH_CHECK(nblk >= 1 && nblk <= 4096 && nthreads >= 64 && nthreads <= 1024 && nthreads % 64 == 0 && lds >= 0 &&
+                  lds <= 65536 && lds >= 4 * nthreads && us > 0 && us < 1e5,
+              "probe_spin: 1-4096 blocks of 64-1024 threads, 4 * threads <= lds <= 64 KiB, 0 < us < 1e5");
+  check(sink, "sink", at::kInt, nblk);
+  launch_probe_spin((int)nblk, (int)nthreads, (int)lds, us, sink.data_ptr<int>(), cur_stream());
   after_launch(__func__);
 }
 
@@ -882,5 +895,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_refresh", &fp8_refresh);
   m.def("set_x_stream", &set_x_stream);
   m.def("metrics_pack", &metrics_pack);
+  m.def("probe_spin", &probe_spin);
   m.attr("arch") = "gfx950";
 }

@@ -210,8 +210,9 @@ struct WgradArgs {
   const unsigned* q8_rd;
   int q8_t[6];
   float q8_xs[6];
-  // row-major operands (csrc/vhead.hip: [ld rows][features]): the row length in elements of layer
-  // l's dY (g_rm) / X (x_rm) operand, 0 = fragment-major
+  // row-major operands: the row length in elements of layer l's dY (g_rm) / X (x_rm) operand —
+  // > 0 plain rows ([ld rows][features]: csrc/phead.hip, x_buf), < 0 the k16-blocked layout
+  // [features / 16][ld][16] (csrc/vhead.hip), 0 = fragment-major
   int g_rm[6], x_rm[6];
 };
 
@@ -271,6 +272,8 @@ void launch_obs_merge(const double* s12, int O, double count, double n_a, const 
 // per-block sums of squares the last Adam launch left in norm_part]
 void launch_metrics_pack(const double* ep, const float* loss8, const float* norm_part, int nblk, double* out,
                          hipStream_t s);
+// diagnostics: nblk workgroups of nthreads (lds bytes each) spinning `us` microseconds each
+void launch_probe_spin(int nblk, int nthreads, int lds, double us, int* sink, hipStream_t s);
 }
 
 // operand buffers (feature-major) are padded to multiples of 128 rows

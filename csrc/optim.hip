@@ -503,6 +503,32 @@ extern "C" void launch_debug_invalid(double* out, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+// DIAGNOSTIC (scripts/probe_side_kernel.py): a stand-in for an RCCL all-reduce kernel's CU
+// footprint — nblk workgroups of nthreads with lds bytes of LDS, each spinning until the 100 MHz
+// real-time counter has advanced `ticks` since ITS OWN start (so a workgroup that waits for a CU
+// still runs its full time once admitted) — to see whether a collective launched on a side stream
+// gets CUs while the update kernels hold them (docs/ARCHITECTURE.md §13).  Every wave exits after
+// its bounded spin.
+__global__ void probe_spin_kernel(unsigned long long ticks, int* __restrict__ sink) {
+  extern __shared__ int probe_lds[];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t = t0;
+  int n = 0;
+  while (t - t0 < ticks && n < (1 << 24)) {
+    __builtin_amdgcn_s_sleep(2);
+    t = __builtin_amdgcn_s_memrealtime();
+    ++n;
+  }
+  probe_lds[threadIdx.x] = n;
+  if (threadIdx.x == 0 && n < 0) sink[blockIdx.x] = probe_lds[0];   // (never: keeps the loop)
+}
+
+extern "C" void launch_probe_spin(int nblk, int nthreads, int lds, double us, int* sink, hipStream_t s) {
+  const unsigned long long ticks = (unsigned long long)(us * 100.0);   // s_memrealtime: 100 MHz
+  hipLaunchKernelGGL(probe_spin_kernel, dim3(nblk), dim3(nthreads), (size_t)lds, s, ticks, sink);
+  HIP_CHECK_LAUNCH();
+}
+
 extern "C" void launch_metrics_pack(const double* ep, const float* loss8, const float* norm_part, int nblk,
                                     double* out, hipStream_t s) {
   hipLaunchKernelGGL(metrics_pack_kernel, dim3(1), dim3(256), 0, s, ep, loss8, norm_part, nblk, out);

@@ -235,11 +235,12 @@ class HipEngine:
             bias_rows.append((self.h1vT, lv1.fan_out))
         if not self.phead:
             bias_rows.append((self.h1pT, lp1.fan_out))
-        # wgrad operand layout flags (dY side of the 6 layers, then X side): row-major for v_fc1's dY
-        # (g1v) and v_fc2's dY (g2v) / X (h1v) under the 32x32 value head
+        # wgrad operand layout flags (dY side of the 6 layers, then X side; 1 row-major, 2 the
+        # k16-blocked row-major layout [features / 16][ldT][16]): k16-blocked for v_fc1's dY (g1v)
+        # and v_fc2's dY (g2v) / X (h1v) under the 32x32 value head (csrc/vhead.hip)
         self.rm = [0] * 12
         if self.vhead:
-            self.rm[3] = self.rm[4] = self.rm[6 + 4] = 1
+            self.rm[3] = self.rm[4] = self.rm[6 + 4] = 2
         # ... and under the 32x32 policy head p_fc1's / p_fc2's dY (g1p, g2p), p_fc2's X (h1p) and
         # the observation operand of both fc1 layers
         self.wg_x_full = self.wg_x

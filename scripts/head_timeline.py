@@ -23,14 +23,16 @@ from pytorch_dppo_amd.utils.obs_stats import RunningObsStats  # noqa: E402
 # stamp i -> i+1 phases (HD_STAMP 0..7), plus fc1 sub-spans from stamps 8 / 9
 PHASES = ["fc1", "fc2", "fc3 wait", "fc3 + loss", "dgrad fc3", "dgrad fc2", "partials"]
 # the 32x32 transposed-chain value head (csrc/vhead.hip VH_STAMP)
-VPHASES = ["fc1", "fc2", "pair sum", "fc3 + loss + g2", "dgrad passes 1-2", "dgrad passes 3-4", "partials"]
+VPHASES = ["fc1", "fc2", "fc3 + loss + g2", "dgrad passes 0-1", "dgrad pass 2", "dgrad pass 3", "partials"]
 EVERY = 8
 
 
 def main():
     dev = torch.device("cuda", 0)
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536, batch_size=65536,
-                    dtype=sys.argv[1] if len(sys.argv) > 1 else "bf16x3", update_kernels="heads")
+                    dtype=args[0] if args else "bf16x3", update_kernels="heads")
+    p.vhead_kernel = "--vhead" in sys.argv     # the 32x32 value head (csrc/vhead.hip)
     spec = get_spec(p.env_name)
     torch.manual_seed(0)
     model = ActorCritic(spec.obs_dim, spec.act_dim).to(dev)
@@ -48,7 +50,8 @@ def main():
     out = {}
     mbt = eng._minibatch(None)
     for h in (0, 1):
-        nw = int(ext.head_waves(h))
+        # (the 32x32 value head: 4 waves, one per SIMD, csrc/vhead.hip)
+        nw = 4 if (h == 1 and bool(getattr(eng, "vhead", False))) else int(ext.head_waves(h))
         buf = torch.zeros(((nblk + EVERY - 1) // EVERY) * nw * 16, dtype=torch.int64, device=dev)
         for _ in range(3):
             eng._head_chain(h, *mbt)

@@ -267,9 +267,10 @@ def test_phead_gate_on_observation_width(env_name):
 
 @pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
 def test_wgrad_row_major_operands_match_fragment_major(dtype):
-    """The wgrad reading the 32x32 value head's row-major operands (per-lane row DMA into XOR-
-    swizzled 128-byte-row images, ds_read_b64_tr_b16) gives the same MFMA operands in the same k
-    order as the fragment-major copy of the same values: bit-identical split-K slabs"""
+    """The wgrad reading the 32x32 value head's k16-blocked row-major operands ([features / 16][ldT]
+    [16], per-lane DMA into XOR-swizzled 128-byte-row images, ds_read_b64_tr_b16) gives the same MFMA
+    operands in the same k order as the plain row-major copy ([ldT][features], rm flag 1: the policy
+    head's layout) — bit-identical slabs — and as the fragment-major copy of the same values"""
     from pytorch_dppo_amd.models.actor_critic import fm_index
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=256, exploration_size=256 * 16,
                     batch_size=256 * 16, dtype=dtype, update_kernels="heads")
@@ -285,12 +286,15 @@ def test_wgrad_row_major_operands_match_fragment_major(dtype):
     eng.ext.wgrad(eng._wgrad_dt(), eng.wg_g, eng.wg_x, eng.g_rows, eng.x_rows, eng.ldT, b["tasks"],
                   b["tasks_host"], b["slab"], *eng._q8_args(), eng.rm)
     slab_rm = b["slab"].clone()
-    # the fragment-major copies of the row-major operands
-    fm = {}
+    assert [eng.rm[3], eng.rm[4], eng.rm[10]] == [2, 2, 2]
+    # the plain row-major and fragment-major copies of the k16-blocked operands
+    fm, rmc = {}, {}
     for name, li, side in (("g1vT", 3, "g"), ("g2vT", 4, "g"), ("h1vT", 4, "x")):
         buf = getattr(eng, name)
         width = (eng.g_rows if side == "g" else eng.x_rows)[li]
-        rows = eng.decode(buf).view(eng.ldT, width)                  # [ldT][features]
+        # (k16-blocked [width / 16][ldT][16] -> [ldT][features]: a pure permutation of the slots)
+        rmc[name] = buf.view(-1).view(width // 16, eng.ldT, -1).permute(1, 0, 2).contiguous().view_as(buf)
+        rows = eng.decode(rmc[name]).view(eng.ldT, width)             # [ldT][features]
         f = torch.arange(width, device=DEV).repeat_interleave(eng.ldT)
         c = torch.arange(eng.ldT, device=DEV).repeat(width)
         flat = torch.zeros(width * eng.ldT, device=DEV)
@@ -298,6 +302,12 @@ def test_wgrad_row_major_operands_match_fragment_major(dtype):
         fm[name] = eng.encode(flat).view_as(buf)
     wg_g = list(eng.wg_g)
     wg_x = list(eng.wg_x)
+    wg_g[3], wg_g[4], wg_x[4] = rmc["g1vT"], rmc["g2vT"], rmc["h1vT"]
+    b["slab"].zero_()
+    rm1 = [1 if f else 0 for f in eng.rm]
+    eng.ext.wgrad(eng._wgrad_dt(), wg_g, wg_x, eng.g_rows, eng.x_rows, eng.ldT, b["tasks"],
+                  b["tasks_host"], b["slab"], *eng._q8_args(), rm1)
+    assert torch.equal(slab_rm, b["slab"])   # same bytes, same operands, same order
     wg_g[3], wg_g[4], wg_x[4] = fm["g1vT"], fm["g2vT"], fm["h1vT"]
     b["slab"].zero_()
     eng.ext.wgrad(eng._wgrad_dt(), wg_g, wg_x, eng.g_rows, eng.x_rows, eng.ldT, b["tasks"],
@@ -895,8 +905,10 @@ def test_head_kernels_match_one_kernel_update(env_name, mb, dtype, loss, monkeyp
         eng.grad(idx)
         n1p, n1v = model.layer("p_fc1").fan_out, model.layer("v_fc1").fan_out
 
-        def rowmajor(buf, nfeat, rm=False):   # FM [features][ldT] -> [features][mb] (rm: [ldT][width] rows)
-            if rm:   # (the 32x32 value head's row-major operands, csrc/vhead.hip)
+        def rowmajor(buf, nfeat, rm=False, kb=False):   # FM [features][ldT] -> [features][mb]
+            if kb:   # the 32x32 value head's k16-blocked rows [width / 16][ldT][16] (csrc/vhead.hip)
+                return eng.decode(buf).view(-1, eng.ldT, 16).permute(1, 0, 2).reshape(eng.ldT, -1)[:mb, :nfeat].t()
+            if rm:   # [ldT][width] rows (the 32x32 policy head's X rows)
                 return eng.decode(buf).view(eng.ldT, -1)[:mb, :nfeat].t()
             r = torch.arange(nfeat, device=DEV).repeat_interleave(mb)
             c = torch.arange(mb, device=DEV).repeat(nfeat)
@@ -907,10 +919,11 @@ def test_head_kernels_match_one_kernel_update(env_name, mb, dtype, loss, monkeyp
         ph = bool(getattr(eng, "phead", False))
         if heads == "1":
             use_h1v = ph
-        h1 = (rowmajor(eng.h1vT, model.layer("v_fc2").fan_in, bool(getattr(eng, "vhead", False))) if use_h1v
+        vh = bool(getattr(eng, "vhead", False))
+        h1 = (rowmajor(eng.h1vT, model.layer("v_fc2").fan_in, kb=vh) if use_h1v
               else rowmajor(eng.h1pT, n1p))
         res[heads] = (eng.grad_flat.clone(), eng.last_losses(), h1,
-                      rowmajor(eng.g1vT, n1v, bool(getattr(eng, "vhead", False))),
+                      rowmajor(eng.g1vT, n1v, kb=vh),
                       rowmajor(eng.xT, model.num_inputs, ph), eng.mu_prev.clone(), eng.v_prev.clone())
         if heads == "1" and loss == "ppo":
             g_ref, _ = _torch_grad(model, p, xq, eng, idx.to(DEV))
