@@ -134,9 +134,9 @@ def main():
     ap.add_argument("--dist-timeout-s", type=float, default=300.0,
                     help="bound of every wait on peers (collective watchdog; abort + non-zero exit)")
     ap.add_argument("--heartbeat-timeout-s", type=float, default=60.0)
-    ap.add_argument("--t32", default="auto", choices=["auto", "off", "value", "policy", "both"],
-                    help="update head kernels: the 32x32 transposed-chain kernels (csrc/vhead.hip, csrc/phead.hip) "
-                         "for none / the value head / both heads; auto = the Params defaults")
+    ap.add_argument("--t32", default="auto", choices=["auto", "off", "policy"],
+                    help="policy update head kernel: the 32x32 transposed-chain kernel (csrc/phead.hip) or the "
+                         "16x16 head kernel (off); auto = the Params default")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -174,8 +174,7 @@ def main():
                         dist_timeout_s=args.dist_timeout_s,
                         phase_timing=args.phase_timing if not args.verbose else max(args.phase_timing, 1))
         if args.t32 != "auto":
-            p.vhead_kernel = args.t32 in ("value", "both")
-            p.phead_kernel = args.t32 in ("policy", "both")
+            p.phead_kernel = args.t32 == "policy"
         w = DPPOWorker(p, ctx)
         m = {}
         for i in range(args.warmup):
@@ -221,8 +220,7 @@ def main():
     if ctx.collective:
         grad_ar = ("process_group" if ctx.native is None else
                    "rccl_in_stream" if ctx.backend == "nccl" else "gloo_in_stream")
-    t32_heads = [k for k, on in (("value", getattr(w.engine, "vhead", False)),
-                                 ("policy", getattr(w.engine, "phead", False))) if on]
+    t32_heads = ["policy"] if getattr(w.engine, "phead", False) else []
     # what the engine DID with the value-head steps (not what the flags asked for): run on the side
     # stream (a second communicator), left pending on a process-group all-reduce, or in stream order
     n_iter = args.warmup + args.steps

@@ -335,13 +335,12 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   // its fused narrow-layer weight gradient at partial column part_dw (policy [32][128], value [128])
   const int head = opts.size() >= 7 ? (int)opts[5] : -1;
   const int part_dw = opts.size() >= 7 ? (int)opts[6] : 0;
-  // t32: the head's transposed-chain 32x32 kernel — value (csrc/vhead.hip): h1v / g1v / g2v
-  // ROW-MAJOR ([ldT][512] / [ldT][512] / [ldT][128]); policy (csrc/phead.hip): h1p / g1p / g2p
-  // ([ldT][128]) and, unless xT_ready, the observation rows into xT ([ldT][d0]).  The engine's
-  // wgrad must read them so (its rm flags)
-  // (policy: opts[7] == 1 also sums p_fc2's weight gradient in the kernel, 2 stores h1p / g2p)
+  // t32: the policy head's transposed-chain 32x32 kernel (csrc/phead.hip): h1p / g1p / g2p and,
+  // unless xT_ready, the observation rows into xT, ROW-MAJOR (the engine's wgrad reads them so: its
+  // rm flags).  opts[7] == 1 also sums p_fc2's weight gradient in the kernel (no h1p / g2p), 2
+  // stores h1p / g2p.  (The value head's update stays on the 16x16 kernel: docs/ARCHITECTURE.md §13.)
   const bool t32 = opts.size() == 8 && opts[7] != 0;
-  const bool p2 = t32 && head == 0 && opts[7] == 1;
+  const bool p2 = t32 && opts[7] == 1;
   TORCH_CHECK(head >= -1 && head <= 1, "head: -1 (both heads, one kernel), 0 policy, 1 value");
   TORCH_CHECK(fopts.size() == 2, "fopts: clip, ent_coeff");
   TORCH_CHECK(tbufs.size() == 11, "11 transposed buffers");
@@ -406,8 +405,8 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
               "xT_ready needs a full-batch call");
   a.xT_ready = xT_ready ? 1 : 0;
   if (g_tstamp != nullptr) {
-    // (the 32x32 value head: 4 waves, csrc/vhead.hip; the policy: 4 too, but it takes no stamps)
-    const int64_t nw = (t32 && head == 1) ? 4 : (head >= 0 ? mlp_head_waves(head) : mlp_train_waves((int)dt, a));
+    // (the 32x32 policy head takes no stamps)
+    const int64_t nw = head >= 0 ? mlp_head_waves(head) : mlp_train_waves((int)dt, a);
     TORCH_CHECK(g_tstamp_numel >= ((nblk + g_tstamp_every - 1) / g_tstamp_every) * nw * 16, "tstamp buffer too small");
     a.tstamp = g_tstamp;
     a.tstamp_every = g_tstamp_every;
@@ -416,18 +415,12 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
   TORCH_CHECK(!(w8.defined() && w8.numel() > 0) || (dt == 1 && head >= 0), "w8: the fp8 mode's per-head bf16 update only");
   set_w8(a, w8, qscale, L);
   if (t32) {   // the row-major operand rows the kernels write are whole padded widths
-    const int64_t pn = head == 0 && !p2 ? 128 : 0;   // h1p / g2p
-    const int64_t wid[11] = {head == 0 && !xT_ready ? L.d_in[0] : 0, pn, 0, head == 1 ? 512 : 0, 0,
-                             head == 0 ? 128 : 0, pn, 0, head == 1 ? 512 : 0, head == 1 ? 128 : 0, 0};
+    const int64_t pn = !p2 ? 128 : 0;   // h1p / g2p
+    const int64_t wid[11] = {!xT_ready ? L.d_in[0] : 0, pn, 0, 0, 0, 128, pn, 0, 0, 0, 0};
     for (int i = 0; i < 11; ++i)
       TORCH_CHECK(tbufs[i].numel() >= wid[i] * ldT, "t32 head: row-major operand buffer ", i, " too small");
   }
-  if (t32 && head == 1) {
-    TORCH_CHECK(!q8 && a.W8 == nullptr && vhead_shape_ok(a), "vhead: the value head at bf16x3 / bf16");
-    TORCH_CHECK(ldT * 512 * (dt == 3 ? 4 : 2) < (int64_t(1) << 31), "vhead: row-major operands beyond 2 GiB");
-    TORCH_CHECK(ldT % vhead_rows() == 0 && Mpad <= ldT, "vhead: ldT covers whole workgroups");
-    launch_vhead_train((int)dt, a, cur_stream());
-  } else if (t32) {
+  if (t32) {
     TORCH_CHECK(head == 0 && !q8 && a.W8 == nullptr && phead_shape_ok(a), "phead: the policy head at bf16x3 / bf16");
     TORCH_CHECK(part_dw + 32 * 128 + (p2 ? 128 * 128 : 0) <= npart,
                 "phead: the dW_mu (and dW_p2) blocks must fit the partial row");
@@ -443,14 +436,6 @@ void mlp_train(int64_t dt, torch::Tensor x_buf, torch::Tensor idx, int64_t row0,
     launch_mlp_train((int)dt, a, cur_stream());
   }
   after_launch(__func__);
-}
-
-// the transposed-chain value head covers this (dtype, network)
-bool vhead_train_applies(int64_t dt, std::vector<int64_t> layout) {
-  const Layout L = parse_layout(layout);
-  MlpArgs a{};
-  for (int i = 0; i < 6; ++i) { a.d_in[i] = L.d_in[i]; a.d_out[i] = L.d_out[i]; a.n_out[i] = L.n_out[i]; }
-  return (dt == 3 || dt == 1) && vhead_shape_ok(a) != 0;
 }
 
 // the transposed-chain policy head covers this (dtype, network, action width)
@@ -539,16 +524,15 @@ WgradArgs wgrad_args(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torc
   }
   a.ld = (int)ld;
   // rm: 12 flags (dY side of layers 0-5, then X side): 1 = row-major operands of row length g_rows /
-  // x_rows (csrc/phead.hip, x_buf), 2 = the k16-blocked row-major layout [len / 16][ld][16]
-  // (csrc/vhead.hip); split-bf16 / bf16 only, 64-feature quadrants inside the row
+  // x_rows (csrc/phead.hip, x_buf); split-bf16 / bf16 only, 64-feature quadrants inside the row
   TORCH_CHECK(rm.empty() || rm.size() == 12, "rm: 12 row-major flags");
   for (size_t i = 0; i < rm.size(); ++i) {
     if (!rm[i]) continue;
     TORCH_CHECK(dt == 1 || dt == 3, "row-major wgrad operands: split-bf16 / bf16 only");
-    TORCH_CHECK(rm[i] == 1 || rm[i] == 2, "rm flag: 0 fragment-major, 1 row-major, 2 k16-blocked row-major");
+    TORCH_CHECK(rm[i] == 1, "rm flag: 0 fragment-major, 1 row-major");
     const int64_t len = i < 6 ? g_rows[i] : x_rows[i - 6];
     TORCH_CHECK(len % 64 == 0 && ld * len * (dt == 3 ? 4 : 2) < (int64_t(1) << 40), "row-major operand rows");
-    (i < 6 ? a.g_rm[i] : a.x_rm[i - 6]) = rm[i] == 2 ? -(int)len : (int)len;
+    (i < 6 ? a.g_rm[i] : a.x_rm[i - 6]) = (int)len;
   }
   a.tasks = reinterpret_cast<const WgradTask*>(tasks.data_ptr<int>());
   a.ntasks = ntasks;
@@ -853,7 +837,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_value", &mlp_value);
   m.def("mlp_train", &mlp_train);
   m.def("head_applies", &head_applies);
-  m.def("vhead_train_applies", &vhead_train_applies);
   m.def("phead_train_applies", &phead_train_applies);
   m.def("set_phead", [](int64_t on) { set_phead((int)on); });
   m.def("head_rows", []() { return (int64_t)mlp_head_rows(); });

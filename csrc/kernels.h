@@ -147,7 +147,6 @@ extern "C" int head_kernels_enabled();
 // value head on 32x32x16 MFMAs, transposed chain (csrc/vhead.hip): 128 rows per workgroup
 extern "C" int vhead_applies(const MlpArgs& a);   // the forward (set_vhead flag and shapes)
 extern "C" int vhead_shape_ok(const MlpArgs& a);
-extern "C" void launch_vhead_train(int dt, const MlpArgs& a, hipStream_t s);   // the update chain
 extern "C" int vhead_rows();
 extern "C" void launch_vhead_fwd(int dt, const MlpArgs& a, hipStream_t s);   // V(x): dt bf16x3 or bf16
 extern "C" void set_vhead(int enable);
@@ -210,9 +209,8 @@ struct WgradArgs {
   const unsigned* q8_rd;
   int q8_t[6];
   float q8_xs[6];
-  // row-major operands: the row length in elements of layer l's dY (g_rm) / X (x_rm) operand —
-  // > 0 plain rows ([ld rows][features]: csrc/phead.hip, x_buf), < 0 the k16-blocked layout
-  // [features / 16][ld][16] (csrc/vhead.hip), 0 = fragment-major
+  // row-major operands: the row length in elements of layer l's dY (g_rm) / X (x_rm) operand
+  // ([ld rows][features]: csrc/phead.hip, x_buf), 0 = fragment-major
   int g_rm[6], x_rm[6];
 };
 

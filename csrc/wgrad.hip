@@ -120,9 +120,7 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
     const bool gs = ff < NF;
     const int fl = gs ? ff : ff - NF;
     const int feat0 = (gs ? tk.n0 : tk.k0) + 16 * fl;
-    // rm: 0 fragment-major; > 0 row-major rows of rm elements; < 0 the k16-blocked row-major
-    // layout [-rm / 16][ld][16] (csrc/vhead.hip: a wave's 32 rows x 16 features are one contiguous
-    // 1-2 KiB piece, so its operand stores write whole cache lines)
+    // rm: 0 fragment-major; > 0 row-major rows of rm elements
     const int rm = (DT == DT_S3 || DT == DT_BF16) ? (gs ? a.g_rm[tk.layer] : a.x_rm[tk.layer]) : 0;
     const char* ob = gs ? g : x;
     if (rm == 0) {
@@ -137,21 +135,17 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
 #pragma unroll
       for (int hh = 0; hh < NI; ++hh) {
         const int n = NI * sq + hh;                   // 1 KiB DMA instruction of the quadrant image
-        // (the LDS image is the same for both layouts: only the lane's source address differs;
-        // k16-blocked: 16-byte chunk c of a row is in feature block f0 / 16 + c / (split 4 | bf16 2))
         if constexpr (IsSplit<DT>::value) {           // rows 4 n .. 4 n + 3, 256 bytes each
           const int row = 4 * n + (lane >> 4);
           const int c = (lane & 15) ^ wgrad_swz16(row);
-          srcp[q][hh] = rm > 0 ? ob + ((size_t)(tk.m0 + row) * rm + f0) * sizeof(T) + 16 * c
-                               : ob + (((size_t)(f0 / 16 + (c >> 2)) * a.ld + tk.m0 + row) * 16) * sizeof(T) + 16 * (c & 3);
+          srcp[q][hh] = ob + ((size_t)(tk.m0 + row) * rm + f0) * sizeof(T) + 16 * c;
         } else {                                      // rows 8 n .. 8 n + 7, 128 bytes each
           const int row = 8 * n + (lane >> 3);
           const int c = (lane & 7) ^ wgrad_swz(row);
-          srcp[q][hh] = rm > 0 ? ob + ((size_t)(tk.m0 + row) * rm + f0 + 8 * c) * sizeof(T)
-                               : ob + (((size_t)(f0 / 16 + (c >> 1)) * a.ld + tk.m0 + row) * 16) * sizeof(T) + 16 * (c & 1);
+          srcp[q][hh] = ob + ((size_t)(tk.m0 + row) * rm + f0 + 8 * c) * sizeof(T);
         }
       }
-      kstride[q] = rm > 0 ? (size_t)32 * rm * sizeof(T) : (size_t)32 * 16 * sizeof(T);
+      kstride[q] = (size_t)32 * rm * sizeof(T);
     }
     dst[q] = f * FB;
   }

@@ -107,8 +107,6 @@ class Params:
     stats_stream: str = "off"            # off | on | auto (on when an all-reduce sits in the chain): the
                                          # obs-stat reduce / all-reduce / merge on a side stream
     wgrad_wgs: int = 0                   # wgrad tasks per launch (0: one per CU of the device)
-    vhead_kernel: bool = False           # the value head's update on the 32x32 kernel (csrc/vhead.hip): opt-in,
-                                         # slower (profiles/r5); V(x) takes it either way (set_vhead)
     phead_kernel: bool = True            # the policy head on the 32x32 kernel (csrc/phead.hip)
     mlp_rows: int = 0                    # diagnostics: force the tile update kernel's row tile (0: auto)
 

@@ -159,11 +159,8 @@ class HipEngine:
         # for the gradients (csrc/common.h Q8) — and the wgrad runs on the e4m3 MFMA: half the
         # operand bytes of the bf16 update's HBM round trip.  fp8_wgrad_operands=False: bf16 operands.
         self.q8 = self.fp8 and self.heads and bool(params.fp8_wgrad_operands)
-        # the value head on the transposed-chain 32x32 kernel (csrc/vhead.hip) at bf16x3 / bf16: it
-        # writes its wgrad operands h1v / g1v / g2v ROW-MAJOR ([ldT][features]), which the wgrad reads
-        # with transposing LDS reads (self.rm); the fp8 mode's e4m3 operands / fc1 keep the 16x16 head
-        self.vhead = (self.heads and not self.fp8 and bool(params.vhead_kernel)
-                      and bool(self.ext.vhead_train_applies(self.dt, self.layout)))
+        # (the value head's update stays on the 16x16 head kernel: its 32x32 one-wave-per-SIMD form
+        # measured slower at every step, docs/ARCHITECTURE.md §13; csrc/vhead.hip is V(x) only)
         # the policy head's update on the transposed-chain kernel too (csrc/phead.hip): h1p / g1p /
         # g2p row-major, and the observation operand of p_fc1 AND v_fc1 row-major — x_buf itself
         # for a full-batch step (no x^T anywhere: the rollout skips writing it), the kernel's
@@ -197,11 +194,12 @@ class HipEngine:
         # (the 32x32 policy head at bf16x3 also sums p_fc2's weight gradient [128][128] right after
         # dW_mu: p_fc2 leaves the wgrad, and h1p / g2p their HBM round trip)
         np_pol = self.part_dw[0] + 32 * 128 + (128 * 128 if self.phead_p2 else 0)
-        self.part_h = [torch.zeros(self.nhead_blk, np_pol, **f32), torch.zeros(self.nhead_blk, 8 + 128, **f32)]
+        nv_val = 128
+        self.part_h = [torch.zeros(self.nhead_blk, np_pol, **f32), torch.zeros(self.nhead_blk, 8 + nv_val, **f32)]
         # world size 1: both head kernels write ONE partial buffer (policy its columns, value
         # column 1 and its dW_v after the policy's block) and one wgrad + gather/Adam launch
         # covers both heads (the observation^T operand is streamed once for p_fc1 and v_fc1)
-        self.part_joint = torch.zeros(self.nhead_blk, np_pol + 128, **f32)
+        self.part_joint = torch.zeros(self.nhead_blk, np_pol + nv_val, **f32)
         self.part_dw_joint = [self.part_dw[0], np_pol]
         self.head_range = [model.head_ranges["policy"], model.head_ranges["value"]]
         self.head_order = (0, 1)     # launch order of the joint head kernels (A/B: scripts/ab_iter.py)
@@ -230,19 +228,13 @@ class HipEngine:
         # buffers are fragment-major, so "row r" is a scattered index set.
         cols = torch.arange(self.ldT, device=device)
         # (row-major h1v / h1p: the t32 kernels write their bias columns themselves)
-        bias_rows = [(self.h2pT, lp2.fan_out), (self.h2vT, lv2.fan_out)]
-        if not self.vhead:
-            bias_rows.append((self.h1vT, lv1.fan_out))
+        bias_rows = [(self.h2pT, lp2.fan_out), (self.h2vT, lv2.fan_out), (self.h1vT, lv1.fan_out)]
         if not self.phead:
             bias_rows.append((self.h1pT, lp1.fan_out))
-        # wgrad operand layout flags (dY side of the 6 layers, then X side; 1 row-major, 2 the
-        # k16-blocked row-major layout [features / 16][ldT][16]): k16-blocked for v_fc1's dY (g1v)
-        # and v_fc2's dY (g2v) / X (h1v) under the 32x32 value head (csrc/vhead.hip)
+        # wgrad operand layout flags (dY side of the 6 layers, then X side; 1 row-major [ldT][features]):
+        # under the 32x32 policy head p_fc1's / p_fc2's dY (g1p, g2p), p_fc2's X (h1p) and the
+        # observation operand of both fc1 layers
         self.rm = [0] * 12
-        if self.vhead:
-            self.rm[3] = self.rm[4] = self.rm[6 + 4] = 2
-        # ... and under the 32x32 policy head p_fc1's / p_fc2's dY (g1p, g2p), p_fc2's X (h1p) and
-        # the observation operand of both fc1 layers
         self.wg_x_full = self.wg_x
         if self.phead:
             self.rm[0] = self.rm[1] = self.rm[6 + 0] = self.rm[6 + 1] = self.rm[6 + 3] = 1
@@ -283,6 +275,10 @@ class HipEngine:
         # launch (one element per thread: a grid-stride second pass would double the load latency
         # chain of the blocks that take it) needs A + 8 reduction blocks plus one per 256 elements
         n_whole = min(4096, (n - self.A + 255) // 256 + self.A + 8)
+        # (the fused gather + Adam launch takes one block per 32 reduce items first: with the fused
+        # narrow / second-layer weight gradients there are tens of thousands of items)
+        # (blocks of 32 items, csrc/kernels.h ITEM_IPB; sized for 8 so an A/B build with smaller blocks fits)
+        n_whole = min(4096, max(n_whole, -(-len(self.items["joint"][0]) // 8) + (n + 255) // 256))
         # per-head regions (fixed: every head launch writes each block of its region): policy
         # [0, np_), value [np_, np_ + nv_)
         (plo, phi), (vlo, vhi) = self.head_range
@@ -350,12 +346,13 @@ class HipEngine:
         names = [l.name for l in ls]
         # (the 32x32 policy head at bf16x3 sums p_fc2's weight gradient itself)
         pol = ("p_fc1",) if getattr(self, "phead_p2", False) else ("p_fc1", "p_fc2")
+        val = ("v_fc1", "v_fc2")
         if self.heads and joint:
-            groups = [[names.index(n) for n in pol + ("v_fc1", "v_fc2")]]
+            groups = [[names.index(n) for n in pol + val]]
             ranges = [(self.A, model.num_params)]
             partials = [True]
         elif self.heads:
-            groups = [[names.index(n) for n in pol], [names.index(n) for n in ("v_fc1", "v_fc2")]]
+            groups = [[names.index(n) for n in pol], [names.index(n) for n in val]]
             (_, phi), (vlo, vhi) = self.head_range
             ranges = [(self.A, phi), (vlo, vhi)]
             partials = [True, False]
@@ -506,14 +503,15 @@ class HipEngine:
             add("legacy", 8 + j, j)
         vlo = self.head_range[1][0]
 
-        def narrow(kind, layer, dw, base):
-            """the weight gradient of the narrow layer (rows j, k <= fan_in: k == fan_in is the bias)"""
+        def narrow(kind, layer, dw, base, stride=128):
+            """the weight gradient of a layer summed in a head kernel, [out][stride] at partial column
+            dw (rows j, k <= fan_in: k == fan_in is the bias)"""
             l = model.layer(layer)
             wo, bo = model.offsets[f"{layer}.weight"][0], model.offsets[f"{layer}.bias"][0]
             for j in range(l.fan_out):
                 for k in range(l.fan_in):
-                    add(kind, dw + j * 128 + k, wo - base + j * l.fan_in + k)
-                add(kind, dw + j * 128 + l.fan_in, bo - base + j)
+                    add(kind, dw + j * stride + k, wo - base + j * l.fan_in + k)
+                add(kind, dw + j * stride + l.fan_in, bo - base + j)
         for kind, dwp, dwv, vbase in (("policy", self.part_dw[0], None, None),
                                       ("value", None, self.part_dw[1], vlo),
                                       ("joint", self.part_dw_joint[0], self.part_dw_joint[1], 0)):
@@ -1049,10 +1047,10 @@ class HipEngine:
 
     def _head_kernel(self, h: int, idx_t, first: bool, xt_ready: bool, part: torch.Tensor, part_dw: int) -> None:
         p, M = self.p, self.mb
-        t32 = (h == 1 and self.vhead) or (h == 0 and self.phead)
+        t32 = h == 0 and self.phead
         opts = [0 if p.loss == "ppo" else 1, 0 if p.value_loss == "mse" else 1,
                 1 if p.std_convention == "var" else 0, 1 if first else 0, part.shape[1], h, part_dw,
-                (2 if h == 0 and not self.phead_p2 else 1) if t32 else 0]
+                (1 if self.phead_p2 else 2) if t32 else 0]
         # (the 32x32 policy kernel: xt_ready as _minibatch resolved it — it writes X rows into xT
         # only for x-mode "mb", a minibatch)
         # fp8: the value head's fc1 on the e4m3 image; the policy's GEMMs only with fp8_policy_gemms

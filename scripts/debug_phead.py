@@ -36,9 +36,9 @@ def main():
     mb = N if mode == "full" else int(mode)
     p = ppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=128, exploration_size=N, batch_size=mb, dtype=dt,
                    ent_coeff=0.01, update_kernels="heads")
-    p.vhead_kernel = p.phead_kernel = True
+    p.phead_kernel = True
     eng, model, _, _ = _engine(p)
-    print("phead", eng.phead, "vhead", eng.vhead, "ldT", eng.ldT, flush=True)
+    print("phead", eng.phead, "ldT", eng.ldT, flush=True)
     xq = _fill_buffer(eng, model)
     idx = None if mode == "full" else torch.randperm(eng.N, generator=torch.Generator().manual_seed(5))[:mb]
     for nm in ("g1pT", "xT"):

@@ -19,7 +19,7 @@ def main():
     p = ppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=128, exploration_size=128 * 16, batch_size=mb,
                    dtype=dt, ent_coeff=0.01, loss="ppo", value_loss="mse", update_kernels="heads")
     eng, model, _, _ = _engine(p)
-    print("vhead", eng.vhead, "phead", getattr(eng, "phead", None), flush=True)
+    print("phead", getattr(eng, "phead", None), flush=True)
     _fill_buffer(eng, model)
     idx = torch.randperm(eng.N, generator=torch.Generator().manual_seed(5))[:mb]
     for name in ("h1vT", "g1vT", "g2vT", "h1pT", "g1pT", "g2pT", "xT"):

@@ -22,8 +22,6 @@ from pytorch_dppo_amd.utils.obs_stats import RunningObsStats  # noqa: E402
 
 # stamp i -> i+1 phases (HD_STAMP 0..7), plus fc1 sub-spans from stamps 8 / 9
 PHASES = ["fc1", "fc2", "fc3 wait", "fc3 + loss", "dgrad fc3", "dgrad fc2", "partials"]
-# the 32x32 transposed-chain value head (csrc/vhead.hip VH_STAMP)
-VPHASES = ["fc1", "fc2", "fc3 + loss + g2", "dgrad passes 0-1", "dgrad pass 2", "dgrad pass 3", "partials"]
 EVERY = 8
 
 
@@ -32,7 +30,7 @@ def main():
     args = [x for x in sys.argv[1:] if not x.startswith("--")]
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536, batch_size=65536,
                     dtype=args[0] if args else "bf16x3", update_kernels="heads")
-    p.vhead_kernel = "--vhead" in sys.argv     # the 32x32 value head (csrc/vhead.hip)
+    p.phead_kernel = False     # (the 32x32 policy head, csrc/phead.hip, takes no stamps)
     spec = get_spec(p.env_name)
     torch.manual_seed(0)
     model = ActorCritic(spec.obs_dim, spec.act_dim).to(dev)
@@ -50,8 +48,7 @@ def main():
     out = {}
     mbt = eng._minibatch(None)
     for h in (0, 1):
-        # (the 32x32 value head: 4 waves, one per SIMD, csrc/vhead.hip)
-        nw = 4 if (h == 1 and bool(getattr(eng, "vhead", False))) else int(ext.head_waves(h))
+        nw = int(ext.head_waves(h))
         buf = torch.zeros(((nblk + EVERY - 1) // EVERY) * nw * 16, dtype=torch.int64, device=dev)
         for _ in range(3):
             eng._head_chain(h, *mbt)
@@ -66,20 +63,12 @@ def main():
         t = buf.view(-1, nw, 16).cpu().double()
         d = t[:, :, 1:8] - t[:, :, 0:7]
         tot = t[:, :, 7] - t[:, :, 0]
-        vh = h == 1 and bool(getattr(eng, "vhead", False))
-        res = {"kernel": "vhead_kernel (32x32 transposed chain)" if vh else "mlp_head_kernel",
+        res = {"kernel": "mlp_head_kernel",
                "sampled_blocks": t.shape[0], "total_cycles_median": float(tot.max(dim=1).values.median()),
                "chain_ms": ev[0].elapsed_time(ev[1]),
                "phases_median_cycles(max over waves)": {ph: float(d[:, :, i].max(dim=1).values.median())
-                                                        for i, ph in enumerate(VPHASES if vh else PHASES)},
+                                                        for i, ph in enumerate(PHASES)},
                }
-        if vh:
-            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-            rnd = (torch.arange(t.shape[0]) * EVERY) // ncu
-            res["total_by_round"] = {int(r): float(tot[rnd == r].max(dim=1).values.median())
-                                     for r in sorted(set(rnd.tolist()))}
-            out["value"] = res
-            continue
         res["fc1_first_span"] = float((t[:, :, 8] - t[:, :, 0]).max(dim=1).values.median())
         res["fc1_mid_span(4 k-steps value / 3 stages policy)"] = float((t[:, :, 9] - t[:, :, 8]).max(dim=1).values.median())
         # sub-spans (max over waves): fc3 MFMAs (3 -> 12) vs the loss (12 -> 4); the partials phase as

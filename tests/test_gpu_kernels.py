@@ -155,47 +155,8 @@ def test_vhead_forward_matches_torch_and_16x16_head(dtype, tol):
 
 
 @pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
-@pytest.mark.parametrize("loss,value_loss,mb", [("ppo", "mse", 1024), ("ppo", "clipped_half", 1000),
-                                                ("dppo_ref", "clipped_half", 768)])
-def test_vhead_update_matches_16x16_head_update(dtype, loss, value_loss, mb):
-    """The value head's update on the 32x32 transposed-chain kernel (row-major h1v / g1v / g2v
-    wgrad operands, read by the wgrad's transposing LDS reads) vs the 16x16 head kernel
-    (vhead_kernel=False: fragment-major operands): the whole gradient, the loss sums and the
-    reference loss's v_prev, on an index-gathered minibatch (a ragged last workgroup at mb 1000 /
-    768: rows past M carry zero gradient), and vs autograd for the ppo loss"""
-    kw = dict(device="gpu", env_name="Humanoid-v2", num_envs=128, exploration_size=128 * 16, batch_size=mb,
-              dtype=dtype, ent_coeff=0.01, loss=loss, value_loss=value_loss, update_kernels="heads")
-    bf = dtype == "bf16"
-    res = {}
-    for vh in (True, False):
-        p = ppo_preset(**kw) if loss == "ppo" else dppo_preset(**kw)
-        p.vhead_kernel = vh
-        p.phead_kernel = False    # the value head alone (the policy head: test_phead_update_*)
-        eng, model, _, _ = _engine(p)
-        assert eng.vhead == vh
-        xq = _fill_buffer(eng, model)
-        idx = torch.randperm(eng.N, generator=torch.Generator().manual_seed(5))[:mb]
-        eng.begin_update()
-        eng.grad(idx)
-        torch.cuda.synchronize()
-        res[vh] = (eng.grad_flat.clone(), eng.last_losses(), eng.v_prev.clone())
-        if vh and loss == "ppo":
-            g_ref, _ = _torch_grad(model, p, xq, eng, idx.to(DEV))
-            assert (eng.grad_flat - g_ref).norm().item() / g_ref.norm().item() < (6e-2 if bf else 2e-4)
-    (g1, l1, vp1), (g0, l0, vp0) = res[True], res[False]
-    assert torch.isfinite(g1).all()
-    rel = (g1 - g0).norm().item() / g0.norm().item()
-    assert rel < (2e-2 if bf else 2e-5), rel
-    for k in ("loss_value", "loss_clip", "loss_ent"):
-        assert abs(l1[k] - l0[k]) < (1e-2 if bf else 1e-5) * (1 + abs(l0[k])), (k, l1[k], l0[k])
-    if loss == "dppo_ref":
-        assert (vp1 - vp0).abs().max().item() <= (2e-2 if bf else 2e-5) * (1 + vp0.abs().max().item())
-
-
-@pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
-@pytest.mark.parametrize("loss,mb,vh", [("ppo", None, True), ("ppo", 1024, True), ("ppo", 1000, False),
-                                        ("dppo_ref", 768, True), ("ppo", None, False)])
-def test_phead_update_matches_16x16_head_update(dtype, loss, mb, vh):
+@pytest.mark.parametrize("loss,mb", [("ppo", None), ("ppo", 1024), ("ppo", 1000), ("dppo_ref", 768)])
+def test_phead_update_matches_16x16_head_update(dtype, loss, mb):
     """The policy head's update on the 32x32 transposed-chain kernel (csrc/phead.hip: row-major
     h1p / g1p / g2p, the observation operand of both fc1 layers row-major — x_buf itself for a
     full batch (mb None), the kernel's gathered rows for a minibatch; dW_mu by MFMA over the
@@ -209,10 +170,9 @@ def test_phead_update_matches_16x16_head_update(dtype, loss, mb, vh):
     res = {}
     for ph in (True, False):
         p = ppo_preset(**kw) if loss == "ppo" else dppo_preset(**kw)
-        p.vhead_kernel = ph and vh     # (vh False: the policy kernel beside the 16x16 value head)
         p.phead_kernel = ph
         eng, model, _, _ = _engine(p)
-        assert eng.phead == ph and eng.vhead == (ph and vh)
+        assert eng.phead == ph
         # (bf16x3: p_fc2's weight gradient summed in the kernel; bf16: h1p / g2p row-major for the wgrad)
         assert eng.phead_p2 == (ph and not bf)
         xq = _fill_buffer(eng, model)
@@ -267,57 +227,48 @@ def test_phead_gate_on_observation_width(env_name):
 
 @pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
 def test_wgrad_row_major_operands_match_fragment_major(dtype):
-    """The wgrad reading the 32x32 value head's k16-blocked row-major operands ([features / 16][ldT]
-    [16], per-lane DMA into XOR-swizzled 128-byte-row images, ds_read_b64_tr_b16) gives the same MFMA
-    operands in the same k order as the plain row-major copy ([ldT][features], rm flag 1: the policy
-    head's layout) — bit-identical slabs — and as the fragment-major copy of the same values"""
+    """The wgrad reading the 32x32 policy head's row-major operands ([ldT][features]: g1p, and at bf16
+    g2p / h1p; per-lane DMA into XOR-swizzled 128-byte-row images, ds_read_b64_tr_b16) gives the same
+    slabs as the fragment-major copies of the same values (rm flag 0).  (p_fc1's observation operand
+    stays x_buf's rows in both.)"""
     from pytorch_dppo_amd.models.actor_critic import fm_index
     p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=256, exploration_size=256 * 16,
                     batch_size=256 * 16, dtype=dtype, update_kernels="heads")
-    p.phead_kernel = False   # the value layers' operands only (v_fc1's X stays fragment-major)
-    p.vhead_kernel = True
     eng, model, _, _ = _engine(p)
-    assert eng.vhead
+    assert eng.phead
     _fill_buffer(eng, model)
     eng.begin_update()
     eng.grad(None)
     torch.cuda.synchronize()
-    b = eng.buckets[1]   # the value layers' bucket (v_fc1, v_fc2)
-    eng.ext.wgrad(eng._wgrad_dt(), eng.wg_g, eng.wg_x, eng.g_rows, eng.x_rows, eng.ldT, b["tasks"],
+    assert eng._x_mode == "buf"
+    b = eng.buckets[0]   # the policy layers' bucket (p_fc1 [, p_fc2])
+    wg_x = list(eng.wg_x_full)
+    eng.ext.wgrad(eng._wgrad_dt(), eng.wg_g, wg_x, eng.g_rows, eng.x_rows, eng.ldT, b["tasks"],
                   b["tasks_host"], b["slab"], *eng._q8_args(), eng.rm)
     slab_rm = b["slab"].clone()
-    assert [eng.rm[3], eng.rm[4], eng.rm[10]] == [2, 2, 2]
-    # the plain row-major and fragment-major copies of the k16-blocked operands
-    fm, rmc = {}, {}
-    for name, li, side in (("g1vT", 3, "g"), ("g2vT", 4, "g"), ("h1vT", 4, "x")):
+    ops = [("g1pT", 0, "g")] + ([] if eng.phead_p2 else [("g2pT", 1, "g"), ("h1pT", 1, "x")])
+    wg_g, rm = list(eng.wg_g), list(eng.rm)
+    for name, li, side in ops:
+        assert rm[li if side == "g" else 6 + li] == 1
         buf = getattr(eng, name)
         width = (eng.g_rows if side == "g" else eng.x_rows)[li]
-        # (k16-blocked [width / 16][ldT][16] -> [ldT][features]: a pure permutation of the slots)
-        rmc[name] = buf.view(-1).view(width // 16, eng.ldT, -1).permute(1, 0, 2).contiguous().view_as(buf)
-        rows = eng.decode(rmc[name]).view(eng.ldT, width)             # [ldT][features]
+        rows = eng.decode(buf).view(eng.ldT, width)             # [ldT][features]
         f = torch.arange(width, device=DEV).repeat_interleave(eng.ldT)
         c = torch.arange(eng.ldT, device=DEV).repeat(width)
         flat = torch.zeros(width * eng.ldT, device=DEV)
         flat[fm_index(f, c, eng.ldT)] = rows.t().reshape(-1)
-        fm[name] = eng.encode(flat).view_as(buf)
-    wg_g = list(eng.wg_g)
-    wg_x = list(eng.wg_x)
-    wg_g[3], wg_g[4], wg_x[4] = rmc["g1vT"], rmc["g2vT"], rmc["h1vT"]
-    b["slab"].zero_()
-    rm1 = [1 if f else 0 for f in eng.rm]
-    eng.ext.wgrad(eng._wgrad_dt(), wg_g, wg_x, eng.g_rows, eng.x_rows, eng.ldT, b["tasks"],
-                  b["tasks_host"], b["slab"], *eng._q8_args(), rm1)
-    assert torch.equal(slab_rm, b["slab"])   # same bytes, same operands, same order
-    wg_g[3], wg_g[4], wg_x[4] = fm["g1vT"], fm["g2vT"], fm["h1vT"]
+        (wg_g if side == "g" else wg_x)[li] = eng.encode(flat).view_as(buf)
+        rm[li if side == "g" else 6 + li] = 0
     b["slab"].zero_()
     eng.ext.wgrad(eng._wgrad_dt(), wg_g, wg_x, eng.g_rows, eng.x_rows, eng.ldT, b["tasks"],
-                  b["tasks_host"], b["slab"], *eng._q8_args(), [0] * 12)
+                  b["tasks_host"], b["slab"], *eng._q8_args(), rm)
+    slab_fm = b["slab"]
     # (the fragment-major copies are re-encoded from the decoded fp32 rows: a split-bf16 value can
     # re-split with its lo part one rounding step off, so the slabs agree to that rounding)
     if dtype == "bf16":
-        assert torch.equal(slab_rm, b["slab"])
+        assert torch.equal(slab_rm, slab_fm)
     else:
-        assert (slab_rm - b["slab"]).abs().max().item() <= 2e-5 * b["slab"].abs().max().item() + 1e-6
+        assert (slab_rm - slab_fm).abs().max().item() <= 2e-5 * slab_fm.abs().max().item() + 1e-6
 
 
 def _torch_rollout(params, model, seed_state_from):
@@ -905,25 +856,22 @@ def test_head_kernels_match_one_kernel_update(env_name, mb, dtype, loss, monkeyp
         eng.grad(idx)
         n1p, n1v = model.layer("p_fc1").fan_out, model.layer("v_fc1").fan_out
 
-        def rowmajor(buf, nfeat, rm=False, kb=False):   # FM [features][ldT] -> [features][mb]
-            if kb:   # the 32x32 value head's k16-blocked rows [width / 16][ldT][16] (csrc/vhead.hip)
-                return eng.decode(buf).view(-1, eng.ldT, 16).permute(1, 0, 2).reshape(eng.ldT, -1)[:mb, :nfeat].t()
+        def rowmajor(buf, nfeat, rm=False):   # FM [features][ldT] -> [features][mb]
             if rm:   # [ldT][width] rows (the 32x32 policy head's X rows)
                 return eng.decode(buf).view(eng.ldT, -1)[:mb, :nfeat].t()
             r = torch.arange(nfeat, device=DEV).repeat_interleave(mb)
             c = torch.arange(mb, device=DEV).repeat(nfeat)
             return eng.decode(buf).reshape(-1)[fm_index(r, c, eng.ldT)].view(nfeat, mb)
 
-        # (the 32x32 policy head: X rows row-major; h1p is not stored — p_fc2's weight gradient is
-        # summed in the kernel — so both arms compare h1v instead)
+        # (the 32x32 policy head: X rows row-major, h1p row-major or not stored — p_fc2's weight
+        # gradient summed in the kernel — so both arms compare h1v instead)
         ph = bool(getattr(eng, "phead", False))
         if heads == "1":
             use_h1v = ph
-        vh = bool(getattr(eng, "vhead", False))
-        h1 = (rowmajor(eng.h1vT, model.layer("v_fc2").fan_in, kb=vh) if use_h1v
+        h1 = (rowmajor(eng.h1vT, model.layer("v_fc2").fan_in) if use_h1v
               else rowmajor(eng.h1pT, n1p))
         res[heads] = (eng.grad_flat.clone(), eng.last_losses(), h1,
-                      rowmajor(eng.g1vT, n1v, kb=vh),
+                      rowmajor(eng.g1vT, n1v),
                       rowmajor(eng.xT, model.num_inputs, ph), eng.mu_prev.clone(), eng.v_prev.clone())
         if heads == "1" and loss == "ppo":
             g_ref, _ = _torch_grad(model, p, xq, eng, idx.to(DEV))
