@@ -490,7 +490,6 @@ WgradArgs wgrad_args(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torc
                      std::vector<int64_t> g_rows, std::vector<int64_t> x_rows, int64_t ld, torch::Tensor tasks,
                      torch::Tensor tasks_host, torch::Tensor slab, torch::Tensor q8_amax, int64_t q8_step,
                      std::vector<int64_t> q8_t, std::vector<double> q8_xs, std::vector<int64_t> rm) {
-  const int wmax = 8, smax = 6;   // quadrants per task: one per wave of the 8-wave workgroup
   TORCH_CHECK(gT.size() == 6 && xT.size() == 6 && g_rows.size() == 6 && x_rows.size() == 6, "6 layers");
   check(tasks, "tasks", at::kInt, WGRAD_TASK_INTS);
   TORCH_CHECK(tasks.numel() % WGRAD_TASK_INTS == 0, "tasks are 8-int records");
@@ -499,11 +498,13 @@ WgradArgs wgrad_args(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torc
   auto th = tasks_host.contiguous();
   const int* tp = th.data_ptr<int>();
   int64_t slab_need = 0;
+  bool wide = false;
   for (int i = 0; i < ntasks; ++i) {
     const int* t = tp + WGRAD_TASK_INTS * i;
     TORCH_CHECK(t[0] >= 0 && t[0] < 6, "task layer");
     const int nq = t[6], kq = t[7];
-    TORCH_CHECK(nq >= 1 && kq >= 1 && nq * kq <= wmax && nq + kq <= smax, "task quadrants beyond the workgroup");
+    TORCH_CHECK(wgrad_task_ok((int)dt, nq, kq), "task quadrants beyond the workgroup (wgrad_task_ok)");
+    wide = wide || nq * kq > 8;
     TORCH_CHECK(t[1] >= 0 && t[2] >= 0 && t[1] % 16 == 0 && t[2] % 16 == 0, "task tile origin");
     TORCH_CHECK(t[1] + 64 * nq <= g_rows[t[0]] && t[2] + 64 * kq <= x_rows[t[0]], "task tile beyond operand rows");
     // the kernel consumes 32-row k-steps in pairs (e4m3: in fours): every range is a positive
@@ -534,6 +535,7 @@ WgradArgs wgrad_args(int64_t dt, std::vector<torch::Tensor> gT, std::vector<torc
     TORCH_CHECK(len % 64 == 0 && ld * len * (dt == 3 ? 4 : 2) < (int64_t(1) << 40), "row-major operand rows");
     (i < 6 ? a.g_rm[i] : a.x_rm[i - 6]) = (int)len;
   }
+  a.wide = wide ? 1 : 0;
   a.tasks = reinterpret_cast<const WgradTask*>(tasks.data_ptr<int>());
   a.ntasks = ntasks;
   a.slab = slab.data_ptr<float>();
@@ -864,6 +866,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_train_tstamp", &set_train_tstamp);
   m.def("set_rollout_tstamp", &set_rollout_tstamp);
   m.def("wgrad", &wgrad);
+  m.def("wgrad_task_ok", [](int64_t dt, int64_t nq, int64_t kq) { return wgrad_task_ok((int)dt, (int)nq, (int)kq) != 0; });
   m.def("grad_gather", &grad_gather);
   m.def("gae", &gae);
   m.def("set_adam_fused", [](int64_t on) { set_adam_fused((int)on); });

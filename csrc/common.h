@@ -299,13 +299,14 @@ inline void set_max_lds_once(size_t bytes) {
 // the loads of 16 chunks are issued before the first add, instead of one load -> wait -> add
 // round trip per chunk that a variable trip count otherwise compiles to.
 __device__ __forceinline__ float slab_sum(const float* __restrict__ p, int nch, size_t st) {
+  constexpr int B = 16;   // (24 / 32 in flight: 106 / 131 VGPRs, no faster; profiles/r6/ab_iter_slab_batch.log)
   float s = 0.f;
-  for (int c0 = 0; c0 < nch; c0 += 16) {
-    float x[16];
+  for (int c0 = 0; c0 < nch; c0 += B) {
+    float x[B];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) x[c] = (c0 + c < nch) ? p[(size_t)(c0 + c) * st] : 0.f;
+    for (int c = 0; c < B; ++c) x[c] = (c0 + c < nch) ? p[(size_t)(c0 + c) * st] : 0.f;
 #pragma unroll
-    for (int c = 0; c < 16; ++c)
+    for (int c = 0; c < B; ++c)
       if (c0 + c < nch) s += x[c];
   }
   return s;

@@ -212,6 +212,7 @@ struct WgradArgs {
   // row-major operands: the row length in elements of layer l's dY (g_rm) / X (x_rm) operand
   // ([ld rows][features]: csrc/phead.hip, x_buf), 0 = fragment-major
   int g_rm[6], x_rm[6];
+  int wide;   // some task runs two quadrants per wave (wgrad_task_ok): the launch takes the wider LDS ring
 };
 
 extern "C" {
@@ -231,6 +232,7 @@ void set_s3_train_waves(int nw);                // split-bf16 32-row tile: 4 or 
 void set_s3_value_waves(int nw);                // split-bf16 value forward: 4 or 8 waves (A/B)
 int mlp_train_waves(int dt, const MlpArgs& a);  // workgroup waves the launcher will use
 void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s);
+int wgrad_task_ok(int dt, int nq, int kq);   // the (nq, kq) quadrant tiles the wgrad kernel runs
 // grad[i] for i in [i_lo, i_hi) from the slabs (src_off / src_meta: see grad_gather_kernel);
 // with_partials: also log_std grads [0, A) and the 8 loss sums from the per-workgroup partials
 void launch_grad_gather(const float* slab, const int* src_off, const int* src_meta, const float* part, int nblk,

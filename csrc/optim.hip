@@ -340,8 +340,8 @@ __global__ __launch_bounds__(256) void gather_adam_kernel(
     const int o = src_off[i];
     const float mi = m[i], vi = v[i], pv = p[i];
     const int wi = w_map[i], wti = wt_map[i];
-    const int nch = mt >> 4;
-    const size_t st = (size_t)(mt & 15) << 12;
+    const int nch = mt >> 5;
+    const size_t st = (size_t)(mt & 31) << 12;
     const float s = slab_sum(slab + o, nch, st);
     const float gi = s * scale;
     ss = fmaf(gi, gi, ss);

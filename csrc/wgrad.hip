@@ -5,8 +5,8 @@
 // Both operands are feature-major (written transposed by mlp_train_kernel), so every MFMA
 // fragment is one 16-byte load along m, the reduction axis.  A task = (layer, output tile,
 // batch chunk).  The tile is nq x kq QUADRANTS of 64x64 (nq * kq <= 8, nq + kq <= 6), one per
-// wave of the 8-wave workgroup; each quadrant = 4x4 MFMA tiles of 16x16 (64 f32 accumulator
-// registers).  The host plan picks (nq, kq) per layer to minimise operand rows read per
+// wave of the 8-wave workgroup, or at split-bf16 / bf16 up to 16 quadrants, two per wave
+// (wgrad_task_ok); each quadrant = 4x4 MFMA tiles of 16x16 (64 f32 accumulator registers).  The host plan picks (nq, kq) per layer to minimise operand rows read per
 // k-step: the kernel is bound by the operand stream (HBM / MALL), and a 256x128 tile reads
 // 384 rows per step for 2x the outputs of a 128x128 tile's 256 (v_fc1: 2304 instead of 3072
 // rows per step).  Results go to per-chunk fp32 slabs ([nq*64][kq*64] per task) that
@@ -17,7 +17,6 @@
 namespace {
 
 constexpr int WG_WAVES = 8;
-constexpr int WG_SLOTS = 24;   // fragment slots per stage: (nq + kq) * 4 <= 24 (nq + kq <= 6)
 
 // The workgroup stages each k-step's distinct fragments (4*nq of dY^T, 4*kq of X^T) ONCE into
 // LDS with LDS-DMA (global_load_lds_dwordx4): an FM fragment is 64 lanes x 16 B per KiB in lane
@@ -25,7 +24,7 @@ constexpr int WG_SLOTS = 24;   // fragment slots per stage: (nq + kq) * 4 <= 24 
 // ds_read_b128 at lane*16.  A split-bf16 fragment (32 B per lane: hi | lo) is two DMA
 // instructions, instruction h moving the fragment's h-th KiB (lanes 32h .. 32h+31) so it lands
 // as [their hi][their lo] (the dense layout of mlp_stream.hip frag_lane_off).  Each wave DMAs C
-// fixed slots per stage (C = 2 when the task has <= 16 fragments, else 3; slots past the task's
+// fixed slots per stage (C = 2 when the task has <= 16 fragments, 3 <= 24, 4 <= 32, 5 <= 40; slots past the task's
 // fragment count re-load one of its fragments, an L2 hit, so every wave's DMA count — and with
 // it the vmcnt arithmetic — is task-independent).  S-deep ring, counted vmcnt and a raw
 // s_barrier keep S-1 steps of DMA in flight across the barrier (cdna_hip_programming.md
@@ -39,8 +38,6 @@ constexpr int wgrad_frag_bytes() { return DT == DT_FP8 ? 2048 : 512 * Prec<DT>::
 template <int DT>
 constexpr int wgrad_step_rows() { return DT == DT_FP8 ? 128 : 32; }
 typedef __attribute__((ext_vector_type(8))) int i32x8;
-template <int DT, int S>
-constexpr size_t wgrad_lds_bytes() { return (size_t)S * WG_SLOTS * wgrad_frag_bytes<DT>(); }
 
 // the 16-byte chunk swizzle of a row-major operand image (128-byte rows): even XOR values keep the two
 // chunks of a 16-feature column group adjacent; rows r, r + 2, r + 8, r + 10 (the rows of a 32-lane
@@ -87,14 +84,37 @@ DEV typename Prec<DT>::Frag rm_frag_at(const char* st, const unsigned (&o)[4]) {
   }
 }
 
-template <int DT, int S, int C>
+// Tasks of up to 8 quadrants run one quadrant per wave (QW 1: 24 fragment slots per stage); split-bf16
+// and bf16 tasks of 9-16 quadrants (nq even) run TWO per wave (QW 2: 40 slots, nq + kq <= 10), the
+// wave's quadrants (wn, wk) and (wn + nq / 2, wk) sharing its X fragments — a wider tile streams fewer
+// operand rows per output (Humanoid v_fc1 as 4x4 + 4x2 quadrant tiles: 28 x 64 rows per k-step
+// instead of 36 x 64 with 4x2 tiles) and a wave reads 12 fragments per 32 MFMA tiles instead of 8
+// per 16.  The ring depth follows the stage size: split-bf16 3 stages of 24 slots or 2 of 40 (the
+// twice-longer stage covers the same latency), bf16 4 of either.
+template <int DT, int QW>
+struct WgCfg {
+  static constexpr int SLOTS = QW == 1 ? 24 : 40;
+  static constexpr int S = DT == DT_BF16 ? 4 : (QW == 1 ? 3 : 2);
+};
+template <int DT, bool WIDE>
+constexpr size_t wgrad_lds_bytes() {
+  constexpr size_t one = (size_t)WgCfg<DT, 1>::S * WgCfg<DT, 1>::SLOTS * wgrad_frag_bytes<DT>();
+  constexpr size_t two = (size_t)WgCfg<DT, 2>::S * WgCfg<DT, 2>::SLOTS * wgrad_frag_bytes<DT>();
+  return WIDE && two > one ? two : one;
+}
+static_assert(wgrad_lds_bytes<DT_S3, true>() <= 160 * 1024 && wgrad_lds_bytes<DT_BF16, true>() <= 160 * 1024, "wgrad LDS");
+
+template <int DT, int QW, int C>
 DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   using P = Prec<DT>;
   using T = typename P::T;
   using Frag = typename P::Frag;
   constexpr int FB = wgrad_frag_bytes<DT>();     // bytes per fragment
   constexpr int NI = FB / 1024;                  // DMA instructions per fragment (64 lanes x 16 B)
-  constexpr int SB = WG_SLOTS * FB;              // bytes per stage
+  constexpr int S = WgCfg<DT, QW>::S;
+  constexpr int SB = WgCfg<DT, QW>::SLOTS * FB;  // bytes per stage
+  static_assert(QW == 1 || DT == DT_S3 || DT == DT_BF16, "two quadrants per wave: split-bf16 / bf16");
+  static_assert(C * WG_WAVES <= WgCfg<DT, QW>::SLOTS, "slots");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const char* g = reinterpret_cast<const char*>(a.gT[tk.layer]);
@@ -104,12 +124,12 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   const int NF = 4 * tk.nq, F = NF + 4 * tk.kq;
   // slot f of a stage holds fragment f: f < NF -> dY^T row tile n0/16 + f, else X^T row tile
   // k0/16 + f - NF.  Wave w DMAs slots C*w .. C*w + C-1 (a slot >= F re-loads fragment f mod F).
-  // FM operands: a fragment is contiguous (FB bytes per k-step).  Row-major operands (RM: the
-  // transposed-chain value head's h1 / g1 / g2, csrc/vhead.hip; row length a.g_rm / a.x_rm): a
-  // quadrant's 4 slots hold its [32 rows][64 features] image per k-step — bf16: 128-byte rows, the
-  // 16-byte chunks XOR-swizzled by wgrad_swz(row), 8 rows per DMA instruction; split-bf16: the
-  // memory's 256-byte [8 hi | 8 lo] rows, wgrad_swz16, 4 rows per instruction — read back
-  // transposed (ds_read_b64_tr_b16).
+  // FM operands: a fragment is contiguous (FB bytes per k-step).  Row-major operands (the 32x32
+  // policy head's g1p / g2p / h1p and the observation rows, csrc/phead.hip; row length a.g_rm /
+  // a.x_rm): a quadrant's 4 slots hold its [32 rows][64 features] image per k-step — bf16: 128-byte
+  // rows, the 16-byte chunks XOR-swizzled by wgrad_swz(row), 8 rows per DMA instruction;
+  // split-bf16: the memory's 256-byte [8 hi | 8 lo] rows, wgrad_swz16, 4 rows per instruction —
+  // read back transposed (ds_read_b64_tr_b16).
   const char* srcp[C][NI];
   size_t kstride[C];
   int dst[C];
@@ -161,37 +181,47 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
   // oldest vector-memory op: it never holds up a counted wait), folded in the epilogue
   uint32_t q8v = 0;
   if constexpr (DT == DT_FP8) q8v = a.q8_rd[(a.q8_t[tk.layer] * Q8_SUB + lane) * Q8_LINE];
-  const bool active = wave < tk.nq * tk.kq;
+  // QW 2: waves (wn, wk) for wn < nq / 2, quadrant rows wn and wn + nq / 2
+  const int nqw = QW == 1 ? tk.nq : tk.nq >> 1;
+  const bool active = wave < nqw * tk.kq;
   constexpr bool RMOK = DT == DT_S3 || DT == DT_BF16;   // (fp32 / e4m3 operands are fragment-major only)
   const bool g_rm = RMOK && a.g_rm[tk.layer] != 0, x_rm = RMOK && a.x_rm[tk.layer] != 0;
   const int wn = wave / tk.kq, wk = wave - (wave / tk.kq) * tk.kq;
-  // per-lane byte offsets (within a stage) of the wave's 4 dY and 4 X fragments: fragment-major
-  // [0] = the lane's 16 bytes; row-major [0] / [1] = the two 4-row transposed reads (rm_off)
-  unsigned oa[4][4], ob[4][4];
+  // per-lane byte offsets within a quadrant's 4 slots: fragment-major, the lane's 16 bytes of slot i
+  // at fmo + i * FB; row-major, the two 4-row transposed reads (rm_off) of slot i (split: hi, lo) —
+  // the same pattern for every quadrant and side (a quadrant adds its uniform slot base)
+  const unsigned fmo = IsSplit<DT>::value ? (unsigned)((lane >> 5) * 1024 + (lane & 31) * 16)
+                                          : (unsigned)(lane * 8 * (int)sizeof(T));
+  unsigned pat[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    auto fill = [&](unsigned (&o)[4], int f, bool rm) {
-      o[1] = o[2] = o[3] = 0;
-      if (RMOK && rm) {
-        if constexpr (IsSplit<DT>::value) {
-          for (int j = 0; j < 4; ++j) o[j] = rm_off_s3(f, j & 1, j >> 1, lane, FB);
-        } else {
-          o[0] = rm_off(f, 0, lane, FB);
-          o[1] = rm_off(f, 1, lane, FB);
-        }
-      } else {
-        o[0] = IsSplit<DT>::value ? (unsigned)(f * FB + (lane >> 5) * 1024 + (lane & 31) * 16)
-                                  : (unsigned)(f * FB + lane * 8 * (int)sizeof(T));
-      }
-    };
-    fill(oa[i], wn * 4 + i, g_rm);
-    fill(ob[i], NF + wk * 4 + i, x_rm);
+    pat[i][0] = pat[i][1] = pat[i][2] = pat[i][3] = 0;
+    if constexpr (IsSplit<DT>::value) {
+      for (int j = 0; j < 4; ++j) pat[i][j] = rm_off_s3(i, j & 1, j >> 1, lane, FB);
+    } else if constexpr (RMOK) {
+      pat[i][0] = rm_off(i, 0, lane, FB);
+      pat[i][1] = rm_off(i, 1, lane, FB);
+    }
   }
-  f32x4 acc[4][4];
+  // slot i of the quadrant whose first slot is `slot` in stage st
+  auto frag = [&](const char* st, int slot, bool rm, int i) __attribute__((always_inline)) -> Frag {
+    const char* qb = st + slot * FB;
+    if constexpr (RMOK)
+      if (rm) return rm_frag_at<DT>(qb, pat[i]);
+    const char* b = qb + fmo + i * FB;
+    if constexpr (IsSplit<DT>::value) {
+      return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + 512)};
+    } else {
+      return P::load(reinterpret_cast<const T*>(b));
+    }
+  };
+  f32x4 acc[QW][4][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int u = 0; u < QW; ++u)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[u][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < S - 1; ++s) issue(s);
   for (int k = 0; k < nk; ++k) {
@@ -204,7 +234,6 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
     if (!LATE || !active) issue(k + S - 1);
     if (active) {
       const char* st = smem + (k % S) * SB;
-      Frag af[4], bf[4];
       if constexpr (DT == DT_FP8) {
         // four e4m3 k-steps per slot: lane l's 8 bytes of k-step 4kk + j at j * 512 + l * 8.  The
         // 16x16x128 operand of lane l is those 32 bytes in j order — rows {32 j + 8 (l >> 4) + e}
@@ -228,30 +257,29 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8[i], b8[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+            acc[0][i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8[i], b8[j], acc[0][i][j], 0, 0, 0, 127, 0, 127);
         continue;
       }
-      // (lane offsets precomputed per task: the loop adds the stage base only)
-      auto lds_frag = [&](int i, bool rm, const unsigned (&o)[4][4]) {
-        if constexpr (DT == DT_S3 || DT == DT_BF16)
-          if (rm) return rm_frag_at<DT>(st, o[i]);
-        if constexpr (IsSplit<DT>::value) {
-          const char* b = st + o[i][0];
-          return Frag{*reinterpret_cast<const bf16x8*>(b), *reinterpret_cast<const bf16x8*>(b + 512)};
-        } else {
-          return P::load(reinterpret_cast<const T*>(st + o[i][0]));
-        }
-      };
+      Frag af[4], bf[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        af[i] = lds_frag(i, g_rm, oa);
-        bf[i] = lds_frag(i, x_rm, ob);
+        af[i] = frag(st, 4 * wn, g_rm, i);
+        bf[i] = frag(st, NF + 4 * wk, x_rm, i);
       }
       if constexpr (LATE) issue(k + S - 1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(acc[i][j], af[i], bf[j]);
+        for (int j = 0; j < 4; ++j) acc[0][i][j] = P::mma(acc[0][i][j], af[i], bf[j]);
+      if constexpr (QW == 2) {
+        // the second quadrant's dY fragments (its X fragments are the first's)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = frag(st, 4 * (wn + nqw), g_rm, i);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[QW - 1][i][j] = P::mma(acc[QW - 1][i][j], af[i], bf[j]);
+      }
     }
   }
   WAIT_VMCNT(0);                               // no DMA may outlive the workgroup's LDS
@@ -263,39 +291,50 @@ DEV void wgrad_lds_body(const WgradArgs& a, const WgradTask& tk, char* smem) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] *= inv;
+      for (int j = 0; j < 4; ++j) acc[0][i][j] *= inv;
   }
   const int col = wk * 64 + (lane & 15);
-  const int rbase = wn * 64 + (lane >> 4) * 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int u = 0; u < QW; ++u) {
+    const int rbase = (wn + u * nqw) * 64 + (lane >> 4) * 4;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * KE + col + 16 * j] = acc[i][j][q];
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(rbase + 16 * i + q) * KE + col + 16 * j] = acc[u][i][j][q];
+  }
 }
 
-template <int DT, int S>
+// WIDE: the launch holds two-quadrant-per-wave tasks (wgrad_task_ok), the LDS of either ring
+template <int DT, bool WIDE>
 __global__ __launch_bounds__(WG_WAVES * 64) void wgrad_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // the kernel's ONLY LDS object
   const WgradTask tk = a.tasks[blockIdx.x];
-  if (4 * (tk.nq + tk.kq) <= 2 * WG_WAVES) wgrad_lds_body<DT, S, 2>(a, tk, smem);
-  else wgrad_lds_body<DT, S, 3>(a, tk, smem);
+  const int F = 4 * (tk.nq + tk.kq);
+  if constexpr (WIDE) {
+    if (tk.nq * tk.kq > WG_WAVES) {
+      if (F <= 4 * WG_WAVES) wgrad_lds_body<DT, 2, 4>(a, tk, smem);
+      else wgrad_lds_body<DT, 2, 5>(a, tk, smem);
+      return;
+    }
+  }
+  if (F <= 2 * WG_WAVES) wgrad_lds_body<DT, 1, 2>(a, tk, smem);
+  else wgrad_lds_body<DT, 1, 3>(a, tk, smem);
 }
 
-// ring depth: fp32, split-bf16 and e4m3 3 stages (144 KiB), bf16 4 (96 KiB)
-template <int DT, int S>
+template <int DT, bool WIDE>
 void launch_wgrad_lds(const WgradArgs& a, hipStream_t s) {
-  const size_t lds = wgrad_lds_bytes<DT, S>();
-  set_max_lds_once<wgrad_kernel<DT, S>>(lds);
-  hipLaunchKernelGGL((wgrad_kernel<DT, S>), dim3(a.ntasks), dim3(WG_WAVES * 64), lds, s, a);
+  const size_t lds = wgrad_lds_bytes<DT, WIDE>();
+  set_max_lds_once<wgrad_kernel<DT, WIDE>>(lds);
+  hipLaunchKernelGGL((wgrad_kernel<DT, WIDE>), dim3(a.ntasks), dim3(WG_WAVES * 64), lds, s, a);
 }
 
 // Blocks [0, item_blocks(nitems)): the reduce items (log_std, loss-term sums, the per-head
 // kernels' fused narrow-layer weight gradients): column sums of the per-workgroup partial rows in
 // a fixed order (item_reduce), grad[d] = scale * sum or loss_out[q] (red_dst).
 // Blocks past them: grad[i] = scale * sum_{c < nch} slab[src_off[i] + c * stride] for the slab
-// elements i of `runs` (src_meta[i] = nch * 16 + stride / 4096, each tile has its own batch-chunk
+// elements i of `runs` (src_meta[i] = nch * 32 + stride / 4096, each tile has its own batch-chunk
 // count).  Fixed chunk order: deterministic; no float atomics anywhere.
 __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restrict__ slab,
                                                           const int* __restrict__ src_off,
@@ -322,8 +361,8 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
     const int i = runs.flat(j);
     const int mt = src_meta[i];
     const int o = src_off[i];
-    const int nch = mt >> 4;
-    const size_t st = (size_t)(mt & 15) << 12;
+    const int nch = mt >> 5;
+    const size_t st = (size_t)(mt & 31) << 12;
     const float s = slab_sum(slab + o, nch, st);
     grad[i] = s * scale;
   }
@@ -331,12 +370,25 @@ __global__ __launch_bounds__(256) void grad_gather_kernel(const float* __restric
 
 }  // namespace
 
+// a task's quadrant tile: one quadrant per wave (nq * kq <= 8, nq + kq <= 6: 24 slots), or at
+// split-bf16 / bf16 two per wave (9-16 quadrants, nq even, nq + kq <= 10: 40 slots)
+extern "C" int wgrad_task_ok(int dt, int nq, int kq) {
+  if (nq < 1 || kq < 1) return 0;
+  if (nq * kq <= WG_WAVES) return nq + kq <= 6;
+  return (dt == DT_S3 || dt == DT_BF16) && nq * kq <= 2 * WG_WAVES && nq % 2 == 0 && nq + kq <= 10;
+}
+
 extern "C" void launch_wgrad(int dt, const WgradArgs& a, hipStream_t s) {
   if (a.ntasks <= 0) return;
-  if (dt == DT_F32) launch_wgrad_lds<DT_F32, 3>(a, s);
-  else if (dt == DT_S3) launch_wgrad_lds<DT_S3, 3>(a, s);
-  else if (dt == DT_FP8) launch_wgrad_lds<DT_FP8, 3>(a, s);
-  else launch_wgrad_lds<DT_BF16, 4>(a, s);
+  if (dt == DT_F32) launch_wgrad_lds<DT_F32, false>(a, s);
+  else if (dt == DT_FP8) launch_wgrad_lds<DT_FP8, false>(a, s);
+  else if (dt == DT_S3) {
+    if (a.wide) launch_wgrad_lds<DT_S3, true>(a, s);
+    else launch_wgrad_lds<DT_S3, false>(a, s);
+  } else {
+    if (a.wide) launch_wgrad_lds<DT_BF16, true>(a, s);
+    else launch_wgrad_lds<DT_BF16, false>(a, s);
+  }
   HIP_CHECK_LAUNCH();
 }
 

@@ -107,6 +107,8 @@ class Params:
     stats_stream: str = "off"            # off | on | auto (on when an all-reduce sits in the chain): the
                                          # obs-stat reduce / all-reduce / merge on a side stream
     wgrad_wgs: int = 0                   # wgrad tasks per launch (0: one per CU of the device)
+    wgrad_wide: bool = True              # wgrad tiles of up to 16 quadrants, two per wave (split-bf16 / bf16;
+                                         # csrc/wgrad.hip)
     phead_kernel: bool = True            # the policy head on the 32x32 kernel (csrc/phead.hip)
     mlp_rows: int = 0                    # diagnostics: force the tile update kernel's row tile (0: auto)
 

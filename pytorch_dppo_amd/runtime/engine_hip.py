@@ -39,28 +39,43 @@ Q8_SUB = 64                  # sub-slots per tensor of the gradient-amax ring (c
 WT = 128            # operand-buffer row padding (csrc/kernels.h WGRAD_TILE)
 
 
-def wgrad_tiles(li: int, n: int, k: int):
+def wgrad_tile_ok(nq: int, kq: int, wide: bool = False) -> bool:
+    """the quadrant tiles the wgrad kernel runs (csrc/wgrad.hip wgrad_task_ok): one quadrant per wave
+    of the 8-wave workgroup (nq*kq <= 8, nq + kq <= 6: 24 fragment slots per ring stage), or with
+    ``wide`` (split-bf16 / bf16) two per wave (9-16 quadrants, nq even, nq + kq <= 10: 40 slots)"""
+    if nq < 1 or kq < 1:
+        return False
+    if nq * kq <= 8:
+        return nq + kq <= 6
+    return wide and nq * kq <= 16 and nq % 2 == 0 and nq + kq <= 10
+
+
+def wgrad_tiles(li: int, n: int, k: int, wide: bool = False):
     """Output tiles of one layer's weight gradient ([n][k], k including the bias column) for the
-    wgrad kernel: (layer, n0, k0, nq, kq), a tile = nq x kq quadrants of 64x64, one per wave of
-    the 8-wave workgroup (nq*kq <= 8, nq + kq <= 6).  The kernel streams (nq + kq) * 64 operand
-    rows per 32-row k-step, so the (nq, kq) minimising the layer's total rows read wins (ties:
-    fewer tasks, then wider n).  Humanoid v_fc1 (512 x 377): 4x2 tiles, 2304 rows per step
-    instead of 3072 with 128x128 tiles."""
+    wgrad kernel: (layer, n0, k0, nq, kq), a tile = nq x kq quadrants of 64x64 (wgrad_tile_ok).  The
+    kernel streams (nq + kq) * 64 operand rows per 32-row k-step, so the (nq, kq) minimising the
+    layer's total rows read wins (ties: fewer tasks, then wider n).  Humanoid v_fc1 (512 x 377):
+    4x2 tiles, 2304 rows per step instead of 3072 with 128x128 tiles; ``wide``: 4x4 + 4x2 tiles,
+    1792 rows per step."""
     N, K = -(-n // 64), -(-k // 64)
     best = None
-    for nq in range(1, 9):
-        for kq in range(1, 9):
-            if nq * kq > 8 or nq + kq > 6 or nq > N or kq > K:
+    for nq in range(1, 17):
+        for kq in range(1, 17):
+            if nq > N or kq > K or not wgrad_tile_ok(nq, kq, wide):
                 continue
             tl = []
             for a in range(0, N, nq):
                 for b in range(0, K, kq):
                     tl.append((li, a * 64, b * 64, min(nq, N - a), min(kq, K - b)))
+            if not all(wgrad_tile_ok(t[3], t[4], wide) for t in tl):
+                continue
             cost = sum(t[3] + t[4] for t in tl)
             key = (cost, len(tl), -nq)
             if best is None or key < best[0]:
                 best = (key, tl)
     return best[1]
+
+
 ROLL_ROWS = 16
 WGRAD_TARGET_WGS = 0     # wgrad tasks per launch; 0: one per CU of the device (256 on MI355X)
 
@@ -255,6 +270,12 @@ class HipEngine:
                 storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), Q8_SH, 2)
             else:
                 storage.set_elements(buf, fm_index(torch.full_like(cols, r), cols, self.ldT), 1.0, self.dt)
+        # wgrad tiles of up to 16 quadrants, two per wave (csrc/wgrad.hip; split-bf16 / bf16 operands):
+        # fewer operand rows streamed per output (v_fc1 1792 instead of 2304 rows per k-step), more
+        # slab chunks for the gather; per iteration −0.4 % at bf16x3, −2 % at bf16 (same process,
+        # profiles/r6/ab_heads_wide_*.log).  Restricting it to the fc1 layers was slower than both.
+        self.wgrad_wide = bool(params.wgrad_wide) and self.dt in (native.DT_CODE["bf16x3"], native.DT_CODE["bf16"]) \
+            and not self.q8
         self._build_wgrad_plan(model)
         if self.heads:
             # the joint (one-bucket) plan of world size 1 beside the per-head buckets
@@ -371,10 +392,12 @@ class HipEngine:
         # dealt over the tiles of ALL buckets together, so the per-head buckets and the joint one
         # split every tile identically: each weight-gradient element is the same fixed-order sum
         # on every path (the process-group chains == the in-stream joint path, bit for bit).
+        # (two quadrants per wave at split-bf16 / bf16: Params.wgrad_wide)
+        wide = bool(getattr(self, "wgrad_wide", False))
         all_tiles = []  # (layer, n0, k0, nq, kq)
         for li in sorted({li for layers in groups for li in layers}):
             l = ls[li]
-            all_tiles += wgrad_tiles(li, l.fan_out, l.fan_in + 1)
+            all_tiles += wgrad_tiles(li, l.fan_out, l.fan_in + 1, wide)
         costs = [t[3] + t[4] for t in all_tiles]
         raw = [target_wgs * c / sum(costs) for c in costs]
         nch_all = [max(1, int(r)) for r in raw]
@@ -412,7 +435,7 @@ class HipEngine:
                 j += 1
             tasks_host = torch.tensor(order, dtype=torch.int32).reshape(-1).contiguous()
             # flat index -> (offset of its element in its tile's chunk-0 slab, chunk count and
-            # slab stride of that tile packed as nch * 16 + size / 4096)
+            # slab stride of that tile packed as nch * 32 + size / 4096)
             for li in layers:
                 l = ls[li]
                 woff, wn = model.offsets[f"{l.name}.weight"]
@@ -427,7 +450,7 @@ class HipEngine:
             # on it); the elements without a tile (src_meta 0) are reduce items
             so, sm = src[lo:hi], meta[lo:hi]
             has = sm > 0
-            reach = so + ((sm >> 4) - 1).clamp(min=0) * ((sm & 15) << 12)
+            reach = so + ((sm >> 5) - 1).clamp(min=0) * ((sm & 31) << 12)
             assert bool((so[has] >= 0).all()) and int(reach[has].max()) < base, "wgrad gather plan exceeds its slab"
             self.buckets.append({
                 "tasks_host": tasks_host, "tasks": tasks_host.to(self.device),
@@ -549,7 +572,7 @@ class HipEngine:
                 continue
             m = (n >= n0) & (n < n0 + 64 * nq) & (k >= k0) & (k < k0 + 64 * kq)
             out[m] = base + (n[m] - n0) * (64 * kq) + (k[m] - k0)
-            meta[m] = nch * 16 + size // 4096
+            meta[m] = nch * 32 + size // 4096
         assert bool((out >= 0).all()), "wgrad tiles do not cover the layer"
         return out, meta
 

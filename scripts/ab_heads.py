@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Whole-iteration A/B of the update's head kernels on the bench configuration: the 16x16 head
 kernels (csrc/mlp_head.hip) vs the 32x32 transposed-chain policy head (csrc/phead.hip) beside the
-16x16 value head.  One worker per arm in ONE process, interleaved
+16x16 value head, and the wgrad's wide tiles vs one quadrant per wave ("narrow").  One worker per arm in ONE process, interleaved
 rounds of K deferred iterations each (the bench's production loop); ms per iteration per round.
 
-    python scripts/ab_heads.py [dtype] [rounds] [iters] [arms: h16,p32]
+    python scripts/ab_heads.py [dtype] [rounds] [iters] [arms: h16,p32,narrow]
 """
 import json
 import os
@@ -20,8 +20,8 @@ from pytorch_dppo_amd.parallel.dist import init_single_rank_collective  # noqa: 
 from pytorch_dppo_amd.runtime.launcher import free_port  # noqa: E402
 from pytorch_dppo_amd.runtime.worker import DPPOWorker  # noqa: E402
 
-# arm -> Params.phead_kernel
-ARMS = {"h16": False, "p32": True}
+# arm -> Params overrides: the 16x16 policy head, the default, the wgrad with one quadrant per wave
+ARMS = {"h16": {"phead_kernel": False}, "p32": {}, "narrow": {"wgrad_wide": False}}
 
 
 def main():
@@ -36,14 +36,15 @@ def main():
     for a in arms:
         # "<arm>:w<N>": the same arm with Params.wgrad_wgs = N (wgrad tasks per launch)
         base, _, wg = a.partition(":w")
-        ph = ARMS[base]
+
         p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=4096, exploration_size=65536,
                         batch_size=65536, dtype=dtype, seed=1, phase_timing=0)
-        p.phead_kernel = ph
+        for k, v in ARMS[base].items():
+            setattr(p, k, v)
         if wg:
             p.wgrad_wgs = int(wg)
         w = DPPOWorker(p, ctx)
-        assert w.engine.phead == ph, a
+        assert w.engine.phead == p.phead_kernel, a
         for _ in range(2):
             w.iteration_step()
         workers[a] = w

@@ -1255,6 +1255,34 @@ def test_bench_geometry_gradient_vs_autograd_on_fp32_observations(dtype, tol):
         assert (gk - gr).norm().item() <= 3 * tol * (gr.norm().item() + 1e-8), name
 
 
+@pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
+def test_wgrad_wide_tiles_match_one_quadrant_per_wave(dtype):
+    """The wgrad's wide plan (csrc/wgrad.hip: up to 16 quadrants per task, two per wave, a 40-slot
+    ring; Humanoid v_fc1 as four 4x3 tiles, p_fc1 one 2x6 tile over row-major operands) vs one
+    quadrant per wave (Params.wgrad_wide False) on the same full-batch buffer: the same products,
+    summed over different batch chunks — equal to fp32 rounding of the chunk sums."""
+    res = {}
+    for wide in (True, False):
+        p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=1024, exploration_size=1024 * 16,
+                        batch_size=1024 * 16, dtype=dtype, update_kernels="heads")
+        p.wgrad_wide = wide
+        eng, model, _, _ = _engine(p)
+        assert eng.wgrad_wide == wide
+        qs = [t[6] * t[7] for t in eng.joint_bucket["tasks_host"].view(-1, 8).tolist()]
+        assert (max(qs) > 8) == wide
+        _fill_buffer(eng, model, gen_seed=7)
+        eng.begin_update()
+        eng.grad(None)
+        torch.cuda.synchronize()
+        res[wide] = eng.grad_flat.clone()
+    assert torch.isfinite(res[True]).all()
+    for name in ("p_fc1", "p_fc2", "v_fc1", "v_fc2"):
+        for part in ("weight", "bias"):
+            o, n = model.offsets[f"{name}.{part}"]
+            a_, b_ = res[True][o:o + n], res[False][o:o + n]
+            assert (a_ - b_).norm().item() <= 1e-5 * (b_.norm().item() + 1e-8), (name, part)
+
+
 @pytest.mark.parametrize("env_name", ["Humanoid-v2"])
 def test_rollout_bf16_eight_wave_kernel_tracks_torch_engine(env_name):
     """The benchmarked bf16 rollout variant (rollout_kernel<bf16, 16 envs, 8 waves>) vs the torch

@@ -1,13 +1,14 @@
 """Host-side plan of the grouped wgrad launch (pytorch_dppo_amd/runtime/engine_hip.py
 wgrad_tiles): every layer's [fan_out][fan_in + 1] gradient is covered exactly once by tiles the
-kernel accepts (csrc/wgrad.hip: nq*kq <= 8 waves, nq + kq <= 6 fragment slots, tiles inside the
-128-row padded operand buffers).  CPU only — the kernel itself is checked against autograd in
+kernel accepts (csrc/wgrad.hip wgrad_task_ok: nq*kq <= 8 waves and nq + kq <= 6 fragment slots, or
+wide: two quadrants per wave, nq even, nq + kq <= 10; tiles inside the 128-row padded operand
+buffers).  CPU only — the kernel itself is checked against autograd in
 tests/test_gpu_kernels.py."""
 
 import pytest
 import torch
 
-from pytorch_dppo_amd.runtime.engine_hip import WT, wgrad_tiles
+from pytorch_dppo_amd.runtime.engine_hip import WT, wgrad_tile_ok, wgrad_tiles
 
 # (fan_out, fan_in) of the six layers for the reference envs' obs / act dims
 LAYERS = {
@@ -21,14 +22,19 @@ def _r(x, m):
     return -(-x // m) * m
 
 
+@pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("env", sorted(LAYERS))
-def test_tiles_cover_each_gradient_once(env):
+def test_tiles_cover_each_gradient_once(env, wide):
     for li, (n, fan_in) in enumerate(LAYERS[env]):
         k = fan_in + 1
         cover = torch.zeros(_r(n, 64), _r(k, 64), dtype=torch.int32)
-        for (tl, n0, k0, nq, kq) in wgrad_tiles(li, n, k):
+        for (tl, n0, k0, nq, kq) in wgrad_tiles(li, n, k, wide):
             assert tl == li
-            assert nq >= 1 and kq >= 1 and nq * kq <= 8 and nq + kq <= 6
+            assert wgrad_tile_ok(nq, kq, wide)
+            if nq * kq > 8:
+                assert wide and nq * kq <= 16 and nq % 2 == 0 and nq + kq <= 10
+            else:
+                assert nq + kq <= 6
             assert n0 % 64 == 0 and k0 % 64 == 0
             # operand buffers hold _r(rows, WT) rows (engine_hip: g_rows / x_rows)
             assert n0 + 64 * nq <= _r(n, WT) and k0 + 64 * kq <= _r(k, WT)
@@ -41,11 +47,16 @@ def test_humanoid_value_fc1_streams_fewer_rows_than_square_tiles():
     rows_per_step = sum(64 * (nq + kq) for (_, _, _, nq, kq) in tiles)
     square = (_r(500, 128) // 128) * (_r(377, 128) // 128) * 256   # 128x128 tiles
     assert rows_per_step == 2304 and rows_per_step < square
+    # two quadrants per wave: 4x3 tiles (two waves per 128 x 64 output rows)
+    wide = wgrad_tiles(3, 500, 377, True)
+    assert sorted((nq, kq) for (_, _, _, nq, kq) in wide) == [(4, 3)] * 4
+    assert sum(64 * (nq + kq) for (_, _, _, nq, kq) in wide) == 1792
 
 
-@pytest.mark.parametrize("heads,q8", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("heads,q8,wide", [(False, False, False), (True, False, False), (True, True, False),
+                                           (True, False, True)])
 @pytest.mark.parametrize("env", ["Humanoid-v2", "HalfCheetah-v2"])
-def test_plan_tasks_cover_tiles_and_batch_once(env, heads, q8):
+def test_plan_tasks_cover_tiles_and_batch_once(env, heads, q8, wide):
     """The full task list (HipEngine._build_wgrad_plan run on a CPU stand-in): each output tile's
     tasks cover the batch rows [0, ldT) exactly once with 64-row-aligned chunks, every task owns
     a disjoint slab region, the task count is ~one per CU, and every parameter's gather entry
@@ -59,7 +70,7 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads, q8):
     spec = get_spec(env)
     model = ActorCritic(spec.obs_dim, spec.act_dim)
     stub = SimpleNamespace(L=model.packed_layout(), ldT=65536, A=spec.act_dim, device=torch.device("cpu"),
-                           heads=heads, q8=q8, head_range=[model.head_ranges["policy"], model.head_ranges["value"]],
+                           heads=heads, q8=q8, wgrad_wide=wide, head_range=[model.head_ranges["policy"], model.head_ranges["value"]],
                            _slab_index=HipEngine._slab_index, _slab_runs=HipEngine._slab_runs)
     HipEngine._build_wgrad_plan(stub, model, target_wgs=256)
     total = 0
@@ -70,6 +81,7 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads, q8):
         used = torch.zeros(b["slab"].numel(), dtype=torch.int32)
         rows = {}
         for (li, n0, k0, m0, m1, off, nq, kq) in t:
+            assert wgrad_tile_ok(nq, kq, wide)
             al = 128 if q8 else 64
             assert m0 % al == 0 and (m1 - m0) % al == 0 and 0 <= m0 < m1 <= stub.ldT
             used[off:off + 64 * nq * 64 * kq] += 1
@@ -86,7 +98,7 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads, q8):
             o, n = model.offsets[name]
             slab_fed[o:o + n] = False
     meta = stub.src_meta
-    assert bool(((meta[slab_fed] >> 4) >= 1).all()) and bool(((meta[slab_fed] & 15) >= 1).all())
+    assert bool(((meta[slab_fed] >> 5) >= 1).all()) and bool(((meta[slab_fed] & 31) >= 1).all())
     assert bool((meta[~slab_fed] == 0).all())
     # the gathers' slab runs cover exactly the slab-fed elements of each bucket's range
     for b in stub.buckets:
