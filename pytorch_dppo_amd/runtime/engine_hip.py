@@ -298,8 +298,8 @@ class HipEngine:
         n_whole = min(4096, (n - self.A + 255) // 256 + self.A + 8)
         # (the fused gather + Adam launch takes one block per 32 reduce items first: with the fused
         # narrow / second-layer weight gradients there are tens of thousands of items)
-        # (blocks of 32 items, csrc/kernels.h ITEM_IPB; sized for 8 so an A/B build with smaller blocks fits)
-        n_whole = min(4096, max(n_whole, -(-len(self.items["joint"][0]) // 8) + (n + 255) // 256))
+        # (blocks of 32 items, csrc/kernels.h ITEM_IPB; blocks of 8 measured no faster, profiles/r6/ab_iter_phead_kb_vs_plain_ipb8_*.log)
+        n_whole = min(4096, max(n_whole, -(-len(self.items["joint"][0]) // 32) + (n + 255) // 256))
         # per-head regions (fixed: every head launch writes each block of its region): policy
         # [0, np_), value [np_, np_ + nv_)
         (plo, phi), (vlo, vhi) = self.head_range
