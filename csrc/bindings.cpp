@@ -842,7 +842,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("phead_train_applies", &phead_train_applies);
   m.def("set_phead", [](int64_t on) { set_phead((int)on); });
   m.def("head_rows", []() { return (int64_t)mlp_head_rows(); });
-  m.def("set_vhead", [](int64_t on) { set_vhead((int)on); });
   m.def("head_waves", [](int64_t h) { return (int64_t)mlp_head_waves((int)h); });
   m.def("set_head_kernels", [](bool on) { set_head_kernels(on ? 1 : 0); });
   m.def("head_kernels_enabled", []() { return head_kernels_enabled() != 0; });

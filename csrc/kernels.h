@@ -144,12 +144,6 @@ extern "C" void launch_mlp_head(int dt, int head, const MlpArgs& a, hipStream_t 
 extern "C" void launch_mlp_head_value(int dt, const MlpArgs& a, hipStream_t s);   // V(x) on the value head kernel
 extern "C" void set_head_kernels(int enable);
 extern "C" int head_kernels_enabled();
-// value head on 32x32x16 MFMAs, transposed chain (csrc/vhead.hip): 128 rows per workgroup
-extern "C" int vhead_applies(const MlpArgs& a);   // the forward (set_vhead flag and shapes)
-extern "C" int vhead_shape_ok(const MlpArgs& a);
-extern "C" int vhead_rows();
-extern "C" void launch_vhead_fwd(int dt, const MlpArgs& a, hipStream_t s);   // V(x): dt bf16x3 or bf16
-extern "C" void set_vhead(int enable);
 // policy head update on 32x32x16 MFMAs, transposed chain (csrc/phead.hip): 128 rows per workgroup
 extern "C" int phead_applies(const MlpArgs& a);   // set_phead flag and shapes
 extern "C" int phead_shape_ok(const MlpArgs& a);

@@ -627,12 +627,11 @@ void value_t(const MlpArgs& a, hipStream_t s);
 // 2.125 rounds, and the 32-workgroup third round costs as much as a full one.  Rows past the last
 // full round (when they are at most a quarter round) go to the 32-row tile kernel instead, whose
 // small workgroups spread over all CUs.
-// (the transposed-chain 32x32 value head, csrc/vhead.hip, takes the rows when it applies; the e4m3
-// fc1 of the fp8 mode stays on the head kernel)
+// (rounds 5-6 ran these rows on a 32x32 transposed-chain kernel, csrc/vhead.hip: at par in round 5,
+// 128 vs 116 us per values() call at bf16x3 in its round-6 one-wave-per-SIMD form; removed)
 template <int DT>
 void head_fwd(const MlpArgs& a, hipStream_t s) {
-  if (a.W8 == nullptr && vhead_applies(a)) launch_vhead_fwd(DT, a, s);
-  else launch_mlp_head_value(DT, a, s);
+  launch_mlp_head_value(DT, a, s);
 }
 
 template <int DT>

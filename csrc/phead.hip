@@ -2,7 +2,7 @@
 // forward, ppo.py:148-167 corrected loss, train.py:142-161 reference loss; the update of
 // train.py:162-170 / ppo.py:168-175 consumes its outputs).
 //
-// The value head's scheme (csrc/vhead.hip, helpers in csrc/t32.h) on the narrow policy network
+// The transposed chain (helpers in csrc/t32.h) on the narrow policy network
 // (d0 -> 100 -> 100 -> A): every layer computes out^T = W . in^T with A = a 32x16 weight fragment
 // from the LDS ring and B = the activations in registers (batch row on the lane); each wave owns
 // 32 rows and ALL 128 (padded) features of both hidden layers (4 accumulator tiles each).
@@ -143,7 +143,8 @@ __global__ __launch_bounds__(PH_WAVES * 64, 2) void phead_kernel(MlpArgs a) {
   // ---- DMA sources ----
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), (short)0, 0x7fffffff, 0x00020000);
   // per-lane byte offset of the lane's piece of a 32x16 A fragment in an FM image of c32 block
-  // columns (csrc/vhead.hip lane_off)
+  // columns: a 32x16 fragment is four 256-byte pieces of two 16x32 FM blocks (split: the DMA
+  // instruction d carries reader lanes 32 d .. 32 d + 31, its lanes >= 32 the lo halves)
   auto lane_off = [&](int c32, int d) __attribute__((always_inline)) -> unsigned {
     const int i = lane & 31;
     if constexpr (S3) return (unsigned)(((i >> 4) * c32 * 512 + ((i & 15) + 16 * d) * 8) * 4 + 16 * (lane >> 5));

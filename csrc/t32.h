@@ -1,4 +1,4 @@
-// Shared device helpers of the transposed-chain 32x32x16 MFMA kernels (csrc/vhead.hip, csrc/phead.hip).
+// Device helpers of the transposed-chain 32x32x16 MFMA kernel (csrc/phead.hip).
 //
 // In the transposed chain every layer computes out^T = W . in^T: A = a weight fragment (32 output
 // features x 16 k from an LDS ring), B = the activations (16 k x 32 batch rows, in registers).  The

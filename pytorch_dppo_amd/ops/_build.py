@@ -24,10 +24,9 @@ OUT_DIR = os.path.dirname(os.path.abspath(__file__))
 EXT_NAME = "_dppo_hip"
 ARCH = os.environ.get("DPPO_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-DEVICE_SRCS = ["rollout.hip", "mlp.hip", "mlp_head.hip", "vhead.hip", "phead.hip", "wgrad.hip", "optim.hip", "obs.hip"]
+DEVICE_SRCS = ["rollout.hip", "mlp.hip", "mlp_head.hip", "phead.hip", "wgrad.hip", "optim.hip", "obs.hip"]
 HOST_SRCS = ["bindings.cpp", "comm.cpp"]   # compiled with the torch include paths
 HEADERS = ["common.h", "mlp_core.h", "kernels.h", "t32.h"]
-AGPR_SRCS = {"vhead.hip"}   # built without -amdgpu-mfma-vgpr-form (AGPR accumulators)
 
 
 def ext_path(variant: str = "") -> str:
@@ -65,11 +64,8 @@ def _compile(src: str, cflags, verbose: bool, csrc: str = CSRC, extra=()) -> str
     # -amdgpu-mfma-vgpr-form: MFMA accumulators in ordinary VGPRs (gfx90a+ unified register
     # file).  With AGPR accumulators the allocator shuffled them through VGPRs every loop turn
     # (~1,600 v_accvgpr_* in mlp_train, 96 per wgrad k-step pair); with it those copies vanish.
-    base = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
-    # (not for the one-wave-per-SIMD value head, csrc/vhead.hip: its 256 fc1 accumulator registers
-    # per lane must live in AGPRs — VGPR-form MFMAs can address only 256 registers in all)
-    if src not in AGPR_SRCS:
-        base += ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+    base = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+            "-mllvm", "-amdgpu-mfma-vgpr-form"]
     # A/B builds of compile-time variants (e.g. DPPO_EXTRA_CFLAGS="-DDPPO_X_CACHED"); the
     # flags enter the object cache key, so switching back rebuilds nothing stale
     base += os.environ.get("DPPO_EXTRA_CFLAGS", "").split() + list(extra)

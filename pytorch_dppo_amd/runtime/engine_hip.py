@@ -175,7 +175,7 @@ class HipEngine:
         # operand bytes of the bf16 update's HBM round trip.  fp8_wgrad_operands=False: bf16 operands.
         self.q8 = self.fp8 and self.heads and bool(params.fp8_wgrad_operands)
         # (the value head's update stays on the 16x16 head kernel: its 32x32 one-wave-per-SIMD form
-        # measured slower at every step, docs/ARCHITECTURE.md §13; csrc/vhead.hip is V(x) only)
+        # measured slower at every step, docs/ARCHITECTURE.md §13)
         # the policy head's update on the transposed-chain kernel too (csrc/phead.hip): h1p / g1p /
         # g2p row-major, and the observation operand of p_fc1 AND v_fc1 row-major — x_buf itself
         # for a full-batch step (no x^T anywhere: the rollout skips writing it), the kernel's

@@ -6,7 +6,7 @@ OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT/pmc"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 rocprofv3 -L > "$OUT/pmc/counters_list.txt" 2>&1 || true
-REGEX=${REGEX:-'mlp_head|mlp_train|wgrad_kernel|rollout_kernel|mlp_value|gather_adam|vhead|phead'}
+REGEX=${REGEX:-'mlp_head|mlp_train|wgrad_kernel|rollout_kernel|mlp_value|gather_adam|phead'}
 i=0
 for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
          "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_INSTS_SALU" \

@@ -122,38 +122,6 @@ def test_value_forward_on_head_kernel_matches_tile_kernel(dtype, tol, E, T):
     assert (out[True] - out[False]).abs().max().item() < tol * scale
 
 
-@pytest.mark.parametrize("dtype,tol", [("bf16x3", 2e-5), ("bf16", 3e-2)])
-def test_vhead_forward_matches_torch_and_16x16_head(dtype, tol):
-    """values() on the transposed-chain 32x32 value head (csrc/vhead.hip: weights as the A operand,
-    batch rows on the lanes, no LDS transposes; the pair's two fc2 partials summed in LDS; fc3 on
-    the VALU in fp32) vs the 16x16 row-stationary head kernel (set_vhead(0)) and the fp32 torch
-    model, at 2048 x 16 + 2048 rows (one round of workgroups + the tail on the 32-row kernel)"""
-    E, T = 2048, 16
-    p = dppo_preset(device="gpu", env_name="Humanoid-v2", num_envs=E, exploration_size=E * T,
-                    batch_size=E * T, dtype=dtype)
-    eng, model, _, _ = _engine(p)
-    O, M = model.num_inputs, (T + 1) * E
-    xb = torch.zeros(M, eng.d0, device=DEV)
-    xb[:, :O] = torch.randn(M, O, device=DEV).clamp(-5, 5)
-    xb[:, O] = 1.0
-    eng.x_buf.copy_(eng.encode(xb))
-    out = {}
-    try:
-        for on in (1, 0):
-            eng.ext.set_vhead(on)
-            eng.values_buf.fill_(float("nan"))
-            eng.values()
-            out[on] = eng.values_buf.clone()
-    finally:
-        eng.ext.set_vhead(1)
-    with torch.no_grad():
-        _, _, v = model(eng.decode(eng.x_buf)[:, :O])
-    scale = v.abs().max().item()
-    assert torch.isfinite(out[1]).all()
-    assert (out[1] - v.reshape(-1)).abs().max().item() < tol * scale
-    assert (out[1] - out[0]).abs().max().item() < tol * scale
-
-
 @pytest.mark.parametrize("dtype", ["bf16x3", "bf16"])
 @pytest.mark.parametrize("loss,mb", [("ppo", None), ("ppo", 1024), ("ppo", 1000), ("dppo_ref", 768)])
 def test_phead_update_matches_16x16_head_update(dtype, loss, mb):
