@@ -115,3 +115,19 @@ def test_plan_tasks_cover_tiles_and_batch_once(env, heads, q8, wide):
         assert (b0["lo"], b0["hi"]) == (spec.act_dim, model.head_ranges["policy"][1]) and b0["partials"]
         assert (b1["lo"], b1["hi"]) == model.head_ranges["value"] and not b1["partials"]
     assert total >= 200
+
+
+def test_tile_rule_matches_the_kernel():
+    """The host plan's tile rule (wgrad_tile_ok) is the kernel's (csrc/wgrad.hip wgrad_task_ok, which
+    the launch binding enforces) for every dtype: fp32 / e4m3 one quadrant per wave only, split-bf16 /
+    bf16 also the two-quadrant tiles.  Needs the built extension (it loads on the CPU too)."""
+    from pytorch_dppo_amd.ops import native
+    try:
+        ext = native.load()
+    except Exception as e:  # noqa: BLE001 — not built in this checkout
+        pytest.skip(f"HIP extension not built: {e}")
+    for dt in (native.DT_CODE[d] for d in ("fp32", "bf16x3", "bf16", "fp8")):
+        wide = dt in (native.DT_CODE["bf16x3"], native.DT_CODE["bf16"])
+        for nq in range(0, 18):
+            for kq in range(0, 18):
+                assert bool(ext.wgrad_task_ok(dt, nq, kq)) == wgrad_tile_ok(nq, kq, wide), (dt, nq, kq)
