@@ -87,10 +87,11 @@ DEV typename Prec<DT>::Frag rm_frag_at(const char* st, const unsigned (&o)[4]) {
 // Tasks of up to 8 quadrants run one quadrant per wave (QW 1: 24 fragment slots per stage); split-bf16
 // and bf16 tasks of 9-16 quadrants (nq even) run TWO per wave (QW 2: 40 slots, nq + kq <= 10), the
 // wave's quadrants (wn, wk) and (wn + nq / 2, wk) sharing its X fragments — a wider tile streams fewer
-// operand rows per output (Humanoid v_fc1 as 4x4 + 4x2 quadrant tiles: 28 x 64 rows per k-step
-// instead of 36 x 64 with 4x2 tiles) and a wave reads 12 fragments per 32 MFMA tiles instead of 8
-// per 16.  The ring depth follows the stage size: split-bf16 3 stages of 24 slots or 2 of 40 (the
-// twice-longer stage covers the same latency), bf16 4 of either.
+// operand rows per output (Humanoid v_fc1 as four 4x3 quadrant tiles: 28 x 64 rows per k-step
+// instead of 36 x 64 with six 4x2 tiles) and a wave reads 12 fragments per 32 MFMA tiles instead of
+// 8 per 16.  The ring depth follows the stage size: split-bf16 3 stages of 24 slots or 2 of 40 (one
+// stage in flight: a 4x3 tile's 3-stage ring would need 168 KiB; the wait share grows, 0.46 -> 0.52
+// of the wave cycles, docs/ARCHITECTURE.md §13), bf16 4 of either.
 template <int DT, int QW>
 struct WgCfg {
   static constexpr int SLOTS = QW == 1 ? 24 : 40;
