@@ -110,6 +110,8 @@ class Params:
     wgrad_wide: bool = True              # wgrad tiles of up to 16 quadrants, two per wave (split-bf16 / bf16;
                                          # csrc/wgrad.hip)
     phead_kernel: bool = True            # the policy head on the 32x32 kernel (csrc/phead.hip)
+    phead_fused_dw2: str = "auto"        # auto | on | off: ... summing p_fc2's weight gradient in the kernel
+                                         # (auto: at bf16x3 only, the measured-faster choice per dtype)
     mlp_rows: int = 0                    # diagnostics: force the tile update kernel's row tile (0: auto)
 
     # ------------------------------------------------------------------------------------
@@ -131,6 +133,8 @@ class Params:
             raise ValueError(f"env_backend must be builtin|gym, got {self.env_backend}")
         if self.dtype not in ("fp32", "bf16x3", "bf16", "fp8"):
             raise ValueError(f"dtype must be fp32|bf16x3|bf16|fp8, got {self.dtype}")
+        if self.phead_fused_dw2 not in ("auto", "on", "off"):
+            raise ValueError(f"phead_fused_dw2 must be auto|on|off, got {self.phead_fused_dw2}")
         if self.loss not in ("ppo", "dppo_ref"):
             raise ValueError(f"loss must be ppo|dppo_ref, got {self.loss}")
         if self.value_loss not in ("mse", "clipped_half"):

@@ -185,7 +185,8 @@ class HipEngine:
         # ... summing p_fc2's weight gradient itself at bf16x3 (h1p / g2p never reach HBM: 4.26 ->
         # 4.15 ms per iteration); at bf16 their round trip is half the bytes and storing them for
         # the wgrad is faster (2.27 vs 2.36 ms; same box, profiles/r5/ab_p2_by_dtype.log)
-        self.phead_p2 = self.phead and self.dt == native.DT_CODE["bf16x3"]
+        fused = params.phead_fused_dw2
+        self.phead_p2 = self.phead and (fused == "on" or (fused == "auto" and self.dt == native.DT_CODE["bf16x3"]))
         # the gradient-amax ring: 3 slots x 4 tensors x 64 sub-slot lines of 32 dwords (csrc/kernels.h)
         self.q8_amax = torch.zeros(3 * 4 * Q8_SUB * 32, dtype=torch.int32, device=device)
         self._q8_next = 0          # step counter of the amax ring

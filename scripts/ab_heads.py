@@ -21,7 +21,8 @@ from pytorch_dppo_amd.runtime.launcher import free_port  # noqa: E402
 from pytorch_dppo_amd.runtime.worker import DPPOWorker  # noqa: E402
 
 # arm -> Params overrides: the 16x16 policy head, the default, the wgrad with one quadrant per wave
-ARMS = {"h16": {"phead_kernel": False}, "p32": {}, "narrow": {"wgrad_wide": False}}
+ARMS = {"h16": {"phead_kernel": False}, "p32": {}, "narrow": {"wgrad_wide": False},
+        "p2on": {"phead_fused_dw2": "on"}, "p2off": {"phead_fused_dw2": "off"}}
 
 
 def main():
